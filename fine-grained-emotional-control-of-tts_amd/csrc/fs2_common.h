@@ -1,0 +1,76 @@
+// Shared device helpers for the FastSpeech2 MI355X (gfx950) kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "fs2_hip.h"
+
+typedef __bf16 bf16;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
+
+#define FS2_WAVE 64
+
+__device__ __forceinline__ float to_f(float x) { return x; }
+__device__ __forceinline__ float to_f(bf16 x) { return (float)x; }
+template <typename T> __device__ __forceinline__ T from_f(float x);
+template <> __device__ __forceinline__ float from_f<float>(float x) { return x; }
+template <> __device__ __forceinline__ bf16 from_f<bf16>(float x) { return (bf16)x; }
+
+__device__ __forceinline__ float bf16_bits_to_f(unsigned short u) {
+  return __builtin_bit_cast(float, ((unsigned int)u) << 16);
+}
+
+// ---- wave reductions (64 lanes) ----
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ float wave_min(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// ---- counter-based dropout RNG: keep(seed, salt, index) ----
+// A stateless 32-bit mixer (murmur3 finaliser over a 64-bit counter); forward and
+// backward regenerate the same mask from (seed, salt, element index), so no mask
+// tensor is stored.
+__device__ __forceinline__ uint32_t fs2_mix32(uint32_t h) {
+  h ^= h >> 16; h *= 0x85ebca6bu; h ^= h >> 13; h *= 0xc2b2ae35u; h ^= h >> 16;
+  return h;
+}
+__device__ __forceinline__ bool fs2_keep(uint32_t seed, uint32_t salt, uint64_t idx, float p) {
+  if (p <= 0.f) return true;
+  uint32_t h = fs2_mix32((uint32_t)idx ^ fs2_mix32(seed ^ (salt * 0x9E3779B9u)));
+  h = fs2_mix32(h ^ (uint32_t)(idx >> 32) ^ 0x68bc21ebu);
+  // uniform in [0,1) with 24 bits
+  float u = (float)(h >> 8) * (1.0f / 16777216.0f);
+  return u >= p;
+}
+
+// reflect index into [0, T) (torch F.pad(mode="reflect") semantics, single bounce)
+__device__ __forceinline__ int reflect_idx(int i, int T) {
+  if (i < 0) i = -i;
+  if (i >= T) i = 2 * (T - 1) - i;
+  return i;
+}
+
+#define FS2_CHECK_LAUNCH()                         \
+  do {                                             \
+    hipError_t e__ = hipGetLastError();            \
+    if (e__ != hipSuccess) return (int)e__;        \
+  } while (0)

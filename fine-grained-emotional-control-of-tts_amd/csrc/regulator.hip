@@ -1,0 +1,558 @@
+// Token-axis data movement of the FastSpeech2 path: embedding + positional encoding,
+// key-padding masks, speaker/intensity concat, LengthRegulator, average_over_durations,
+// the pitch/energy embedding conv, predictor heads and small utilities.
+//
+// These are HBM-bound integer / gather / segment-reduction kernels (SURVEY K1-K3, K7,
+// K9-K11): coalesced row copies, no MFMA.
+#include "fs2_common.h"
+
+namespace {
+
+// ---------------------------------------------------------------- embedding (K1, K2)
+template <typename T>
+__global__ void embed_fwd_kernel(const int64_t* tok, const float* table, const float* pe, int pad,
+                                 int T_, int D, T* X, float* keep, long n) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const long m = i / D;
+  const int d = (int)(i - m * D);
+  const int t = (int)(m % T_);
+  const int64_t v = tok[m];
+  const float k = (v != pad) ? 1.f : 0.f;
+  X[i] = from_f<T>((table[v * D + d] + pe[(long)t * D + d]) * k);
+  if (d == 0) keep[m] = k;
+}
+
+// one block per vocabulary row; deterministic sequential accumulation over tokens
+template <typename T>
+__global__ void embed_bwd_kernel(const int64_t* tok, const T* dX, const float* keep, int M, int D,
+                                 float* dtable) {
+  const int v = blockIdx.x;
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    float s = 0.f;
+    for (int m = 0; m < M; ++m)
+      if (tok[m] == v) s += to_f(dX[(long)m * D + d]) * keep[m];
+    dtable[(long)v * D + d] += s;
+  }
+}
+
+__global__ void keypad_tokens_kernel(const int64_t* tok, int pad, int M, uint8_t* kp) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < M) kp[i] = tok[i] == pad;
+}
+
+__global__ void keypad_lengths_kernel(const int64_t* lens, int B, int T_, uint8_t* kp,
+                                      float* keep) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * T_) return;
+  const int b = i / T_, t = i - b * T_;
+  const bool valid = t < lens[b];
+  kp[i] = !valid;
+  if (keep) keep[i] = valid ? 1.f : 0.f;
+}
+
+// ---------------------------------------------------------------- concat (K7)
+template <typename T>
+__global__ void concat_fwd_kernel(const T* feats, const float* spk_table, const int64_t* spk,
+                                  const float* inten, int T_, int D, int E, T* cat, int ldc,
+                                  long n) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const long m = i / ldc;
+  const int c = (int)(i - m * ldc);
+  const int b = (int)(m / T_);
+  float v = 0.f;
+  if (c < D) v = to_f(feats[m * D + c]);
+  else if (c < 2 * D) v = spk_table[spk[b] * D + (c - D)];
+  else if (c < 2 * D + E) v = inten ? inten[m * E + (c - 2 * D)] : 0.f;
+  cat[i] = from_f<T>(v);
+}
+
+template <typename T>
+__global__ void concat_bwd_spk_kernel(const T* dcat, int ldc, const int64_t* spk, int B, int T_,
+                                      int D, float* dspk) {
+  const int s = blockIdx.x;
+  const int d = blockIdx.y * blockDim.x + threadIdx.x;
+  if (d >= D) return;
+  float acc = 0.f;
+  for (int b = 0; b < B; ++b) {
+    if (spk[b] != s) continue;
+    for (int t = 0; t < T_; ++t) acc += to_f(dcat[((long)b * T_ + t) * ldc + D + d]);
+  }
+  dspk[(long)s * D + d] += acc;
+}
+
+template <typename T>
+__global__ void mask_rows_kernel(T* X, long ldx, const float* keep, int M, int D) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)M * D) return;
+  const long m = i / D;
+  const int d = (int)(i - m * D);
+  T* p = X + m * ldx + d;
+  *p = from_f<T>(to_f(*p) * keep[m]);
+}
+
+// ---------------------------------------------------------------- predictor head
+template <typename T>
+__global__ void __launch_bounds__(256) rowdot_fwd_kernel(const T* u, long ldu, const float* w,
+                                                         const float* b, float scale, int M,
+                                                         int D, T* y) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  float s = 0.f;
+  for (int d = lane; d < D; d += 64) s += to_f(u[(long)row * ldu + d]) * w[d];
+  s = wave_sum(s);
+  if (lane == 0) y[row] = from_f<T>((s + b[0]) * scale);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) rowdot_bwd_kernel(const T* dy, const T* u, long ldu,
+                                                         const float* w, float scale, int M,
+                                                         int D, T* du, float* part,
+                                                         int rows_per_block) {
+  // part: [nb][D+1] partial sums of dy*scale*u and dy*scale
+  const int rbeg = blockIdx.x * rows_per_block, rend = min(M, rbeg + rows_per_block);
+  for (int d = threadIdx.x; d <= D; d += blockDim.x) {
+    float s = 0.f;
+    for (int m = rbeg; m < rend; ++m) {
+      const float g = to_f(dy[m]) * scale;
+      s += (d < D) ? g * to_f(u[(long)m * ldu + d]) : g;
+    }
+    part[(long)blockIdx.x * (D + 1) + d] = s;
+  }
+  for (long i = (long)rbeg * D + threadIdx.x; i < (long)rend * D; i += blockDim.x) {
+    const long m = i / D;
+    const int d = (int)(i - m * D);
+    du[m * D + d] = from_f<T>(to_f(dy[m]) * scale * w[d]);
+  }
+}
+
+__global__ void reduce_cols_kernel(const float* part, int nb, int N, float* out, float* out2,
+                                   int split) {
+  // out[n] += sum_b part[b][n] for n < split; out2[n - split] += ... for n >= split
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  float s = 0.f;
+  for (int b = 0; b < nb; ++b) s += part[(long)b * N + n];
+  if (n < split) out[n] += s;
+  else out2[n - split] += s;
+}
+
+// ---------------------------------------------------------------- average_over_durations (K9)
+// Replicates torch CPU semantics of SB average_over_durations (App. A.10): cumsum of the
+// values accumulated in double and stored as float, cumsum of (values != 0) as int64,
+// differences gathered at the duration cumsum ends/starts, float division.
+__global__ void avg_over_dur_kernel(const float* vals, int Tm, const int64_t* durs, int Tp,
+                                    float* avg, float* vcum, int* nzcum) {
+  const int b = blockIdx.x;
+  const float* v = vals + (long)b * Tm;
+  float* vc = vcum + (long)b * (Tm + 1);
+  int* nc = nzcum + (long)b * (Tm + 1);
+  if (threadIdx.x == 0) {
+    double acc = 0.0;
+    int cnt = 0;
+    vc[0] = 0.f; nc[0] = 0;
+    for (int t = 0; t < Tm; ++t) {
+      acc += (double)v[t];
+      cnt += (v[t] != 0.f);
+      vc[t + 1] = (float)acc;
+      nc[t + 1] = cnt;
+    }
+  }
+  __syncthreads();
+  // per-phoneme gather; the duration cumsum is recomputed by a block scan of d
+  __shared__ long long cs[1024 + 1];
+  if (threadIdx.x == 0) {
+    long long c = 0;
+    cs[0] = 0;
+    for (int p = 0; p < Tp; ++p) { c += durs[(long)b * Tp + p]; cs[p + 1] = c; }
+  }
+  __syncthreads();
+  for (int p = threadIdx.x; p < Tp; p += blockDim.x) {
+    long long s0 = cs[p], s1 = cs[p + 1];
+    s0 = s0 < 0 ? 0 : (s0 > Tm ? Tm : s0);
+    s1 = s1 < 0 ? 0 : (s1 > Tm ? Tm : s1);
+    const float sums = vc[s1] - vc[s0];
+    const float nel = (float)(nc[s1] - nc[s0]);
+    avg[(long)b * Tp + p] = (nel == 0.f) ? nel : sums / nel;
+  }
+}
+
+// ---------------------------------------------------------------- pitch/energy embed (K10)
+template <typename T>
+__global__ void embed1d_fwd_kernel(const T* base, const float* a, const float* W, const float* bias,
+                                   int T_, int D, int KW, T* out, long n) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const long m = i / D;
+  const int o = (int)(i - m * D);
+  const int b = (int)(m / T_), t = (int)(m - (long)b * T_);
+  const int P = (KW - 1) / 2;
+  float s = bias[o];
+  for (int j = 0; j < KW; ++j) s += W[o * KW + j] * a[(long)b * T_ + reflect_idx(t + j - P, T_)];
+  out[i] = from_f<T>(to_f(base[i]) + s);
+}
+
+template <typename T>
+__global__ void embed1d_bwd_kernel(const T* dout, const float* a, int M, int T_, int D, int KW,
+                                   int rows_per_block, float* part) {
+  // part: [nb][KW+1][D]
+  const int o = blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= D) return;
+  const int P = (KW - 1) / 2;
+  const int rbeg = blockIdx.y * rows_per_block, rend = min(M, rbeg + rows_per_block);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float ab = 0.f;
+  for (int m = rbeg; m < rend; ++m) {
+    const int b = m / T_, t = m - b * T_;
+    const float g = to_f(dout[(long)m * D + o]);
+    ab += g;
+    for (int j = 0; j < KW && j < 8; ++j) acc[j] += g * a[(long)b * T_ + reflect_idx(t + j - P, T_)];
+  }
+  float* pp = part + (long)blockIdx.y * (KW + 1) * D;
+  for (int j = 0; j < KW && j < 8; ++j) pp[(long)j * D + o] = acc[j];
+  pp[(long)KW * D + o] = ab;
+}
+
+__global__ void embed1d_reduce_kernel(const float* part, int nb, int D, int KW, float* dW,
+                                      float* dbias) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // i over (KW+1)*D
+  if (i >= (KW + 1) * D) return;
+  float s = 0.f;
+  for (int b = 0; b < nb; ++b) s += part[(long)b * (KW + 1) * D + i];
+  const int j = i / D, o = i - j * D;
+  if (j < KW) dW[o * KW + j] += s;
+  else dbias[o] += s;
+}
+
+// ---------------------------------------------------------------- LengthRegulator (K11)
+template <typename DT>
+__global__ void lr_index_kernel(const DT* durs, float pace, int Tp, int Tm, int64_t* mel_len,
+                                int32_t* cum, int32_t* frame_src) {
+  const int b = blockIdx.x;
+  __shared__ int32_t cs[1024];
+  if (threadIdx.x == 0) {
+    int64_t c = 0;
+    for (int p = 0; p < Tp; ++p) {
+      // torch: (pace * durs).long() -- float32 product, truncation toward zero
+      const float prod = pace * (float)durs[(long)b * Tp + p];
+      c += (int64_t)prod;
+      cs[p] = (int32_t)c;
+      cum[(long)b * Tp + p] = (int32_t)c;
+    }
+    mel_len[b] = c;
+  }
+  __syncthreads();
+  if (!frame_src) return;  // lengths-only pass (host learns T_mel before sizing buffers)
+  const int total = Tp > 0 ? cs[Tp - 1] : 0;
+  for (int t = threadIdx.x; t < Tm; t += blockDim.x) {
+    int src = -1;
+    if (t < total) {  // first p with cs[p] > t (binary search)
+      int lo = 0, hi = Tp - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (cs[mid] > t) hi = mid; else lo = mid + 1;
+      }
+      src = lo;
+    }
+    frame_src[(long)b * Tm + t] = src;
+  }
+}
+
+template <typename T>
+__global__ void lr_gather_kernel(const T* X, const int32_t* fsrc, const float* pe, int Tp, int Tm,
+                                 int D, T* Y, float* keep, long n) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const long m = i / D;
+  const int d = (int)(i - m * D);
+  const int b = (int)(m / Tm), t = (int)(m - (long)b * Tm);
+  const int src = fsrc[m];
+  float v = 0.f;
+  if (src >= 0) v = to_f(X[((long)b * Tp + src) * D + d]) + pe[(long)t * D + d];
+  Y[i] = from_f<T>(v);
+  if (d == 0 && keep) keep[m] = src >= 0 ? 1.f : 0.f;
+}
+
+template <typename T>
+__global__ void lr_scatter_kernel(const T* dY, const int32_t* cum, const float* keep, int Tp,
+                                  int Tm, int D, T* dX) {
+  const int bp = blockIdx.x;  // b*Tp + p
+  const int b = bp / Tp, p = bp - b * Tp;
+  int t0 = p > 0 ? cum[bp - 1] : 0, t1 = cum[bp];
+  t0 = min(t0, Tm); t1 = min(t1, Tm);
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    float s = 0.f;
+    for (int t = t0; t < t1; ++t) {
+      const long m = (long)b * Tm + t;
+      s += to_f(dY[m * D + d]) * keep[m];
+    }
+    dX[(long)bp * D + d] = from_f<T>(s);
+  }
+}
+
+// ---------------------------------------------------------------- utilities
+template <typename T>
+__global__ void fill_kernel(T* X, long n, float v) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) X[i] = from_f<T>(v);
+}
+template <typename T>
+__global__ void add_kernel(T* X, const T* Y, long n, float alpha) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) X[i] = from_f<T>(to_f(X[i]) + alpha * to_f(Y[i]));
+}
+template <typename S, typename D>
+__global__ void cast_kernel(const S* src, D* dst, long n) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = from_f<D>(to_f(src[i]));
+}
+
+inline unsigned nblk(long n, int bs = 256) { return (unsigned)((n + bs - 1) / bs); }
+
+}  // namespace
+
+#define DISPATCH_T(dtype, KERNEL_CALL_BF16, KERNEL_CALL_F32) \
+  do {                                                     \
+    if ((dtype) == FS2_BF16) { KERNEL_CALL_BF16; }          \
+    else if ((dtype) == FS2_F32) { KERNEL_CALL_F32; }       \
+    else return FS2_EINVAL;                                 \
+    FS2_CHECK_LAUNCH();                                     \
+  } while (0)
+
+extern "C" int fs2_embed_fwd(const int64_t* tokens, const float* table, const float* pe,
+                             int pad_idx, int B, int T, int D, void* X, float* keep, int dtype,
+                             void* stream) {
+  const long n = (long)B * T * D;
+  if (n == 0) return 0;
+  if (!tokens || !table || !pe || !X || !keep) return FS2_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  DISPATCH_T(dtype,
+    hipLaunchKernelGGL(embed_fwd_kernel<bf16>, dim3(nblk(n)), dim3(256), 0, s, tokens, table, pe, pad_idx, T, D, (bf16*)X, keep, n),
+    hipLaunchKernelGGL(embed_fwd_kernel<float>, dim3(nblk(n)), dim3(256), 0, s, tokens, table, pe, pad_idx, T, D, (float*)X, keep, n));
+  return 0;
+}
+
+extern "C" int fs2_embed_bwd(const int64_t* tokens, const void* dX, const float* keep, int M,
+                             int D, int V, float* dtable, int dtype, void* stream) {
+  if (M == 0 || V == 0) return 0;
+  if (!tokens || !dX || !keep || !dtable) return FS2_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  DISPATCH_T(dtype,
+    hipLaunchKernelGGL(embed_bwd_kernel<bf16>, dim3(V), dim3(128), 0, s, tokens, (const bf16*)dX, keep, M, D, dtable),
+    hipLaunchKernelGGL(embed_bwd_kernel<float>, dim3(V), dim3(128), 0, s, tokens, (const float*)dX, keep, M, D, dtable));
+  return 0;
+}
+
+extern "C" int fs2_keypad_from_tokens(const int64_t* tokens, int pad_idx, int M, uint8_t* key_pad,
+                                      void* stream) {
+  if (M == 0) return 0;
+  if (!tokens || !key_pad) return FS2_EINVAL;
+  hipLaunchKernelGGL(keypad_tokens_kernel, dim3(nblk(M)), dim3(256), 0, (hipStream_t)stream,
+                     tokens, pad_idx, M, key_pad);
+  FS2_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int fs2_keypad_from_lengths(const int64_t* lens, int B, int T, uint8_t* key_pad,
+                                       float* keep, void* stream) {
+  if (B * T == 0) return 0;
+  if (!lens || !key_pad) return FS2_EINVAL;
+  hipLaunchKernelGGL(keypad_lengths_kernel, dim3(nblk((long)B * T)), dim3(256), 0,
+                     (hipStream_t)stream, lens, B, T, key_pad, keep);
+  FS2_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int fs2_concat_fwd(const void* feats, const float* spk_table, const int64_t* spk,
+                              const float* intensity, int B, int T, int D, int E, void* cat,
+                              int ldc, int dtype, void* stream) {
+  const long n = (long)B * T * ldc;
+  if (n == 0) return 0;
+  if (!feats || !spk_table || !spk || !cat || ldc < 2 * D + E) return FS2_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  DISPATCH_T(dtype,
+    hipLaunchKernelGGL(concat_fwd_kernel<bf16>, dim3(nblk(n)), dim3(256), 0, s, (const bf16*)feats, spk_table, spk, intensity, T, D, E, (bf16*)cat, ldc, n),
+    hipLaunchKernelGGL(concat_fwd_kernel<float>, dim3(nblk(n)), dim3(256), 0, s, (const float*)feats, spk_table, spk, intensity, T, D, E, (float*)cat, ldc, n));
+  return 0;
+}
+
+extern "C" int fs2_concat_bwd_spk(const void* dcat, int ldc, const int64_t* spk, int B, int T,
+                                  int D, int n_spk, float* dspk, int dtype, void* stream) {
+  if (n_spk == 0 || D == 0) return 0;
+  if (!dcat || !spk || !dspk) return FS2_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid(n_spk, (D + 255) / 256);
+  DISPATCH_T(dtype,
+    hipLaunchKernelGGL(concat_bwd_spk_kernel<bf16>, grid, dim3(256), 0, s, (const bf16*)dcat, ldc, spk, B, T, D, dspk),
+    hipLaunchKernelGGL(concat_bwd_spk_kernel<float>, grid, dim3(256), 0, s, (const float*)dcat, ldc, spk, B, T, D, dspk));
+  return 0;
+}
+
+extern "C" int fs2_mask_rows(void* X, int64_t ldx, const float* keep, int M, int D, int dtype,
+                             void* stream) {
+  const long n = (long)M * D;
+  if (n == 0) return 0;
+  if (!X || !keep) return FS2_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  DISPATCH_T(dtype,
+    hipLaunchKernelGGL(mask_rows_kernel<bf16>, dim3(nblk(n)), dim3(256), 0, s, (bf16*)X, ldx, keep, M, D),
+    hipLaunchKernelGGL(mask_rows_kernel<float>, dim3(nblk(n)), dim3(256), 0, s, (float*)X, ldx, keep, M, D));
+  return 0;
+}
+
+extern "C" int fs2_rowdot_fwd(const void* u, int64_t ldu, const float* w, const float* b,
+                              float scale, int M, int D, void* y, int dtype, void* stream) {
+  if (M == 0) return 0;
+  if (!u || !w || !b || !y) return FS2_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid((M + 3) / 4);
+  DISPATCH_T(dtype,
+    hipLaunchKernelGGL(rowdot_fwd_kernel<bf16>, grid, dim3(256), 0, s, (const bf16*)u, ldu, w, b, scale, M, D, (bf16*)y),
+    hipLaunchKernelGGL(rowdot_fwd_kernel<float>, grid, dim3(256), 0, s, (const float*)u, ldu, w, b, scale, M, D, (float*)y));
+  return 0;
+}
+
+extern "C" int fs2_rowdot_bwd(const void* dy, const void* u, int64_t ldu, const float* w,
+                              float scale, int M, int D, void* du, float* dw, float* db,
+                              int dtype, float* workspace, void* stream) {
+  if (M == 0) return 0;
+  if (!dy || !u || !w || !du || !dw || !db || !workspace) return FS2_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  const int nb = min(256, max(1, (M + 31) / 32));
+  const int rpb = (M + nb - 1) / nb;
+  DISPATCH_T(dtype,
+    hipLaunchKernelGGL(rowdot_bwd_kernel<bf16>, dim3(nb), dim3(256), 0, s, (const bf16*)dy, (const bf16*)u, ldu, w, scale, M, D, (bf16*)du, workspace, rpb),
+    hipLaunchKernelGGL(rowdot_bwd_kernel<float>, dim3(nb), dim3(256), 0, s, (const float*)dy, (const float*)u, ldu, w, scale, M, D, (float*)du, workspace, rpb));
+  hipLaunchKernelGGL(reduce_cols_kernel, dim3(nblk(D + 1)), dim3(256), 0, s, workspace, nb, D + 1,
+                     dw, db, D);
+  FS2_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int64_t fs2_avg_workspace_floats(int B, int Tm_in) { return 2L * B * (Tm_in + 1); }
+
+extern "C" int fs2_avg_over_durations(const float* values, int Tm_in, const int64_t* durs, int B,
+                                      int Tp, float* avg, float* workspace, void* stream) {
+  if (B == 0 || Tp == 0) return 0;
+  if (!values || !durs || !avg || !workspace || Tp > 1024) return FS2_EINVAL;
+  float* vcum = workspace;
+  int* nzc = (int*)(workspace + (long)B * (Tm_in + 1));
+  hipLaunchKernelGGL(avg_over_dur_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, values,
+                     Tm_in, durs, Tp, avg, vcum, nzc);
+  FS2_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int fs2_embed1d_fwd(const void* base, const float* a, const float* W,
+                               const float* bias, int B, int T, int D, int KW, void* out,
+                               int dtype, void* stream) {
+  const long n = (long)B * T * D;
+  if (n == 0) return 0;
+  if (!base || !a || !W || !bias || !out || KW > 8 || (KW - 1) / 2 >= T) return FS2_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  DISPATCH_T(dtype,
+    hipLaunchKernelGGL(embed1d_fwd_kernel<bf16>, dim3(nblk(n)), dim3(256), 0, s, (const bf16*)base, a, W, bias, T, D, KW, (bf16*)out, n),
+    hipLaunchKernelGGL(embed1d_fwd_kernel<float>, dim3(nblk(n)), dim3(256), 0, s, (const float*)base, a, W, bias, T, D, KW, (float*)out, n));
+  return 0;
+}
+
+extern "C" int fs2_embed1d_bwd(const void* dout, const float* a, int B, int T, int D, int KW,
+                               float* dW, float* dbias, int dtype, float* workspace,
+                               void* stream) {
+  const int M = B * T;
+  if (M == 0) return 0;
+  if (!dout || !a || !dW || !dbias || !workspace || KW > 8) return FS2_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  const int nb = min(128, max(1, (M + 63) / 64));
+  const int rpb = (M + nb - 1) / nb;
+  dim3 grid((D + 255) / 256, nb);
+  DISPATCH_T(dtype,
+    hipLaunchKernelGGL(embed1d_bwd_kernel<bf16>, grid, dim3(256), 0, s, (const bf16*)dout, a, M, T, D, KW, rpb, workspace),
+    hipLaunchKernelGGL(embed1d_bwd_kernel<float>, grid, dim3(256), 0, s, (const float*)dout, a, M, T, D, KW, rpb, workspace));
+  hipLaunchKernelGGL(embed1d_reduce_kernel, dim3(nblk((long)(KW + 1) * D)), dim3(256), 0, s,
+                     workspace, nb, D, KW, dW, dbias);
+  FS2_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int fs2_lr_index(const void* durs, int d_is_float, float pace, int B, int Tp, int Tm,
+                            int64_t* mel_len, int32_t* cum, int32_t* frame_src, void* stream) {
+  if (B == 0) return 0;
+  if (!durs || !mel_len || !cum || Tp > 1024 || Tp <= 0) return FS2_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  if (d_is_float)
+    hipLaunchKernelGGL(lr_index_kernel<float>, dim3(B), dim3(256), 0, s, (const float*)durs, pace,
+                       Tp, Tm, mel_len, cum, frame_src);
+  else
+    hipLaunchKernelGGL(lr_index_kernel<int64_t>, dim3(B), dim3(256), 0, s, (const int64_t*)durs,
+                       pace, Tp, Tm, mel_len, cum, frame_src);
+  FS2_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int fs2_lr_gather(const void* X, const int32_t* frame_src, const float* pe, int B,
+                             int Tp, int Tm, int D, void* Y, float* keep, int dtype,
+                             void* stream) {
+  const long n = (long)B * Tm * D;
+  if (n == 0) return 0;
+  if (!X || !frame_src || !pe || !Y) return FS2_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  DISPATCH_T(dtype,
+    hipLaunchKernelGGL(lr_gather_kernel<bf16>, dim3(nblk(n)), dim3(256), 0, s, (const bf16*)X, frame_src, pe, Tp, Tm, D, (bf16*)Y, keep, n),
+    hipLaunchKernelGGL(lr_gather_kernel<float>, dim3(nblk(n)), dim3(256), 0, s, (const float*)X, frame_src, pe, Tp, Tm, D, (float*)Y, keep, n));
+  return 0;
+}
+
+extern "C" int fs2_lr_scatter(const void* dY, const int32_t* cum, const float* keep, int B,
+                              int Tp, int Tm, int D, void* dX, int dtype, void* stream) {
+  if ((long)B * Tp == 0) return 0;
+  if (!dY || !cum || !keep || !dX) return FS2_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  DISPATCH_T(dtype,
+    hipLaunchKernelGGL(lr_scatter_kernel<bf16>, dim3(B * Tp), dim3(128), 0, s, (const bf16*)dY, cum, keep, Tp, Tm, D, (bf16*)dX),
+    hipLaunchKernelGGL(lr_scatter_kernel<float>, dim3(B * Tp), dim3(128), 0, s, (const float*)dY, cum, keep, Tp, Tm, D, (float*)dX));
+  return 0;
+}
+
+extern "C" int fs2_fill(void* X, int64_t n, float value, int dtype, void* stream) {
+  if (n == 0) return 0;
+  if (!X) return FS2_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  DISPATCH_T(dtype,
+    hipLaunchKernelGGL(fill_kernel<bf16>, dim3(nblk(n)), dim3(256), 0, s, (bf16*)X, (long)n, value),
+    hipLaunchKernelGGL(fill_kernel<float>, dim3(nblk(n)), dim3(256), 0, s, (float*)X, (long)n, value));
+  return 0;
+}
+
+extern "C" int fs2_add(void* X, const void* Y, int64_t n, float alpha, int dtype, void* stream) {
+  if (n == 0) return 0;
+  if (!X || !Y) return FS2_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  DISPATCH_T(dtype,
+    hipLaunchKernelGGL(add_kernel<bf16>, dim3(nblk(n)), dim3(256), 0, s, (bf16*)X, (const bf16*)Y, (long)n, alpha),
+    hipLaunchKernelGGL(add_kernel<float>, dim3(nblk(n)), dim3(256), 0, s, (float*)X, (const float*)Y, (long)n, alpha));
+  return 0;
+}
+
+extern "C" int fs2_cast(const void* src, int src_dtype, void* dst, int dst_dtype, int64_t n,
+                        void* stream) {
+  if (n == 0) return 0;
+  if (!src || !dst) return FS2_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 g(nblk(n)), b(256);
+  if (src_dtype == FS2_F32 && dst_dtype == FS2_BF16)
+    hipLaunchKernelGGL((cast_kernel<float, bf16>), g, b, 0, s, (const float*)src, (bf16*)dst, (long)n);
+  else if (src_dtype == FS2_BF16 && dst_dtype == FS2_F32)
+    hipLaunchKernelGGL((cast_kernel<bf16, float>), g, b, 0, s, (const bf16*)src, (float*)dst, (long)n);
+  else if (src_dtype == FS2_F32 && dst_dtype == FS2_F32)
+    hipLaunchKernelGGL((cast_kernel<float, float>), g, b, 0, s, (const float*)src, (float*)dst, (long)n);
+  else if (src_dtype == FS2_BF16 && dst_dtype == FS2_BF16)
+    hipLaunchKernelGGL((cast_kernel<bf16, bf16>), g, b, 0, s, (const bf16*)src, (bf16*)dst, (long)n);
+  else return FS2_EINVAL;
+  FS2_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" const char* fs2_version(void) { return "fs2_hip 0.1 gfx950"; }

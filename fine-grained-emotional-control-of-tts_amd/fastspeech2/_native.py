@@ -1,0 +1,166 @@
+"""ctypes binding of the C ABI in ``include/fs2_hip.h`` (libfs2_hip.so, gfx950).
+
+This is the ONLY way the product path reaches compute: there is no CPU fallback and
+no torch-op fallback.  If the shared library is missing or a symbol is absent the import
+fails loudly (``NativeLibraryError``) -- on a GPU box that means "run build()", never
+"silently use something else".
+"""
+
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("FS2_HIP_LIB", os.path.join(_HERE, "libfs2_hip.so"))
+
+F32 = 0
+BF16 = 1
+
+
+class NativeLibraryError(RuntimeError):
+    pass
+
+
+class GemmDesc(ctypes.Structure):
+    _fields_ = [
+        ("M", ctypes.c_int), ("N", ctypes.c_int), ("K", ctypes.c_int), ("kvalid", ctypes.c_int),
+        ("mvalid", ctypes.c_int), ("nvalid", ctypes.c_int), ("dtype", ctypes.c_int),
+        ("A", ctypes.c_void_p), ("lda", ctypes.c_int64), ("a_kmajor", ctypes.c_int),
+        ("B", ctypes.c_void_p), ("ldb", ctypes.c_int64), ("b_kmajor", ctypes.c_int),
+        ("conv_mode", ctypes.c_int), ("conv_t", ctypes.c_int), ("conv_kw", ctypes.c_int),
+        ("conv_c", ctypes.c_int),
+        ("C", ctypes.c_void_p), ("ldc", ctypes.c_int64), ("c_fp32", ctypes.c_int),
+        ("c_conv_kw", ctypes.c_int),
+        ("bias", ctypes.c_void_p), ("relu", ctypes.c_int),
+        ("gate", ctypes.c_void_p), ("ldg", ctypes.c_int64),
+        ("row_scale", ctypes.c_void_p),
+        ("residual", ctypes.c_void_p), ("ldr", ctypes.c_int64),
+        ("row_scale_post", ctypes.c_void_p),
+        ("accumulate", ctypes.c_int), ("split_k", ctypes.c_int),
+        ("batch", ctypes.c_int), ("batch_div", ctypes.c_int),
+        ("sA1", ctypes.c_int64), ("sA2", ctypes.c_int64), ("sB1", ctypes.c_int64),
+        ("sB2", ctypes.c_int64), ("sC1", ctypes.c_int64), ("sC2", ctypes.c_int64),
+        ("sR1", ctypes.c_int64), ("sR2", ctypes.c_int64),
+    ]
+
+
+class LossDesc(ctypes.Structure):
+    _fields_ = [
+        ("B", ctypes.c_int), ("Tm", ctypes.c_int), ("Tp", ctypes.c_int), ("NM", ctypes.c_int),
+        ("dtype", ctypes.c_int),
+        ("mel_out", ctypes.c_void_p), ("postnet_out", ctypes.c_void_p),
+        ("log_dur", ctypes.c_void_p), ("pitch_pred", ctypes.c_void_p),
+        ("energy_pred", ctypes.c_void_p),
+        ("mel_tgt", ctypes.c_void_p), ("dur_tgt", ctypes.c_void_p),
+        ("pitch_avg", ctypes.c_void_p), ("energy_avg", ctypes.c_void_p),
+        ("mel_len", ctypes.c_void_p), ("phon_len", ctypes.c_void_p),
+        ("w_ssim", ctypes.c_float), ("w_mel", ctypes.c_float), ("w_post", ctypes.c_float),
+        ("w_dur", ctypes.c_float), ("w_pitch", ctypes.c_float), ("w_energy", ctypes.c_float),
+        ("loss_out", ctypes.c_void_p),
+        ("d_mel_out", ctypes.c_void_p), ("d_postnet_out", ctypes.c_void_p),
+        ("d_log_dur", ctypes.c_void_p), ("d_pitch", ctypes.c_void_p), ("d_energy", ctypes.c_void_p),
+        ("workspace", ctypes.c_void_p),
+    ]
+
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+I64 = ctypes.c_int64
+U32 = ctypes.c_uint32
+Fl = ctypes.c_float
+
+# name -> (restype, argtypes); must match include/fs2_hip.h exactly
+SIGNATURES = {
+    "fs2_gemm": (I, [ctypes.POINTER(GemmDesc), P]),
+    "fs2_colsum": (I, [P, I64, I, I, I, P, I, P, P]),
+    "fs2_colsum_workspace_floats": (I64, [I, I]),
+    "fs2_ln_fwd": (I, [P, I64, P, I64, Fl, U32, P, P, P, Fl, I, Fl, U32, P, P, I64, P, I64, P, P,
+                       I, I, I, U32, P]),
+    "fs2_ln_bwd": (I, [P, I64, P, I64, P, P, P, P, I, Fl, U32, P, I, P, I64, P, Fl, U32, P, P, I,
+                       I, I, U32, P, P]),
+    "fs2_ln_workspace_floats": (I64, [I, I]),
+    "fs2_softmax_fwd": (I, [P, P, I, I, I, I, I, Fl, Fl, U32, U32, P, P, I, P]),
+    "fs2_softmax_bwd": (I, [P, P, I, I, I, I, I, Fl, Fl, U32, U32, P, I, P]),
+    "fs2_embed_fwd": (I, [P, P, P, I, I, I, I, P, P, I, P]),
+    "fs2_embed_bwd": (I, [P, P, P, I, I, I, P, I, P]),
+    "fs2_keypad_from_tokens": (I, [P, I, I, P, P]),
+    "fs2_keypad_from_lengths": (I, [P, I, I, P, P, P]),
+    "fs2_concat_fwd": (I, [P, P, P, P, I, I, I, I, P, I, I, P]),
+    "fs2_concat_bwd_spk": (I, [P, I, P, I, I, I, I, P, I, P]),
+    "fs2_mask_rows": (I, [P, I64, P, I, I, I, P]),
+    "fs2_rowdot_fwd": (I, [P, I64, P, P, Fl, I, I, P, I, P]),
+    "fs2_rowdot_bwd": (I, [P, P, I64, P, Fl, I, I, P, P, P, I, P, P]),
+    "fs2_avg_over_durations": (I, [P, I, P, I, I, P, P, P]),
+    "fs2_avg_workspace_floats": (I64, [I, I]),
+    "fs2_embed1d_fwd": (I, [P, P, P, P, I, I, I, I, P, I, P]),
+    "fs2_embed1d_bwd": (I, [P, P, I, I, I, I, P, P, I, P, P]),
+    "fs2_lr_index": (I, [P, I, Fl, I, I, I, P, P, P, P]),
+    "fs2_lr_gather": (I, [P, P, P, I, I, I, I, P, P, I, P]),
+    "fs2_lr_scatter": (I, [P, P, P, I, I, I, I, P, I, P]),
+    "fs2_loss_fwd_bwd": (I, [ctypes.POINTER(LossDesc), P]),
+    "fs2_loss_workspace_floats": (I64, [I, I, I]),
+    "fs2_adamw": (I, [P, P, P, P, I64, Fl, Fl, Fl, Fl, Fl, Fl, Fl, Fl, P]),
+    "fs2_weight_prep": (I, [P, I, I, I, P, I, P, I, I, P]),
+    "fs2_fill": (I, [P, I64, Fl, I, P]),
+    "fs2_add": (I, [P, P, I64, Fl, I, P]),
+    "fs2_cast": (I, [P, I, P, I, I64, P]),
+    "fs2_version": (ctypes.c_char_p, []),
+}
+
+_lib = None
+
+
+def load(path=None):
+    """Load libfs2_hip.so and bind every symbol of include/fs2_hip.h (fail loudly)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise NativeLibraryError(
+            f"libfs2_hip.so not found at {p}: build it with `python -c 'import __graft_entry__ as g; "
+            f"g.build()'` (hipcc --offload-arch=gfx950). There is no fallback path.")
+    lib = ctypes.CDLL(p, mode=ctypes.RTLD_GLOBAL)
+    missing = []
+    for name, (res, args) in SIGNATURES.items():
+        try:
+            fn = getattr(lib, name)
+        except AttributeError:
+            missing.append(name)
+            continue
+        fn.restype = res
+        fn.argtypes = args
+    if missing:
+        raise NativeLibraryError(f"libfs2_hip.so is missing symbols: {missing}")
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def lib():
+    return load()
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_ptr():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def check(rc, name):
+    if rc != 0:
+        raise RuntimeError(f"{name} failed with code {rc}")
+
+
+def dtype_code(dt):
+    if dt == torch.float32:
+        return F32
+    if dt == torch.bfloat16:
+        return BF16
+    raise ValueError(f"unsupported activation dtype {dt}")

@@ -1,0 +1,614 @@
+"""Explicit forward / backward of the FastSpeech2-with-emotion-intensity train step on the
+MI355X kernels of libfs2_hip.so.
+
+The reference runs ``FastSpeech2.forward`` (emo_rank_tts/fastspeech2/model.py:279-441) through
+speechbrain lobes and lets autograd derive the backward.  Here the whole step is written out
+by hand so that every byte of activation traffic is known: each GEMM-shaped op goes through
+``fs2_gemm`` (implicit reflect-padded convolution, fused bias/ReLU/mask/residual epilogues),
+LayerNorms fuse their residual add + dropout, attention masks reproduce the head-major
+tiling quirk, and parameter gradients are written straight into one flat fp32 buffer
+(``model._gflat``) laid out in backward-completion order, ready for a bucketed all-reduce.
+
+Activation storage dtype is fp32 (parity mode) or bf16 (throughput mode); parameters,
+gradients, LayerNorm statistics and losses are fp32 in both.
+"""
+
+import math
+
+import torch
+
+from . import _native as N
+from . import ops
+from .ops import round_up
+
+_BK = {N.F32: 32, N.BF16: 64}
+
+
+class _Salt:
+    def __init__(self):
+        self.n = 0
+
+    def __call__(self):
+        self.n += 1
+        return self.n
+
+
+class FS2Engine:
+    def __init__(self, model, act_dtype=torch.float32):
+        self.m = model
+        self.cfg = model.cfg
+        self.adt = act_dtype
+        self.dt = N.dtype_code(act_dtype)
+        self.epc = ops.EPC[self.dt]
+        N.load()
+        model._ensure_packed()
+        self.dev = model._flat.device
+        self.params = dict(model.named_parameters())
+        self.grads = model._grad_views
+        self.pe_enc = model.sinusoidal_positional_embed_encoder.pe[0].float().contiguous()
+        self.pe_dec = model.sinusoidal_positional_embed_decoder.pe[0].float().contiguous()
+        self._ws = torch.empty(1 << 20, dtype=torch.float32, device=self.dev)
+        self.w = {}
+        self._wspecs = self._weight_specs()
+        self._prepared_version = None
+        self.on_grads_ready = None   # optional callback(param_names_done) for DP overlap
+
+    # ------------------------------------------------------------------ helpers
+    def ws(self, n):
+        n = int(n)
+        if self._ws.numel() < n:
+            self._ws = torch.empty(int(n * 1.25) + 1024, dtype=torch.float32, device=self.dev)
+        return self._ws
+
+    def empty(self, *shape, dtype=None):
+        return torch.empty(*shape, dtype=dtype or self.adt, device=self.dev)
+
+    def _weight_specs(self):
+        """name -> (O, C, KW, ldf, ldb_rows) for every GEMM weight."""
+        c = self.cfg
+        D = c.enc_d_model
+        specs = {}
+        for stack, L, F in (("encoder", c.enc_num_layers, c.enc_ffn_dim),
+                            ("decoder", c.dec_num_layers, c.dec_ffn_dim)):
+            k0, k1 = c.ffn_cnn_kernel_size_list
+            for i in range(L):
+                p = f"{stack}.layers.{i}."
+                specs[p + "self_att.att.in_proj_weight"] = (3 * D, D, 1)
+                specs[p + "self_att.att.out_proj.weight"] = (D, D, 1)
+                specs[p + "pos_ffn.0.conv.weight"] = (F, D, k0)
+                specs[p + "pos_ffn.2.conv.weight"] = (D, F, k1)
+        specs["concat_proj.w.weight"] = (D, 2 * D + 5, 1)
+        for pred in ("durPred", "pitchPred", "energyPred"):
+            k = c.dur_pred_kernel_size
+            specs[f"{pred}.conv1.conv.weight"] = (D, D, k)
+            specs[f"{pred}.conv2.conv.weight"] = (D, D, k)
+        specs["linear.w.weight"] = (c.n_mels, D, 1)
+        E, KP = c.postnet_embedding_dim, c.postnet_kernel_size
+        specs["postnet.conv_pre.conv.weight"] = (E, c.n_mels, KP)
+        for i in range(c.postnet_n_convolutions - 2):
+            specs[f"postnet.convs_intermedite.{i}.conv.weight"] = (E, E, KP)
+        specs["postnet.conv_post.conv.weight"] = (c.n_mels, E, KP)
+        return specs
+
+    def prepare_weights(self, force=False):
+        """fp32 master weights -> K-major GEMM images in the activation dtype (fwd + dgrad)."""
+        ver = (self.m._param_version, self.m._flat._version)
+        if not force and self._prepared_version == ver:
+            return
+        for name, (O, C, KW) in self._wspecs.items():
+            ldf = round_up(KW * C, self.epc)
+            ldb = KW * O
+            if name not in self.w:
+                self.w[name] = (self.empty(O, ldf), self.empty(C, ldb))
+            Wf, Wb = self.w[name]
+            ops.weight_prep(self.params[name], O, C, KW, Wf, ldf, Wb, ldb, dt=self.dt)
+        self._prepared_version = ver
+
+    def _fwd(self, X, ldx, M, T, wname, out, ldo, **epi):
+        O, C, KW = self._wspecs[wname]
+        Wf, _ = self.w[wname]
+        K = Wf.shape[1]
+        conv = (1, T, KW, C) if KW > 1 else None
+        ops.gemm(M, O, K, X, ldx, Wf, K, out, ldo, dt=self.dt, conv=conv, **epi)
+
+    def _dgrad(self, dY, lddy, M, T, wname, out, ldo, n_out=None, **epi):
+        O, C, KW = self._wspecs[wname]
+        _, Wb = self.w[wname]
+        conv = (2, T, KW, O) if KW > 1 else None
+        ops.gemm(M, n_out or C, KW * O, dY, lddy, Wb, KW * O, out, ldo, dt=self.dt, conv=conv,
+                 **epi)
+
+    def _wgrad(self, dY, lddy, X, ldx, M, T, wname, n_cols=None):
+        """grad[O][C][KW] += sum_m dY[m][o] * X[reflect(t+j-P)][c]   (fp32, accumulate)."""
+        O, C, KW = self._wspecs[wname]
+        Ncols = n_cols or KW * C
+        K = round_up(M, self.epc)
+        tiles = -(-O // 128) * -(-Ncols // 128)
+        split = 1
+        if tiles < 256:
+            split = max(1, min(-(-512 // tiles), K // (_BK[self.dt] * 4)))
+        conv = (3, T, KW, C) if KW > 1 else None
+        ops.gemm(O, Ncols, K, dY, lddy, X, ldx, self.grads[wname], C * KW, dt=self.dt, a_kmajor=0,
+                 b_kmajor=0, conv=conv, c_fp32=1, c_conv_kw=KW if KW > 1 else 0, kvalid=M,
+                 nvalid=KW * C, accumulate=1, split_k=split)
+
+    def _bias_grad(self, dY, lddy, M, n, gname):
+        ops.colsum(dY, lddy, M, n, self.grads[gname], dt=self.dt, ws=self.ws(ops.colsum_ws(M, n)))
+
+    # ------------------------------------------------------------------ FFT block
+    def _fft_fwd(self, X, B, T, key_pad, prefix, H, p_drop, seed, salt):
+        D = self.cfg.enc_d_model
+        dh = D // H
+        M = B * T
+        P = self.params
+        ctx = {"X": X}
+        QKV = self.empty(M, 3 * D)
+        self._fwd(X, D, M, T, prefix + "self_att.att.in_proj_weight", QKV, 3 * D,
+                  bias=P[prefix + "self_att.att.in_proj_bias"])
+        ldt = round_up(T, 8)
+        S = torch.empty(B * H, T, ldt, dtype=torch.float32, device=self.dev)
+        ops.gemm(T, T, dh, QKV, 3 * D, QKV[:, D:], 3 * D, S, ldt, dt=self.dt, c_fp32=1,
+                 batch=B * H, batch_div=H,
+                 strides=(T * 3 * D, dh, T * 3 * D, dh, H * T * ldt, T * ldt, 0, 0))
+        Pm = self.empty(B * H, T, ldt)
+        Pd = self.empty(B * H, T, ldt) if p_drop > 0 else Pm
+        s_att = salt()
+        ops.softmax_fwd(S, key_pad, B, H, T, T, ldt, 1.0 / math.sqrt(dh), p_drop, seed, s_att, Pm,
+                        Pd if p_drop > 0 else None, dt=self.dt)
+        del S
+        Att = self.empty(M, D)
+        ops.gemm(T, dh, ldt, Pd, ldt, QKV[:, 2 * D:], 3 * D, Att, D, dt=self.dt, b_kmajor=0,
+                 kvalid=T, batch=B * H, batch_div=H,
+                 strides=(H * T * ldt, T * ldt, T * 3 * D, dh, T * D, dh, 0, 0))
+        Ao = self.empty(M, D)
+        self._fwd(Att, D, M, T, prefix + "self_att.att.out_proj.weight", Ao, D,
+                  bias=P[prefix + "self_att.att.out_proj.bias"])
+        X1, s1 = self.empty(M, D), self.empty(M, D)
+        mean1 = torch.empty(M, dtype=torch.float32, device=self.dev)
+        rstd1 = torch.empty_like(mean1)
+        s_r1 = salt()
+        ops.ln_fwd(X, D, P[prefix + "norm1.norm.weight"], P[prefix + "norm1.norm.bias"], 1e-6, X1, D,
+                   mean1, rstd1, M, D, dt=self.dt, seed=seed, r=Ao, ldr=D, p_r=p_drop, salt_r=s_r1,
+                   s_out=s1)
+        del Ao
+        F = self._wspecs[prefix + "pos_ffn.0.conv.weight"][0]
+        Hc = self.empty(M, F)
+        self._fwd(X1, D, M, T, prefix + "pos_ffn.0.conv.weight", Hc, F,
+                  bias=P[prefix + "pos_ffn.0.conv.bias"], relu=1)
+        Y = self.empty(M, D)
+        self._fwd(Hc, F, M, T, prefix + "pos_ffn.2.conv.weight", Y, D,
+                  bias=P[prefix + "pos_ffn.2.conv.bias"])
+        X2, s2 = self.empty(M, D), self.empty(M, D)
+        mean2 = torch.empty(M, dtype=torch.float32, device=self.dev)
+        rstd2 = torch.empty_like(mean2)
+        s_r2 = salt()
+        ops.ln_fwd(X1, D, P[prefix + "norm2.norm.weight"], P[prefix + "norm2.norm.bias"], 1e-6, X2, D,
+                   mean2, rstd2, M, D, dt=self.dt, seed=seed, r=Y, ldr=D, p_r=p_drop, salt_r=s_r2,
+                   s_out=s2)
+        ctx.update(QKV=QKV, Pm=Pm, Pd=Pd, Att=Att, X1=X1, s1=s1, mean1=mean1, rstd1=rstd1, Hc=Hc,
+                   s2=s2, mean2=mean2, rstd2=rstd2, s_att=s_att, s_r1=s_r1, s_r2=s_r2, F=F,
+                   ldt=ldt)
+        return X2, ctx
+
+    def _fft_bwd(self, dX2, ctx, B, T, prefix, H, p_drop, seed):
+        D = self.cfg.enc_d_model
+        dh = D // H
+        M = B * T
+        F, ldt = ctx["F"], ctx["ldt"]
+        P, G = self.params, self.grads
+        lnws = self.ws(ops.ln_ws(M, D))
+        ds2, dY = self.empty(M, D), self.empty(M, D)
+        ops.ln_bwd(dX2, D, ctx["s2"], D, ctx["mean2"], ctx["rstd2"], P[prefix + "norm2.norm.weight"],
+                   P[prefix + "norm2.norm.bias"], ds2, D, M, D, dt=self.dt, ws=lnws, seed=seed,
+                   dr=dY, p_r=p_drop, salt_r=ctx["s_r2"], dgamma=G[prefix + "norm2.norm.weight"],
+                   dbeta=G[prefix + "norm2.norm.bias"])
+        w2 = prefix + "pos_ffn.2.conv.weight"
+        dHc = self.empty(M, F)
+        self._dgrad(dY, D, M, T, w2, dHc, F, gate=ctx["Hc"], ldg=F)
+        self._wgrad(dY, D, ctx["Hc"], F, M, T, w2)
+        self._bias_grad(dY, D, M, D, prefix + "pos_ffn.2.conv.bias")
+        del dY
+        w1 = prefix + "pos_ffn.0.conv.weight"
+        dX1 = self.empty(M, D)
+        self._dgrad(dHc, F, M, T, w1, dX1, D, residual=ds2, ldr=D)
+        self._wgrad(dHc, F, ctx["X1"], D, M, T, w1)
+        self._bias_grad(dHc, F, M, F, prefix + "pos_ffn.0.conv.bias")
+        del dHc, ds2
+        lnws = self.ws(ops.ln_ws(M, D))
+        ds1, dAo = self.empty(M, D), self.empty(M, D)
+        ops.ln_bwd(dX1, D, ctx["s1"], D, ctx["mean1"], ctx["rstd1"], P[prefix + "norm1.norm.weight"],
+                   P[prefix + "norm1.norm.bias"], ds1, D, M, D, dt=self.dt, ws=lnws, seed=seed,
+                   dr=dAo, p_r=p_drop, salt_r=ctx["s_r1"], dgamma=G[prefix + "norm1.norm.weight"],
+                   dbeta=G[prefix + "norm1.norm.bias"])
+        del dX1
+        wo = prefix + "self_att.att.out_proj.weight"
+        dAtt = self.empty(M, D)
+        self._dgrad(dAo, D, M, T, wo, dAtt, D)
+        self._wgrad(dAo, D, ctx["Att"], D, M, T, wo)
+        self._bias_grad(dAo, D, M, D, prefix + "self_att.att.out_proj.bias")
+        del dAo
+        # ---- attention backward over the materialised probabilities
+        QKV, Pm, Pd = ctx["QKV"], ctx["Pm"], ctx["Pd"]
+        dPd = torch.empty(B * H, T, ldt, dtype=torch.float32, device=self.dev)
+        ops.gemm(T, T, dh, dAtt, D, QKV[:, 2 * D:], 3 * D, dPd, ldt, dt=self.dt, c_fp32=1,
+                 batch=B * H, batch_div=H,
+                 strides=(T * D, dh, T * 3 * D, dh, H * T * ldt, T * ldt, 0, 0))
+        dQKV = self.empty(M, 3 * D)
+        # dV = Pd^T dO
+        ops.gemm(ldt, dh, ldt, Pd, ldt, dAtt, D, dQKV[:, 2 * D:], 3 * D, dt=self.dt, a_kmajor=0,
+                 b_kmajor=0, kvalid=T, mvalid=T, batch=B * H, batch_div=H,
+                 strides=(H * T * ldt, T * ldt, T * D, dh, T * 3 * D, dh, 0, 0))
+        dS = self.empty(B * H, T, ldt)
+        ops.softmax_bwd(dPd, Pm, B, H, T, T, ldt, 1.0 / math.sqrt(dh), p_drop, seed, ctx["s_att"], dS,
+                        dt=self.dt)
+        del dPd
+        # dQ = dS K
+        ops.gemm(T, dh, ldt, dS, ldt, QKV[:, D:], 3 * D, dQKV, 3 * D, dt=self.dt, b_kmajor=0,
+                 kvalid=T, batch=B * H, batch_div=H,
+                 strides=(H * T * ldt, T * ldt, T * 3 * D, dh, T * 3 * D, dh, 0, 0))
+        # dK = dS^T Q
+        ops.gemm(ldt, dh, ldt, dS, ldt, QKV, 3 * D, dQKV[:, D:], 3 * D, dt=self.dt, a_kmajor=0,
+                 b_kmajor=0, kvalid=T, mvalid=T, batch=B * H, batch_div=H,
+                 strides=(H * T * ldt, T * ldt, T * 3 * D, dh, T * 3 * D, dh, 0, 0))
+        del dS
+        wi = prefix + "self_att.att.in_proj_weight"
+        dX = self.empty(M, D)
+        self._dgrad(dQKV, 3 * D, M, T, wi, dX, D, residual=ds1, ldr=D)
+        self._wgrad(dQKV, 3 * D, ctx["X"], D, M, T, wi)
+        self._bias_grad(dQKV, 3 * D, M, 3 * D, prefix + "self_att.att.in_proj_bias")
+        return dX
+
+    # ------------------------------------------------------------------ variance predictor
+    def _pred_fwd(self, Zin, keep, B, T, name, rate, p_drop, seed, salt):
+        D = self.cfg.enc_d_model
+        M = B * T
+        P = self.params
+        c = {"Zin": Zin}
+        a1 = self.empty(M, D)
+        self._fwd(Zin, D, M, T, name + ".conv1.conv.weight", a1, D,
+                  bias=P[name + ".conv1.conv.bias"], relu=1)
+        v1 = self.empty(M, D)
+        m1 = torch.empty(M, dtype=torch.float32, device=self.dev)
+        r1 = torch.empty_like(m1)
+        s1 = salt()
+        ops.ln_fwd(a1, D, P[name + ".ln1.norm.weight"], P[name + ".ln1.norm.bias"], 1e-5, v1, D, m1, r1,
+                   M, D, dt=self.dt, seed=seed, p_o=p_drop, salt_o=s1, row_mask=keep)
+        a2 = self.empty(M, D)
+        self._fwd(v1, D, M, T, name + ".conv2.conv.weight", a2, D,
+                  bias=P[name + ".conv2.conv.bias"], relu=1)
+        v2 = self.empty(M, D)
+        m2 = torch.empty(M, dtype=torch.float32, device=self.dev)
+        r2 = torch.empty_like(m2)
+        s2 = salt()
+        ops.ln_fwd(a2, D, P[name + ".ln2.norm.weight"], P[name + ".ln2.norm.bias"], 1e-5, v2, D, m2, r2,
+                   M, D, dt=self.dt, seed=seed, p_o=p_drop, salt_o=s2, row_mask=keep)
+        y = self.empty(B, T)
+        ops.rowdot_fwd(v2, D, P[name + ".linear.w.weight"], P[name + ".linear.w.bias"], float(rate),
+                       M, D, y, dt=self.dt)
+        c.update(a1=a1, v1=v1, m1=m1, r1=r1, a2=a2, v2=v2, m2=m2, r2=r2, s1=s1, s2=s2,
+                 rate=float(rate))
+        return y, c
+
+    def _pred_bwd(self, dy, c, keep, B, T, name, p_drop, seed, residual=None, post_mask=False):
+        """returns dZin (masked by keep) [+ residual] for the predictor input."""
+        D = self.cfg.enc_d_model
+        M = B * T
+        P, G = self.params, self.grads
+        dv2 = self.empty(M, D)
+        nb = min(256, max(1, (M + 31) // 32))
+        ops.rowdot_bwd(dy, c["v2"], D, P[name + ".linear.w.weight"], c["rate"], M, D, dv2,
+                       G[name + ".linear.w.weight"], G[name + ".linear.w.bias"], dt=self.dt,
+                       ws=self.ws(nb * (D + 1)))
+        da2 = self.empty(M, D)
+        ops.ln_bwd(dv2, D, c["a2"], D, c["m2"], c["r2"], P[name + ".ln2.norm.weight"],
+                   P[name + ".ln2.norm.bias"], da2, D, M, D, dt=self.dt, ws=self.ws(ops.ln_ws(M, D)),
+                   seed=seed, p_o=p_drop, salt_o=c["s2"], row_mask=keep, relu_gate_in=1,
+                   dgamma=G[name + ".ln2.norm.weight"], dbeta=G[name + ".ln2.norm.bias"])
+        w2 = name + ".conv2.conv.weight"
+        dv1 = self.empty(M, D)
+        self._dgrad(da2, D, M, T, w2, dv1, D)
+        self._wgrad(da2, D, c["v1"], D, M, T, w2)
+        self._bias_grad(da2, D, M, D, name + ".conv2.conv.bias")
+        da1 = self.empty(M, D)
+        ops.ln_bwd(dv1, D, c["a1"], D, c["m1"], c["r1"], P[name + ".ln1.norm.weight"],
+                   P[name + ".ln1.norm.bias"], da1, D, M, D, dt=self.dt, ws=self.ws(ops.ln_ws(M, D)),
+                   seed=seed, p_o=p_drop, salt_o=c["s1"], row_mask=keep, relu_gate_in=1,
+                   dgamma=G[name + ".ln1.norm.weight"], dbeta=G[name + ".ln1.norm.bias"])
+        w1 = name + ".conv1.conv.weight"
+        dZ = self.empty(M, D)
+        self._dgrad(da1, D, M, T, w1, dZ, D, row_scale=keep, residual=residual,
+                    ldr=D if residual is not None else 0,
+                    row_scale_post=keep if post_mask else None)
+        self._wgrad(da1, D, c["Zin"], D, M, T, w1)
+        self._bias_grad(da1, D, M, D, name + ".conv1.conv.bias")
+        return dZ
+
+    # ------------------------------------------------------------------ PostNet
+    def _postnet_fwd(self, mel, B, T, p_drop, seed, salt):
+        c = self.cfg
+        E, NM = c.postnet_embedding_dim, c.n_mels
+        M = B * T
+        P = self.params
+        ctx = {"in": mel}
+        x, ldx = mel, NM
+        convs = ["postnet.conv_pre"] + [f"postnet.convs_intermedite.{i}"
+                                        for i in range(c.postnet_n_convolutions - 2)]
+        outs = []
+        for i, name in enumerate(convs):
+            p = self.empty(M, E)
+            self._fwd(x, ldx, M, T, name + ".conv.weight", p, E, bias=P[name + ".conv.bias"])
+            outs.append((name, x, ldx, p))
+            if i == 0:
+                q = self.empty(M, E)
+                mn = torch.empty(M, dtype=torch.float32, device=self.dev)
+                rs = torch.empty_like(mn)
+                s = salt()
+                ops.ln_fwd(p, E, P["postnet.ln1.weight"], P["postnet.ln1.bias"], 1e-5, q, E, mn, rs, M,
+                           E, dt=self.dt, seed=seed, do_tanh=1, p_o=p_drop, salt_o=s)
+                ctx["ln1"] = (p, mn, rs, s)
+                x, ldx = q, E
+            else:
+                x, ldx = p, E
+        q3 = self.empty(M, E)
+        mn = torch.empty(M, dtype=torch.float32, device=self.dev)
+        rs = torch.empty_like(mn)
+        s = salt()
+        ops.ln_fwd(x, E, P["postnet.ln2.weight"], P["postnet.ln2.bias"], 1e-5, q3, E, mn, rs, M, E,
+                   dt=self.dt, seed=seed, do_tanh=1, p_o=p_drop, salt_o=s)
+        ctx["ln2"] = (x, mn, rs, s)
+        p4 = self.empty(M, NM)
+        self._fwd(q3, E, M, T, "postnet.conv_post.conv.weight", p4, NM,
+                  bias=P["postnet.conv_post.conv.bias"])
+        post = self.empty(M, NM)
+        mn3 = torch.empty(M, dtype=torch.float32, device=self.dev)
+        rs3 = torch.empty_like(mn3)
+        s3 = salt()
+        ops.ln_fwd(p4, NM, P["postnet.ln3.weight"], P["postnet.ln3.bias"], 1e-5, post, NM, mn3, rs3, M,
+                   NM, dt=self.dt, seed=seed, p_o=p_drop, salt_o=s3, post_add=mel, ldp=NM)
+        ctx.update(convs=outs, q3=q3, p4=p4, ln3=(p4, mn3, rs3, s3))
+        return post, ctx
+
+    def _postnet_bwd(self, d_post, d_mel_total, keep, ctx, B, T, p_drop, seed):
+        """d_mel_total: grad already accumulated on mel (loss + residual); returns masked d_mel."""
+        c = self.cfg
+        E, NM = c.postnet_embedding_dim, c.n_mels
+        M = B * T
+        P, G = self.params, self.grads
+        p4, mn3, rs3, s3 = ctx["ln3"]
+        dp4 = self.empty(M, NM)
+        ops.ln_bwd(d_post, NM, p4, NM, mn3, rs3, P["postnet.ln3.weight"], P["postnet.ln3.bias"], dp4,
+                   NM, M, NM, dt=self.dt, ws=self.ws(ops.ln_ws(M, NM)), seed=seed, p_o=p_drop,
+                   salt_o=s3, dgamma=G["postnet.ln3.weight"], dbeta=G["postnet.ln3.bias"])
+        wname = "postnet.conv_post.conv.weight"
+        dq3 = self.empty(M, E)
+        self._dgrad(dp4, NM, M, T, wname, dq3, E)
+        self._wgrad(dp4, NM, ctx["q3"], E, M, T, wname)
+        self._bias_grad(dp4, NM, M, NM, "postnet.conv_post.conv.bias")
+        x, mn, rs, s = ctx["ln2"]
+        dx = self.empty(M, E)
+        ops.ln_bwd(dq3, E, x, E, mn, rs, P["postnet.ln2.weight"], P["postnet.ln2.bias"], dx, E, M, E,
+                   dt=self.dt, ws=self.ws(ops.ln_ws(M, E)), seed=seed, do_tanh=1, p_o=p_drop,
+                   salt_o=s, dgamma=G["postnet.ln2.weight"], dbeta=G["postnet.ln2.bias"])
+        for i, (name, xin, ldx, p) in reversed(list(enumerate(ctx["convs"]))):
+            if i == 0:
+                p0, mn1, rs1, s1 = ctx["ln1"]
+                dp0 = self.empty(M, E)
+                ops.ln_bwd(dx, E, p0, E, mn1, rs1, P["postnet.ln1.weight"], P["postnet.ln1.bias"], dp0,
+                           E, M, E, dt=self.dt, ws=self.ws(ops.ln_ws(M, E)), seed=seed, do_tanh=1,
+                           p_o=p_drop, salt_o=s1, dgamma=G["postnet.ln1.weight"],
+                           dbeta=G["postnet.ln1.bias"])
+                dx = dp0
+                dmel = self.empty(M, NM)
+                self._dgrad(dx, E, M, T, name + ".conv.weight", dmel, NM, residual=d_mel_total,
+                            ldr=NM, row_scale_post=keep)
+                self._wgrad(dx, E, xin, ldx, M, T, name + ".conv.weight")
+                self._bias_grad(dx, E, M, E, name + ".conv.bias")
+                return dmel
+            dprev = self.empty(M, E)
+            self._dgrad(dx, E, M, T, name + ".conv.weight", dprev, E)
+            self._wgrad(dx, E, xin, ldx, M, T, name + ".conv.weight")
+            self._bias_grad(dx, E, M, E, name + ".conv.bias")
+            dx = dprev
+
+    # ------------------------------------------------------------------ full forward
+    def forward(self, tokens, speakers, durations=None, pitch=None, energy=None, pace=1.0,
+                pitch_rate=1.0, energy_rate=1.0, intensity=None, training=True, seed=0,
+                mel_len_max=None):
+        """Model forward (model.py:279-441).  Returns (outputs tuple, ctx for backward)."""
+        c = self.cfg
+        self.prepare_weights()
+        D, H_e, H_d = c.enc_d_model, c.enc_num_head, c.dec_num_head
+        NM = c.n_mels
+        P = self.params
+        tokens = tokens.contiguous()
+        speakers = speakers.contiguous()
+        B, Tp = tokens.shape
+        Mp = B * Tp
+        salt = _Salt()
+        pe_enc_p = c.enc_dropout if training else 0.0
+        pe_dec_p = c.dec_dropout if training else 0.0
+        pv = c.variance_predictor_dropout if training else 0.0
+        pp_ = c.postnet_dropout if training else 0.0
+        ctx = {"B": B, "Tp": Tp, "seed": seed, "training": training, "tokens": tokens,
+               "speakers": speakers}
+        # encoder prenet + PE + mask (model.py:331-337)
+        X = self.empty(Mp, D)
+        keep_p = torch.empty(Mp, dtype=torch.float32, device=self.dev)
+        ops.embed_fwd(tokens, P["encPreNet.token_embedding.Embedding.weight"], self.pe_enc,
+                      c.padding_idx, B, Tp, D, X, keep_p, dt=self.dt)
+        kp_enc = torch.empty(Mp, dtype=torch.uint8, device=self.dev)
+        ops.keypad_from_tokens(tokens, c.padding_idx, Mp, kp_enc)
+        enc_ctx = []
+        for i in range(c.enc_num_layers):
+            X, lc = self._fft_fwd(X, B, Tp, kp_enc, f"encoder.layers.{i}.", H_e, pe_enc_p, seed, salt)
+            enc_ctx.append(lc)
+        Xe = self.empty(Mp, D)
+        me = torch.empty(Mp, dtype=torch.float32, device=self.dev)
+        re_ = torch.empty_like(me)
+        ops.ln_fwd(X, D, P["encoder.norm.norm.weight"], P["encoder.norm.norm.bias"], 1e-6, Xe, D, me,
+                   re_, Mp, D, dt=self.dt, row_mask=keep_p)                       # :344-347
+        # speaker + emotion-intensity conditioning (model.py:352-360)
+        E_int = 5
+        ldc = round_up(2 * D + E_int, self.epc)
+        cat = self.empty(Mp, ldc)
+        if intensity is None:
+            raise ValueError("intensity (B, T_phon, 5) is required (model.py:356-358)")
+        intensity = intensity.to(device=self.dev, dtype=torch.float32).contiguous()
+        ops.concat_fwd(Xe, P["speaker_emb.Embedding.weight"], speakers, intensity, B, Tp, D, E_int,
+                       cat, ldc, dt=self.dt)
+        Z = self.empty(Mp, D)
+        self._fwd(cat, ldc, Mp, Tp, "concat_proj.w.weight", Z, D, row_scale=keep_p)
+        # variance adaptor (model.py:365-403)
+        pd, dctx = self._pred_fwd(Z, keep_p, B, Tp, "durPred", 1.0, pv, seed, salt)
+        pp, pctx = self._pred_fwd(Z, keep_p, B, Tp, "pitchPred", pitch_rate, pv, seed, salt)
+        kwp = c.pitch_pred_kernel_size
+        if pitch is not None:
+            pitch = pitch.to(torch.float32).contiguous()
+            avg_p = torch.empty(B, Tp, dtype=torch.float32, device=self.dev)
+            ops.avg_over_durations(pitch, pitch.shape[1], durations.contiguous(), B, Tp, avg_p,
+                                   self.ws(ops.avg_ws(B, pitch.shape[1])))
+            a_p = avg_p
+        else:
+            avg_p = None
+            a_p = pp.float()
+        Z2 = self.empty(Mp, D)
+        ops.embed1d_fwd(Z, a_p, P["pitchEmbed.conv.weight"], P["pitchEmbed.conv.bias"], B, Tp, D, kwp,
+                        Z2, dt=self.dt)
+        Z2m = Z2.clone()
+        ops.mask_rows(Z2m, D, keep_p, Mp, D, dt=self.dt)
+        pe_, ectx = self._pred_fwd(Z2m, keep_p, B, Tp, "energyPred", energy_rate, pv, seed, salt)
+        kwe = c.energy_pred_kernel_size
+        if energy is not None:
+            energy = energy.to(torch.float32).contiguous()
+            avg_e = torch.empty(B, Tp, dtype=torch.float32, device=self.dev)
+            ops.avg_over_durations(energy, energy.shape[1], durations.contiguous(), B, Tp, avg_e,
+                                   self.ws(ops.avg_ws(B, energy.shape[1])))
+            a_e = avg_e
+        else:
+            avg_e = None
+            a_e = pe_.float()
+        Z3 = self.empty(Mp, D)
+        ops.embed1d_fwd(Z2, a_e, P["energyEmbed.conv.weight"], P["energyEmbed.conv.bias"], B, Tp, D,
+                        kwe, Z3, dt=self.dt)
+        # LengthRegulator (model.py:406-413)
+        if durations is not None:
+            durs, d_is_float = durations.contiguous(), 0
+        else:
+            durs = torch.clamp(torch.special.expm1(pd.float()), min=0).contiguous()
+            d_is_float = 1
+        mel_len = torch.empty(B, dtype=torch.int64, device=self.dev)
+        cum = torch.empty(B, Tp, dtype=torch.int32, device=self.dev)
+        if mel_len_max is None:
+            ops.lr_index(durs, d_is_float, float(pace), B, Tp, 0, mel_len, cum, None)
+            mel_lens_host = mel_len.cpu()
+            Tm = int(mel_lens_host.max())
+        else:
+            Tm = int(mel_len_max)
+            mel_lens_host = None
+        frame_src = torch.empty(B, Tm, dtype=torch.int32, device=self.dev)
+        ops.lr_index(durs, d_is_float, float(pace), B, Tp, Tm, mel_len, cum, frame_src)
+        Mm = B * Tm
+        S0 = self.empty(Mm, D)
+        keep_m = torch.empty(Mm, dtype=torch.float32, device=self.dev)
+        ops.lr_gather(Z3, frame_src, self.pe_dec, B, Tp, Tm, D, S0, keep_m, dt=self.dt)  # :422-423
+        kp_dec = torch.empty(Mm, dtype=torch.uint8, device=self.dev)
+        ops.keypad_from_lengths(mel_len, B, Tm, kp_dec)
+        Xd = S0
+        dec_ctx = []
+        for i in range(c.dec_num_layers):
+            Xd, lc = self._fft_fwd(Xd, B, Tm, kp_dec, f"decoder.layers.{i}.", H_d, pe_dec_p, seed, salt)
+            dec_ctx.append(lc)
+        Xo = self.empty(Mm, D)
+        md = torch.empty(Mm, dtype=torch.float32, device=self.dev)
+        rd = torch.empty_like(md)
+        ops.ln_fwd(Xd, D, P["decoder.norm.norm.weight"], P["decoder.norm.norm.bias"], 1e-6, Xo, D, md,
+                   rd, Mm, D, dt=self.dt)
+        mel = self.empty(Mm, NM)
+        self._fwd(Xo, D, Mm, Tm, "linear.w.weight", mel, NM, bias=P["linear.w.bias"],
+                  row_scale=keep_m)                                                # :430
+        post, pn_ctx = self._postnet_fwd(mel, B, Tm, pp_, seed, salt)            # :431
+        ctx.update(keep_p=keep_p, enc_ctx=enc_ctx, Xenc_last=X, me=me, re=re_, cat=cat, ldc=ldc,
+                   Z=Z, dctx=dctx, pctx=pctx, ectx=ectx, a_p=a_p, a_e=a_e, Z2m=Z2m, Tm=Tm,
+                   cum=cum, keep_m=keep_m, dec_ctx=dec_ctx, Xdec_last=Xd, md=md, rd=rd, Xo=Xo,
+                   pn_ctx=pn_ctx, p_enc=pe_enc_p, p_dec=pe_dec_p, p_var=pv, p_post=pp_,
+                   mel_len=mel_len)
+        out = (mel.view(B, Tm, NM), post.view(B, Tm, NM), pd.view(B, Tp), pp.view(B, Tp, 1),
+               None if avg_p is None else avg_p.view(B, Tp, 1), pe_.view(B, Tp, 1),
+               None if avg_e is None else avg_e.view(B, Tp, 1),
+               mel_lens_host if mel_lens_host is not None else mel_len)
+        return out, ctx
+
+    # ------------------------------------------------------------------ full backward
+    def backward(self, ctx, d_mel, d_post, d_dur, d_pitch, d_energy):
+        """Backward of ``forward`` for upstream gradients of (mel, postnet, log-dur, pitch,
+        energy) outputs; parameter gradients are ACCUMULATED into model._gflat."""
+        c = self.cfg
+        D, H_e, H_d, NM = c.enc_d_model, c.enc_num_head, c.dec_num_head, c.n_mels
+        B, Tp, Tm, seed = ctx["B"], ctx["Tp"], ctx["Tm"], ctx["seed"]
+        Mp, Mm = B * Tp, B * Tm
+        P, G = self.params, self.grads
+        keep_p, keep_m = ctx["keep_p"], ctx["keep_m"]
+        notify = self.on_grads_ready or (lambda tag: None)
+        d_mel = d_mel.reshape(Mm, NM).to(self.adt).contiguous()
+        d_post = d_post.reshape(Mm, NM).to(self.adt).contiguous()
+        # mel receives the loss gradient and the PostNet residual (model.py:431)
+        d_mel_total = d_mel.clone()
+        ops.add(d_mel_total, d_post, Mm * NM, 1.0, dt=self.dt)
+        dmel = self._postnet_bwd(d_post, d_mel_total, keep_m, ctx["pn_ctx"], B, Tm, ctx["p_post"],
+                                 seed)
+        notify("postnet")
+        # mel linear (masked output, model.py:430)
+        dXo = self.empty(Mm, D)
+        self._dgrad(dmel, NM, Mm, Tm, "linear.w.weight", dXo, D)
+        self._wgrad(dmel, NM, ctx["Xo"], D, Mm, Tm, "linear.w.weight")
+        self._bias_grad(dmel, NM, Mm, NM, "linear.w.bias")
+        dX = self.empty(Mm, D)
+        ops.ln_bwd(dXo, D, ctx["Xdec_last"], D, ctx["md"], ctx["rd"], P["decoder.norm.norm.weight"],
+                   P["decoder.norm.norm.bias"], dX, D, Mm, D, dt=self.dt, ws=self.ws(ops.ln_ws(Mm, D)),
+                   dgamma=G["decoder.norm.norm.weight"], dbeta=G["decoder.norm.norm.bias"])
+        notify("linear")
+        for i in reversed(range(c.dec_num_layers)):
+            dX = self._fft_bwd(dX, ctx["dec_ctx"][i], B, Tm, f"decoder.layers.{i}.", H_d,
+                               ctx["p_dec"], seed)
+            notify(f"decoder.layers.{i}")
+        # LengthRegulator backward: segment sums (masked by the decoder input mask)
+        dZ3 = self.empty(Mp, D)
+        ops.lr_scatter(dX, ctx["cum"], keep_m, B, Tp, Tm, D, dZ3, dt=self.dt)
+        kwe = c.energy_pred_kernel_size
+        ops.embed1d_bwd(dZ3, ctx["a_e"], B, Tp, D, kwe, G["energyEmbed.conv.weight"],
+                        G["energyEmbed.conv.bias"], dt=self.dt,
+                        ws=self.ws(128 * (kwe + 1) * D))
+        d_energy = d_energy.reshape(Mp).to(self.adt).contiguous()
+        dZ2 = self._pred_bwd(d_energy, ctx["ectx"], keep_p, B, Tp, "energyPred", ctx["p_var"], seed,
+                             residual=dZ3)
+        kwp = c.pitch_pred_kernel_size
+        ops.embed1d_bwd(dZ2, ctx["a_p"], B, Tp, D, kwp, G["pitchEmbed.conv.weight"],
+                        G["pitchEmbed.conv.bias"], dt=self.dt, ws=self.ws(128 * (kwp + 1) * D))
+        d_pitch = d_pitch.reshape(Mp).to(self.adt).contiguous()
+        dZa = self._pred_bwd(d_pitch, ctx["pctx"], keep_p, B, Tp, "pitchPred", ctx["p_var"], seed,
+                             residual=dZ2)
+        d_dur = d_dur.reshape(Mp).to(self.adt).contiguous()
+        dZ = self._pred_bwd(d_dur, ctx["dctx"], keep_p, B, Tp, "durPred", ctx["p_var"], seed,
+                            residual=dZa, post_mask=True)
+        notify("variance")
+        # concat projection (Z = proj(cat) * keep) -- dZ is already masked
+        ldc = ctx["ldc"]
+        dcat = self.empty(Mp, 2 * D)
+        self._dgrad(dZ, D, Mp, Tp, "concat_proj.w.weight", dcat, 2 * D, n_out=2 * D)
+        self._wgrad(dZ, D, ctx["cat"], ldc, Mp, Tp, "concat_proj.w.weight", n_cols=ldc)
+        ops.concat_bwd_spk(dcat, 2 * D, ctx["speakers"], B, Tp, D, c.n_speakers,
+                           G["speaker_emb.Embedding.weight"], dt=self.dt)
+        dXl = self.empty(Mp, D)
+        ops.ln_bwd(dcat, 2 * D, ctx["Xenc_last"], D, ctx["me"], ctx["re"], P["encoder.norm.norm.weight"],
+                   P["encoder.norm.norm.bias"], dXl, D, Mp, D, dt=self.dt,
+                   ws=self.ws(ops.ln_ws(Mp, D)), row_mask=keep_p,
+                   dgamma=G["encoder.norm.norm.weight"], dbeta=G["encoder.norm.norm.bias"])
+        notify("conditioning")
+        dX = dXl
+        for i in reversed(range(c.enc_num_layers)):
+            dX = self._fft_bwd(dX, ctx["enc_ctx"][i], B, Tp, f"encoder.layers.{i}.", H_e,
+                               ctx["p_enc"], seed)
+            notify(f"encoder.layers.{i}")
+        ops.embed_bwd(ctx["tokens"], dX, keep_p, Mp, D, c.n_char,
+                      G["encPreNet.token_embedding.Embedding.weight"], dt=self.dt)
+        notify("prenet")

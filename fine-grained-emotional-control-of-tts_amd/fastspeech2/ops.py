@@ -1,0 +1,205 @@
+"""Python operator layer over the C ABI (include/fs2_hip.h).
+
+Every function here is a thin, allocation-free wrapper: it turns tensors into device
+pointers, passes torch's *current* HIP stream, and raises if the native call reports an
+error.  Tensors are owned by torch's caching allocator; the kernels never allocate.
+"""
+
+import ctypes
+
+import torch
+
+from . import _native as N
+
+EPC = {N.F32: 4, N.BF16: 8}   # elements per 16-byte chunk (GEMM K / pitch granularity)
+
+
+def _p(x):
+    if x is None:
+        return None
+    if isinstance(x, int):
+        return x
+    return x.data_ptr()
+
+
+def _s():
+    return N.stream_ptr()
+
+
+def _chk(rc, name):
+    if rc != 0:
+        raise RuntimeError(f"{name} returned {rc}")
+
+
+def round_up(x, m):
+    return (x + m - 1) // m * m
+
+
+def gemm(M, N_, K, A, lda, B, ldb, C, ldc, *, dt, a_kmajor=1, b_kmajor=1, conv=None, c_fp32=0,
+         c_conv_kw=0, bias=None, relu=0, gate=None, ldg=0, row_scale=None, residual=None, ldr=0,
+         row_scale_post=None, accumulate=0, split_k=1, kvalid=0, mvalid=0, nvalid=0, batch=1,
+         batch_div=1, strides=None):
+    d = N.GemmDesc()
+    d.M, d.N, d.K, d.kvalid, d.mvalid, d.nvalid, d.dtype = M, N_, K, kvalid, mvalid, nvalid, dt
+    d.A, d.lda, d.a_kmajor = _p(A), lda, a_kmajor
+    d.B, d.ldb, d.b_kmajor = _p(B), ldb, b_kmajor
+    if conv is not None:
+        d.conv_mode, d.conv_t, d.conv_kw, d.conv_c = conv
+    d.C, d.ldc, d.c_fp32, d.c_conv_kw = _p(C), ldc, c_fp32, c_conv_kw
+    d.bias, d.relu = _p(bias), relu
+    d.gate, d.ldg = _p(gate), ldg
+    d.row_scale = _p(row_scale)
+    d.residual, d.ldr = _p(residual), ldr
+    d.row_scale_post = _p(row_scale_post)
+    d.accumulate, d.split_k = accumulate, split_k
+    d.batch, d.batch_div = batch, batch_div
+    if strides is not None:
+        (d.sA1, d.sA2, d.sB1, d.sB2, d.sC1, d.sC2, d.sR1, d.sR2) = strides
+    _chk(N.lib().fs2_gemm(ctypes.byref(d), _s()), "fs2_gemm")
+
+
+def colsum(X, ldx, M, N_, out, *, dt, ws, accumulate=1):
+    _chk(N.lib().fs2_colsum(_p(X), ldx, M, N_, dt, _p(out), accumulate, _p(ws), _s()), "fs2_colsum")
+
+
+def colsum_ws(M, N_):
+    return N.lib().fs2_colsum_workspace_floats(M, N_)
+
+
+def ln_fwd(x, ldx, gamma, beta, eps, y, ldy, mean, rstd, M, D, *, dt, seed=0, r=None, ldr=0,
+           p_r=0.0, salt_r=0, s_out=None, do_tanh=0, p_o=0.0, salt_o=0, row_mask=None,
+           post_add=None, ldp=0):
+    _chk(N.lib().fs2_ln_fwd(_p(x), ldx, _p(r), ldr, p_r, salt_r, _p(s_out), _p(gamma), _p(beta),
+                            eps, do_tanh, p_o, salt_o, _p(row_mask), _p(post_add), ldp, _p(y), ldy,
+                            _p(mean), _p(rstd), M, D, dt, seed & 0xffffffff, _s()), "fs2_ln_fwd")
+
+
+def ln_bwd(dy, lddy, s, lds, mean, rstd, gamma, beta, ds, ldds, M, D, *, dt, ws, seed=0,
+           do_tanh=0, p_o=0.0, salt_o=0, row_mask=None, relu_gate_in=0, dr=None, p_r=0.0,
+           salt_r=0, dgamma=None, dbeta=None):
+    _chk(N.lib().fs2_ln_bwd(_p(dy), lddy, _p(s), lds, _p(mean), _p(rstd), _p(gamma), _p(beta),
+                            do_tanh, p_o, salt_o, _p(row_mask), relu_gate_in, _p(ds), ldds, _p(dr),
+                            p_r, salt_r, _p(dgamma), _p(dbeta), M, D, dt, seed & 0xffffffff,
+                            _p(ws), _s()), "fs2_ln_bwd")
+
+
+def ln_ws(M, D):
+    return N.lib().fs2_ln_workspace_floats(M, D)
+
+
+def softmax_fwd(S, key_pad, B, H, Tq, Tk, ldt, scale, p_drop, seed, salt, P, Pd, *, dt):
+    _chk(N.lib().fs2_softmax_fwd(_p(S), _p(key_pad), B, H, Tq, Tk, ldt, scale, p_drop,
+                                 seed & 0xffffffff, salt, _p(P), _p(Pd), dt, _s()), "fs2_softmax_fwd")
+
+
+def softmax_bwd(dPd, P, B, H, Tq, Tk, ldt, scale, p_drop, seed, salt, dS, *, dt):
+    _chk(N.lib().fs2_softmax_bwd(_p(dPd), _p(P), B, H, Tq, Tk, ldt, scale, p_drop,
+                                 seed & 0xffffffff, salt, _p(dS), dt, _s()), "fs2_softmax_bwd")
+
+
+def embed_fwd(tokens, table, pe, pad_idx, B, T, D, X, keep, *, dt):
+    _chk(N.lib().fs2_embed_fwd(_p(tokens), _p(table), _p(pe), pad_idx, B, T, D, _p(X), _p(keep),
+                               dt, _s()), "fs2_embed_fwd")
+
+
+def embed_bwd(tokens, dX, keep, M, D, V, dtable, *, dt):
+    _chk(N.lib().fs2_embed_bwd(_p(tokens), _p(dX), _p(keep), M, D, V, _p(dtable), dt, _s()),
+         "fs2_embed_bwd")
+
+
+def keypad_from_tokens(tokens, pad_idx, M, key_pad):
+    _chk(N.lib().fs2_keypad_from_tokens(_p(tokens), pad_idx, M, _p(key_pad), _s()),
+         "fs2_keypad_from_tokens")
+
+
+def keypad_from_lengths(lens, B, T, key_pad, keep=None):
+    _chk(N.lib().fs2_keypad_from_lengths(_p(lens), B, T, _p(key_pad), _p(keep), _s()),
+         "fs2_keypad_from_lengths")
+
+
+def concat_fwd(feats, spk_table, spk, intensity, B, T, D, E, cat, ldc, *, dt):
+    _chk(N.lib().fs2_concat_fwd(_p(feats), _p(spk_table), _p(spk), _p(intensity), B, T, D, E,
+                                _p(cat), ldc, dt, _s()), "fs2_concat_fwd")
+
+
+def concat_bwd_spk(dcat, ldc, spk, B, T, D, n_spk, dspk, *, dt):
+    _chk(N.lib().fs2_concat_bwd_spk(_p(dcat), ldc, _p(spk), B, T, D, n_spk, _p(dspk), dt, _s()),
+         "fs2_concat_bwd_spk")
+
+
+def mask_rows(X, ldx, keep, M, D, *, dt):
+    _chk(N.lib().fs2_mask_rows(_p(X), ldx, _p(keep), M, D, dt, _s()), "fs2_mask_rows")
+
+
+def rowdot_fwd(u, ldu, w, b, scale, M, D, y, *, dt):
+    _chk(N.lib().fs2_rowdot_fwd(_p(u), ldu, _p(w), _p(b), scale, M, D, _p(y), dt, _s()),
+         "fs2_rowdot_fwd")
+
+
+def rowdot_bwd(dy, u, ldu, w, scale, M, D, du, dw, db, *, dt, ws):
+    _chk(N.lib().fs2_rowdot_bwd(_p(dy), _p(u), ldu, _p(w), scale, M, D, _p(du), _p(dw), _p(db),
+                                dt, _p(ws), _s()), "fs2_rowdot_bwd")
+
+
+def avg_over_durations(values, Tm_in, durs, B, Tp, avg, ws):
+    _chk(N.lib().fs2_avg_over_durations(_p(values), Tm_in, _p(durs), B, Tp, _p(avg), _p(ws), _s()),
+         "fs2_avg_over_durations")
+
+
+def avg_ws(B, Tm_in):
+    return N.lib().fs2_avg_workspace_floats(B, Tm_in)
+
+
+def embed1d_fwd(base, a, W, bias, B, T, D, KW, out, *, dt):
+    _chk(N.lib().fs2_embed1d_fwd(_p(base), _p(a), _p(W), _p(bias), B, T, D, KW, _p(out), dt, _s()),
+         "fs2_embed1d_fwd")
+
+
+def embed1d_bwd(dout, a, B, T, D, KW, dW, dbias, *, dt, ws):
+    _chk(N.lib().fs2_embed1d_bwd(_p(dout), _p(a), B, T, D, KW, _p(dW), _p(dbias), dt, _p(ws), _s()),
+         "fs2_embed1d_bwd")
+
+
+def lr_index(durs, d_is_float, pace, B, Tp, Tm, mel_len, cum, frame_src):
+    _chk(N.lib().fs2_lr_index(_p(durs), d_is_float, pace, B, Tp, Tm, _p(mel_len), _p(cum),
+                              _p(frame_src), _s()), "fs2_lr_index")
+
+
+def lr_gather(X, frame_src, pe, B, Tp, Tm, D, Y, keep, *, dt):
+    _chk(N.lib().fs2_lr_gather(_p(X), _p(frame_src), _p(pe), B, Tp, Tm, D, _p(Y), _p(keep), dt,
+                               _s()), "fs2_lr_gather")
+
+
+def lr_scatter(dY, cum, keep, B, Tp, Tm, D, dX, *, dt):
+    _chk(N.lib().fs2_lr_scatter(_p(dY), _p(cum), _p(keep), B, Tp, Tm, D, _p(dX), dt, _s()),
+         "fs2_lr_scatter")
+
+
+def loss_fwd_bwd(desc):
+    _chk(N.lib().fs2_loss_fwd_bwd(ctypes.byref(desc), _s()), "fs2_loss_fwd_bwd")
+
+
+def loss_ws(B, Tm, NM):
+    return N.lib().fs2_loss_workspace_floats(B, Tm, NM)
+
+
+def adamw(param, grad, m, v, n, decay_mul, omb1, beta2, omb2, step_size, bc2_sqrt, eps, gscale):
+    _chk(N.lib().fs2_adamw(_p(param), _p(grad), _p(m), _p(v), n, decay_mul, omb1, beta2, omb2,
+                           step_size, bc2_sqrt, eps, gscale, _s()), "fs2_adamw")
+
+
+def weight_prep(W, O, C, KW, Wf, ldf, Wb, ldb, *, dt):
+    _chk(N.lib().fs2_weight_prep(_p(W), O, C, KW, _p(Wf), ldf, _p(Wb), ldb, dt, _s()),
+         "fs2_weight_prep")
+
+
+def fill(X, n, value, *, dt):
+    _chk(N.lib().fs2_fill(_p(X), n, value, dt, _s()), "fs2_fill")
+
+
+def add(X, Y, n, alpha=1.0, *, dt):
+    _chk(N.lib().fs2_add(_p(X), _p(Y), n, alpha, dt, _s()), "fs2_add")
+
+
+def cast(src, src_dt, dst, dst_dt, n):
+    _chk(N.lib().fs2_cast(_p(src), src_dt, _p(dst), dst_dt, n, _s()), "fs2_cast")

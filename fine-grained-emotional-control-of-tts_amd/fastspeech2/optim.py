@@ -1,0 +1,49 @@
+"""Fused AdamW over the model's flat fp32 parameter / gradient buffers.
+
+Same hyper-parameters and update rule as ``torch.optim.AdamW(model.parameters(), lr=lr)``
+used by the reference (fastspeech2/train.py:232): betas (0.9, 0.999), eps 1e-8,
+weight_decay 1e-2.  Scalars are computed in Python double exactly as torch's single-tensor
+AdamW does, then one HBM-bound kernel (``fs2_adamw``) updates all 85.3 M parameters.
+"""
+
+import torch
+
+from . import ops
+
+
+class FusedAdamW:
+    def __init__(self, model, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2):
+        self.model = model
+        self.lr, self.betas, self.eps, self.weight_decay = lr, betas, eps, weight_decay
+        model._ensure_packed()
+        self.exp_avg = torch.zeros_like(model._flat)
+        self.exp_avg_sq = torch.zeros_like(model._flat)
+        self.step_count = 0
+
+    def zero_grad(self, set_to_none=True):
+        """Gradients accumulate into the flat buffer; zeroing it is one memset."""
+        self.model._gflat.zero_()
+        for n, p in self.model.named_parameters():
+            p.grad = self.model._grad_views[n]
+
+    @torch.no_grad()
+    def step(self, grad_scale=1.0):
+        m = self.model
+        self.step_count += 1
+        b1, b2 = self.betas
+        lr, wd, t = self.lr, self.weight_decay, self.step_count
+        bc1 = 1 - b1 ** t
+        bc2 = 1 - b2 ** t
+        ops.adamw(m._flat, m._gflat, self.exp_avg, self.exp_avg_sq, m._flat.numel(),
+                  1 - lr * wd, 1 - b1, b2, 1 - b2, lr / bc1, bc2 ** 0.5, self.eps, grad_scale)
+        m.mark_params_updated()
+
+    def state_dict(self):
+        return {"step": self.step_count, "exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq,
+                "lr": self.lr, "betas": self.betas, "eps": self.eps,
+                "weight_decay": self.weight_decay}
+
+    def load_state_dict(self, sd):
+        self.step_count = sd["step"]
+        self.exp_avg.copy_(sd["exp_avg"])
+        self.exp_avg_sq.copy_(sd["exp_avg_sq"])

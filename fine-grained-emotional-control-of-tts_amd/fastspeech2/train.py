@@ -1,0 +1,112 @@
+"""Train step (emo_rank_tts/fastspeech2/train.py:54-109, 232) and its data-parallel form.
+
+* ``train_step`` is the reference loop body verbatim in structure -- model forward ->
+  ``Loss`` -> ``optim.zero_grad()`` -> ``loss['total_loss'].backward()`` -> ``optim.step()``
+  (train.py:72-81) -- and works with ``torch.optim.AdamW`` or ``FusedAdamW``.
+* ``FusedTrainer`` is the same step without autograd bookkeeping: engine forward, fused loss,
+  engine backward into the flat gradient buffer, a bucketed RCCL all-reduce (SUM, averaged in
+  the optimizer) launched per bucket as soon as the backward has produced it, then one fused
+  AdamW kernel.  One process per GPU, ``torch.distributed`` with the nccl (= RCCL) backend.
+"""
+
+import torch
+import torch.distributed as dist
+
+from .loss import fused_loss
+from .optim import FusedAdamW
+
+
+def train_step(model, criterion, optim, batch, intensity, epoch=0):
+    """train.py:60-81 loop body (intensity given as an input)."""
+    (phoneme, spk_ids, phon_len, mel_tgt, pitch_tgt, energy_tgt, duration_tgt, mel_len) = batch[:8]
+    predictions = model(phoneme, spk_ids, duration_tgt, pitch_tgt, energy_tgt, intensity=intensity)
+    targets = (mel_tgt, duration_tgt, pitch_tgt, energy_tgt, mel_len, phon_len)
+    loss = criterion(predictions, targets, epoch)
+    optim.zero_grad()
+    loss["total_loss"].backward()
+    optim.step()
+    return predictions, loss
+
+
+class GradBucketer:
+    """Bucketed all-reduce of a flat gradient buffer, overlapped with the backward.
+
+    ``ranges`` are the model's (tag, start, end) backward groups in completion order; they
+    are merged into contiguous buckets of at least ``bucket_bytes``.  ``ready(tag)`` is called
+    by the backward when a group's gradients are final; a bucket is reduced (async, SUM) once
+    its last group is ready.  ``finish()`` waits for every outstanding reduction.
+    """
+
+    def __init__(self, flat, ranges, bucket_bytes=32 << 20, group=None):
+        self.flat, self.group = flat, group
+        self.buckets = []          # [(start, end, last_tag)]
+        cur = None
+        for tag, s, e in ranges:
+            if cur is None:
+                cur = [s, e, tag]
+            else:
+                cur[1], cur[2] = e, tag
+            if (cur[1] - cur[0]) * flat.element_size() >= bucket_bytes:
+                self.buckets.append(tuple(cur))
+                cur = None
+        if cur is not None:
+            self.buckets.append(tuple(cur))
+        self.by_tag = {}
+        for i, (_, _, tag) in enumerate(self.buckets):
+            self.by_tag.setdefault(tag, []).append(i)
+        self.handles = []
+        self.launched = set()
+
+    def ready(self, tag):
+        for i in self.by_tag.get(tag, []):
+            if i in self.launched:
+                continue
+            s, e, _ = self.buckets[i]
+            self.handles.append(dist.all_reduce(self.flat[s:e], op=dist.ReduceOp.SUM,
+                                                group=self.group, async_op=True))
+            self.launched.add(i)
+
+    def finish(self):
+        for i, (s, e, _) in enumerate(self.buckets):
+            if i not in self.launched:   # groups that never reported (defensive)
+                self.handles.append(dist.all_reduce(self.flat[s:e], op=dist.ReduceOp.SUM,
+                                                    group=self.group, async_op=True))
+        for h in self.handles:
+            h.wait()
+        self.handles, self.launched = [], set()
+
+
+class FusedTrainer:
+    """One optimiser step of the FastSpeech2 train path on this rank's shard of the batch."""
+
+    def __init__(self, model, loss_weights=(1.0,) * 6, lr=1e-4, betas=(0.9, 0.999), eps=1e-8,
+                 weight_decay=1e-2, bucket_bytes=32 << 20):
+        self.model = model
+        self.eng = model.engine()
+        self.opt = FusedAdamW(model, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
+        self.weights = tuple(float(w) for w in loss_weights)
+        self.world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+        self.bucketer = None
+        if self.world > 1:
+            self.bucketer = GradBucketer(model._gflat, model.group_ranges(), bucket_bytes)
+            self.eng.on_grads_ready = self.bucketer.ready
+        self.seed = 0
+
+    def step(self, batch, intensity, mel_len_max=None):
+        (phoneme, spk_ids, phon_len, mel_tgt, pitch_tgt, energy_tgt, duration_tgt, mel_len) = batch[:8]
+        m = self.model
+        self.seed += 1
+        m._gflat.zero_()
+        out, ctx = self.eng.forward(phoneme, spk_ids, duration_tgt, pitch_tgt, energy_tgt,
+                                    intensity=intensity, training=True, seed=self.seed,
+                                    mel_len_max=mel_len_max if mel_len_max is not None
+                                    else mel_tgt.shape[1])
+        mel, post, pd, pp, avg_p, pe, avg_e, _ = out
+        loss, grads = fused_loss(mel, post, pd, pp.view(pd.shape), pe.view(pd.shape), mel_tgt,
+                                 duration_tgt, avg_p.view(pd.shape), avg_e.view(pd.shape), mel_len,
+                                 phon_len, self.weights)
+        self.eng.backward(ctx, *grads)
+        if self.bucketer is not None:
+            self.bucketer.finish()
+        self.opt.step(grad_scale=1.0 / self.world)
+        return loss

@@ -1,0 +1,223 @@
+/*
+ * fs2_hip.h -- C ABI of the MI355X (gfx950) FastSpeech2-with-emotion-intensity train path.
+ *
+ * The reference (Orca0917/fine-grained-emotional-control-of-tts) has no native boundary:
+ * its hot path is Python calling speechbrain/torch ops.  Each entry point below replaces
+ * one op site of that path ("op-site inventory" K1..K17) and cites the
+ * reference line(s) it stands in for.  Conventions (identical for every function):
+ *
+ *   - all tensor arguments are DEVICE pointers; sizes are explicit ints; row pitches are in
+ *     ELEMENTS; nothing is allocated, freed or synchronised inside a call;
+ *   - `dtype` selects the activation storage type: FS2_F32 (parity mode) or FS2_BF16;
+ *     statistics, losses, gradients of parameters and optimiser state are always fp32;
+ *   - `stream` is a hipStream_t passed as void*; all work is stream-ordered (graph-capturable);
+ *   - return value: 0 on success, a hipError_t code (>0) on launch failure, or a negative
+ *     FS2_E* code for an invalid argument (checked on the host before any launch).
+ *
+ * Row layout of every token tensor: row m = b*T + t (utterance-major, padded to T), channels
+ * contiguous -- the (B, T_max, hidden) layout of the reference (model.py:335-431).
+ */
+#ifndef FS2_HIP_H
+#define FS2_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FS2_F32 0
+#define FS2_BF16 1
+
+#define FS2_EINVAL (-1)  /* inconsistent sizes / pointers                                  */
+#define FS2_EALIGN (-2)  /* pitch or pointer not 16-byte aligned where the kernel needs it */
+
+/* ------------------------------------------------------------------------------------------
+ * Generalised MFMA GEMM:  C[m][n] = epilogue( sum_k A(m,k) * B(k,n) )
+ * Replaces: every nn.Linear / nn.Conv1d / bmm of the FFT blocks, variance predictors,
+ * concat projection, mel linear and PostNet, forward and backward (K4, K6-K8, K12, K13, K16);
+ * SB Conv1d "same"+reflect (App. A.1) is folded into the operand loader ("implicit conv").
+ * ------------------------------------------------------------------------------------------ */
+typedef struct fs2_gemm_desc {
+  int M, N, K;          /* problem size; K is the iterated reduction length                  */
+  int kvalid;           /* MN-major operands: k rows >= kvalid read as zero (<=0: = K)       */
+  int mvalid, nvalid;   /* epilogue stores only m < mvalid, n < nvalid (<=0: M / N)          */
+  int dtype;            /* FS2_F32 | FS2_BF16 : A, B and activation-typed outputs            */
+  const void* A; int64_t lda; int a_kmajor;   /* 1: A(m,k)=A[m*lda+k]   0: A[k*lda+m]       */
+  const void* B; int64_t ldb; int b_kmajor;   /* 1: B(k,n)=B[n*ldb+k]   0: B[k*ldb+n]       */
+  /* implicit 1-D convolution over the token axis (SB Conv1d, reflect "same" padding):
+   *   1: A fwd   A(m=(b,t), k=(j,c)) = X[b, reflect(t+j-P), c]                  (a_kmajor)
+   *   2: A dgrad A(m=(b,s), k=(j,o)) = sum_{t: reflect(t+j-P)=s} dY[b, t, o]     (a_kmajor)
+   *   3: B wgrad B(k=(b,t), n=(j,c)) = X[b, reflect(t+j-P), c]                  (!b_kmajor)
+   * P = (conv_kw-1)/2, conv_c = channels per tap, conv_t = tokens per utterance.          */
+  int conv_mode, conv_t, conv_kw, conv_c;
+  void* C; int64_t ldc; int c_fp32;           /* output; c_fp32: float output else dtype     */
+  int c_conv_kw;        /* >0: output column n=(j,c) is stored at c*c_conv_kw + j            */
+  const float* bias;    /* [N]       v += bias[n]                                             */
+  int relu;             /*           v = max(v, 0)                                            */
+  const void* gate; int64_t ldg;              /* dtype [M][ldg]: v *= (gate > 0)             */
+  const float* row_scale;                     /* [M]: v *= row_scale[m]                      */
+  const void* residual; int64_t ldr;          /* dtype [M][ldr]: v += residual               */
+  const float* row_scale_post;                /* [M]: v *= row_scale_post[m]                 */
+  int accumulate;       /* fp32 output only: C += v (split_k > 1 implies atomic accumulate)   */
+  int split_k;          /* >1: K split over blockIdx.z, fp32 atomics into C                  */
+  /* batched: z in [0,batch): offset(z) = (z / batch_div)*s1 + (z % batch_div)*s2 (elements) */
+  int batch, batch_div;
+  int64_t sA1, sA2, sB1, sB2, sC1, sC2, sR1, sR2;
+} fs2_gemm_desc;
+
+int fs2_gemm(const fs2_gemm_desc* d, void* stream);
+
+/* column sums: out[n] (+)= sum_m X[m][n]   (bias gradients; SB Linear/Conv1d bias, K16) */
+int fs2_colsum(const void* X, int64_t ldx, int M, int N, int dtype, float* out, int accumulate,
+               float* workspace, void* stream);
+int64_t fs2_colsum_workspace_floats(int M, int N);
+
+/* ------------------------------------------------------------------------------------------
+ * LayerNorm with fused residual / dropout / tanh / mask (K5, K8, K13)
+ *   s = x + drop(r; p_r)          (r optional; SB TransformerEncoderLayer, App. A.2)
+ *   y = LN(s)*gamma + beta         (eps per call: 1e-6 FFT, 1e-5 predictors/PostNet)
+ *   y = tanh(y) (opt) ; y = drop(y; p_o) ; y *= row_mask (opt) ; y += post_add (opt)
+ * ------------------------------------------------------------------------------------------ */
+int fs2_ln_fwd(const void* x, int64_t ldx, const void* r, int64_t ldr, float p_r, uint32_t salt_r,
+               void* s_out, const float* gamma, const float* beta, float eps, int do_tanh,
+               float p_o, uint32_t salt_o, const float* row_mask, const void* post_add,
+               int64_t ldp, void* y, int64_t ldy, float* mean, float* rstd, int M, int D,
+               int dtype, uint32_t seed, void* stream);
+
+/* backward of fs2_ln_fwd; dgamma/dbeta (+)= column sums (fp32).  ds = dL/ds (optionally
+ * gated by (s > 0) for a ReLU that produced s), dr = ds * dropmask_r / (1 - p_r).        */
+int fs2_ln_bwd(const void* dy, int64_t lddy, const void* s, int64_t lds, const float* mean,
+               const float* rstd, const float* gamma, const float* beta, int do_tanh, float p_o,
+               uint32_t salt_o, const float* row_mask, int relu_gate_in, void* ds, int64_t ldds,
+               void* dr, float p_r, uint32_t salt_r, float* dgamma, float* dbeta, int M, int D,
+               int dtype, uint32_t seed, float* workspace, void* stream);
+int64_t fs2_ln_workspace_floats(int M, int D);
+
+/* ------------------------------------------------------------------------------------------
+ * Attention softmax over materialised scores, with the reference's key masking
+ * (model.py:338-343 / 414-419 + key_padding_mask; head-major tiling quirk):
+ *   batch z = b*H + h masks key k iff key_pad[b][k] || key_pad[(b*H+h) % B][k].
+ * S: fp32 [z][Tq][ldt]; P, Pd: dtype [z][Tq][ldt] (softmax and dropped softmax, zero-padded
+ * to ldt); scale applied to S before the softmax (torch MHA q-scaling).
+ * ------------------------------------------------------------------------------------------ */
+int fs2_softmax_fwd(const float* S, const uint8_t* key_pad, int B, int H, int Tq, int Tk,
+                    int ldt, float scale, float p_drop, uint32_t seed, uint32_t salt, void* P,
+                    void* Pd, int dtype, void* stream);
+/* dS = scale * P * (dP - rowsum(P*dP)) with dP = dPd * dropmask / (1-p). dPd fp32.        */
+int fs2_softmax_bwd(const float* dPd, const void* P, int B, int H, int Tq, int Tk, int ldt,
+                    float scale, float p_drop, uint32_t seed, uint32_t salt, void* dS, int dtype,
+                    void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Token embedding + positional encoding + pad mask (K1, K2; model.py:331-337)
+ *   X[m] = (E[tok[m]] + pe[t]) * (tok[m] != pad);  keep[m] = (tok[m] != pad)
+ * ------------------------------------------------------------------------------------------ */
+int fs2_embed_fwd(const int64_t* tokens, const float* table, const float* pe, int pad_idx,
+                  int B, int T, int D, void* X, float* keep, int dtype, void* stream);
+/* dTable[v] (+)= sum_{m: tok[m]==v} dX[m] * keep[m]   (deterministic, one block per row)   */
+int fs2_embed_bwd(const int64_t* tokens, const void* dX, const float* keep, int M, int D,
+                  int V, float* dtable, int dtype, void* stream);
+
+/* key padding masks: from tokens (tok==pad) or from lengths (t >= len)                    */
+int fs2_keypad_from_tokens(const int64_t* tokens, int pad_idx, int M, uint8_t* key_pad,
+                           void* stream);
+int fs2_keypad_from_lengths(const int64_t* lens, int B, int T, uint8_t* key_pad, float* keep,
+                            void* stream);
+
+/* concat [feats, spk_emb[spk[b]], intensity, 0-pad] (model.py:352-358) -> cat [M][ldc]    */
+int fs2_concat_fwd(const void* feats, const float* spk_table, const int64_t* spk,
+                   const float* intensity, int B, int T, int D, int E, void* cat, int ldc,
+                   int dtype, void* stream);
+/* dSpk[spk[b]] (+)= sum_t dcat[b,t,D:2D]                                                  */
+int fs2_concat_bwd_spk(const void* dcat, int ldc, const int64_t* spk, int B, int T, int D,
+                       int n_spk, float* dspk, int dtype, void* stream);
+
+/* rows: X[m][:] *= keep[m]   (in place)                                                   */
+int fs2_mask_rows(void* X, int64_t ldx, const float* keep, int M, int D, int dtype, void* stream);
+
+/* predictor head: y[m] = (dot(u[m], w) + b) * scale (SB DurationPredictor.linear, App. A.7) */
+int fs2_rowdot_fwd(const void* u, int64_t ldu, const float* w, const float* b, float scale, int M,
+                   int D, void* y, int dtype, void* stream);
+/* du = dy*scale*w ; dw (+)= sum_m dy*scale*u ; db (+)= sum_m dy*scale                     */
+int fs2_rowdot_bwd(const void* dy, const void* u, int64_t ldu, const float* w, float scale, int M,
+                   int D, void* du, float* dw, float* db, int dtype, float* workspace,
+                   void* stream);
+
+/* average_over_durations (SB, App. A.10; model.py:383,397): mean of NON-ZERO frame values
+ * per phoneme via double-accumulated prefix sums (replicates torch CPU cumsum).            */
+int fs2_avg_over_durations(const float* values, int Tm_in, const int64_t* durs, int B, int Tp,
+                           float* avg, float* workspace, void* stream);
+int64_t fs2_avg_workspace_floats(int B, int Tm_in);
+
+/* pitch/energy embedding conv (SB Conv1d(1->D, k, reflect), model.py:226-240,384-403) fused
+ * with the residual add:  out[b,t,:] = base[b,t,:] + bias + sum_j W[:, 0, j] a[b, refl(t+j-P)] */
+int fs2_embed1d_fwd(const void* base, const float* a, const float* W, const float* bias, int B,
+                    int T, int D, int KW, void* out, int dtype, void* stream);
+/* dW[o][j] (+)= sum dOut[b,t,o] a[b,refl(t+j-P)]; dbias (+)= sum dOut                     */
+int fs2_embed1d_bwd(const void* dout, const float* a, int B, int T, int D, int KW, float* dW,
+                    float* dbias, int dtype, float* workspace, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * LengthRegulator (SB upsample, App. A.9; model.py:406-413), K11.
+ *   n[b,p] = (int64)(pace * (float)d[b,p])  (float32 product, truncation == .long())
+ *   mel_len[b] = sum_p n[b,p];  frame_src[b,t] = p with cum[p-1] <= t < cum[p], -1 past mel_len
+ * The integer expansion is bit-exact to repeat_interleave.  d: int64 (teacher forcing) or
+ * float (predicted, already clamp(expm1(.),0)) selected by d_is_float.
+ * ------------------------------------------------------------------------------------------ */
+int fs2_lr_index(const void* durs, int d_is_float, float pace, int B, int Tp, int Tm,
+                 int64_t* mel_len, int32_t* cum, int32_t* frame_src, void* stream);
+/* Y[b,t] = (X[b, frame_src[b,t]] + pe[t]) * keep[b,t]  (fused decoder PE add, model.py:422-423) */
+int fs2_lr_gather(const void* X, const int32_t* frame_src, const float* pe, int B, int Tp,
+                  int Tm, int D, void* Y, float* keep, int dtype, void* stream);
+/* dX[b,p] = sum_{t in segment p} dY[b,t] * keep[b,t]                                      */
+int fs2_lr_scatter(const void* dY, const int32_t* cum, const float* keep, int B, int Tp, int Tm,
+                   int D, void* dX, int dtype, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Loss (loss.py:62-186), K14/K15.  loss_out[8] fp32 = {total, ssim, mel, postnet, dur, pitch,
+ * energy, ssim_gradient_scale}; gradients are written for a unit upstream gradient.
+ * ------------------------------------------------------------------------------------------ */
+typedef struct fs2_loss_desc {
+  int B, Tm, Tp, NM;           /* Tm: padded frames of predictions AND target               */
+  int dtype;                   /* predictions' dtype                                         */
+  const void* mel_out; const void* postnet_out;       /* [B][Tm][NM]                       */
+  const void* log_dur; const void* pitch_pred; const void* energy_pred;  /* [B][Tp]         */
+  const float* mel_tgt;                               /* [B][Tm][NM]                        */
+  const int64_t* dur_tgt;                             /* [B][Tp]                            */
+  const float* pitch_avg; const float* energy_avg;    /* [B][Tp] (average_over_durations)   */
+  const int64_t* mel_len; const int64_t* phon_len;    /* [B]                                */
+  float w_ssim, w_mel, w_post, w_dur, w_pitch, w_energy;
+  float* loss_out;                                     /* [8]                                */
+  void* d_mel_out; void* d_postnet_out;               /* dtype, [B][Tm][NM]                 */
+  void* d_log_dur; void* d_pitch; void* d_energy;     /* dtype, [B][Tp]                     */
+  float* workspace;                                    /* fs2_loss_workspace_floats()        */
+} fs2_loss_desc;
+int fs2_loss_fwd_bwd(const fs2_loss_desc* d, void* stream);
+int64_t fs2_loss_workspace_floats(int B, int Tm, int NM);
+
+/* ------------------------------------------------------------------------------------------
+ * Optimiser + weight preparation (K17; train.py:232 torch.optim.AdamW defaults).
+ * ------------------------------------------------------------------------------------------ */
+/* torch AdamW (single-tensor algorithm, fp32), grads scaled by grad_scale (1/world_size).
+ * c_* constants are computed on the host exactly as torch does (see fastspeech2/optim.py). */
+int fs2_adamw(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+              float decay_mul, float one_minus_beta1, float beta2, float one_minus_beta2,
+              float step_size, float bc2_sqrt, float eps, float grad_scale, void* stream);
+
+/* torch weight W[O][C][KW] (fp32) -> fwd copy Wf[O][KW][C] and dgrad copy Wb[C][KW][O]
+ * in dtype, each with row pitch padded to ldf / ldb elements (zeros in the pad).          */
+int fs2_weight_prep(const float* W, int O, int C, int KW, void* Wf, int ldf, void* Wb, int ldb,
+                    int dtype, void* stream);
+
+/* utilities */
+int fs2_fill(void* X, int64_t n, float value, int dtype, void* stream);
+/* X[i] += alpha * Y[i] over n elements of dtype                                           */
+int fs2_add(void* X, const void* Y, int64_t n, float alpha, int dtype, void* stream);
+int fs2_cast(const void* src, int src_dtype, void* dst, int dst_dtype, int64_t n, void* stream);
+const char* fs2_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FS2_HIP_H */
