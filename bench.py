@@ -1,0 +1,155 @@
+"""Benchmark: train mel-frames/sec of the FastSpeech2-with-emotion-intensity train step
+(BASELINE.json metric) at B=32 utterances per GPU, 80-bin mel, default model dims, bf16.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
+
+N>1 is launched by torch.distributed.run (one process per GPU, RCCL all-reduce).  A step is
+forward + loss + backward + bucketed all-reduce + AdamW over one synthetic EmoV-DB-shaped
+batch per rank, inputs resident in HBM.  Prints ONE JSON line on rank 0.
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "fine-grained-emotional-control-of-tts_amd"))
+sys.path.insert(0, ROOT)
+
+import torch
+import torch.distributed as dist
+
+MFMA_BF16_PEAK_TFLOPS = 2500.0   # MI355X dense bf16 (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--max-shape", action="store_true", help="all T_phon=200, d=5 (T_mel=1000)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-utts", type=int, default=2)
+    return ap.parse_args()
+
+
+def cpu_baseline(cfg_all, args):
+    """Oracle (op-for-op PyTorch-CPU fp32 restatement of the reference train step) on a bounded
+    sample of the same workload: ``cpu_utts`` utterances, 1 warm-up + 2 timed steps."""
+    from oracle.fs2_oracle import FastSpeech2Oracle, LossOracle, train_step
+    from fastspeech2.synthetic import make_batch, as_tuple
+    cores = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(cores)
+    torch.manual_seed(0)
+    model = FastSpeech2Oracle(**cfg_all["model"]["fastspeech2"], n_speakers=4).train()
+    crit = LossOracle(**cfg_all["loss"])
+    opt = torch.optim.AdamW(model.parameters(), lr=cfg_all["train"]["learning_rate"])
+    b = make_batch(B=args.cpu_utts, seed=1000, max_shape=args.max_shape)
+    bt, inten = as_tuple(b)
+    train_step(model, crit, opt, bt, inten)
+    ts = []
+    for _ in range(2):
+        t0 = time.perf_counter()
+        train_step(model, crit, opt, bt, inten)
+        ts.append(time.perf_counter() - t0)
+    t = sorted(ts)[len(ts) // 2]
+    frames = int(b["mel_len"].sum())
+    return {"value": frames / t, "unit": "mel-frames/s", "cores": cores, "kind": "port",
+            "sample": f"{args.cpu_utts} utterances of the same synthetic workload "
+                      f"({frames} valid mel frames, T_mel_max={b['mel'].shape[1]}), fp32, dropout on, "
+                      f"median of 2 steps after 1 warm-up; oracle/fs2_oracle.py"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from fastspeech2 import load_config
+    from fastspeech2.model import FastSpeech2
+    from fastspeech2.train import FusedTrainer
+    from fastspeech2.synthetic import make_batch, as_tuple
+    from fastspeech2.timing import KernelTimer
+    from fastspeech2.flops import train_flops
+    cfg_all = load_config()
+    dt = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    torch.manual_seed(0)
+    model = FastSpeech2(**cfg_all["model"]["fastspeech2"], n_speakers=4, act_dtype=dt).cuda().train()
+    trainer = FusedTrainer(model, lr=cfg_all["train"]["learning_rate"])
+    b = make_batch(B=args.batch, seed=rank, max_shape=args.max_shape, device="cuda")
+    bt, inten = as_tuple(b)
+    Tm = b["mel"].shape[1]
+    Tp = b["phoneme"].shape[1]
+    frames_local = int(b["mel_len"].sum())
+    for _ in range(args.warmup):
+        trainer.step(bt, inten, mel_len_max=Tm)
+    torch.cuda.synchronize()
+    timer = KernelTimer()
+    trainer.eng.timer = timer
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = trainer.step(bt, inten, mel_len_max=Tm)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    trainer.eng.timer = None
+    ks = timer.summary()
+    tmax = torch.tensor([elapsed], device="cuda")
+    ftot = torch.tensor([frames_local], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        dist.all_reduce(ftot, op=dist.ReduceOp.SUM)
+    elapsed = float(tmax.item())
+    frames_all = float(ftot.item())
+    loss_v = loss.float().cpu().tolist()
+    if rank == 0:
+        c = model.cfg
+        D, F, KW = c.dec_d_model, c.dec_ffn_dim, c.ffn_cnn_kernel_size_list[0]
+        n, ms = ks.get("ffn_conv1_fwd.decoder", (0, float("nan")))
+        kflop = 2.0 * (args.batch * Tm) * F * (KW * D)
+        achieved = kflop / (ms * 1e-3) / 1e12 if n else None
+        step_ms = elapsed / args.steps * 1e3
+        step_tflops = train_flops(c, args.batch, Tp, Tm) * world / (step_ms * 1e-3) / 1e12
+        line = {
+            "metric": "train mel-frames/sec at B=32, 80-bin mel; 1/2/4/8 MI355X",
+            "value": frames_all * args.steps / elapsed,
+            "unit": "mel-frames/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": step_ms,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": args.dtype, "data": "synthetic (seeded EmoV-DB-shaped batches, random-init weights)",
+            "config": {"workload": f"FastSpeech2 train step (fwd+loss+bwd+allreduce+AdamW), "
+                                   f"B={args.batch}/GPU, T_phon_max={Tp}, T_mel_max={Tm}, "
+                                   f"D=384 F=1536 6+6 FFT layers, 80 mels"
+                                   + (", max-shape" if args.max_shape else ""),
+                       "global_batch": args.batch * world, "seq_len": Tm,
+                       "valid_mel_frames_per_step": frames_all, "parallelism": f"dp{world}"},
+            "roofline": {"bound": "mfma", "kernel": "decoder FFN conv1 (k=9) implicit-GEMM fwd",
+                         "achieved": achieved, "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": (achieved / MFMA_BF16_PEAK_TFLOPS) if achieved else None,
+                         "traffic": None, "launches": n, "avg_ms": ms,
+                         "flop_per_launch": kflop},
+            "step_mfma_frac": step_tflops / (MFMA_BF16_PEAK_TFLOPS * world),
+            "kernel_ms": {k: v[1] for k, v in ks.items()},
+            "loss_total_last": loss_v[0],
+        }
+        if not args.no_cpu_baseline and world == 1:
+            line["cpu_baseline"] = cpu_baseline(cfg_all, args)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -8,10 +8,11 @@
 //   attention bmm's (S = Q K^T, O = P V, dP, dQ, dK, dV) through the batch strides.
 //
 // Tile 128x128 per 256-thread workgroup (4 waves as 2x2, 64x64 per wave = 4x4 MFMA
-// 16x16 tiles).  The LDS image of BOTH operands is always K-major [128 rows][128 bytes]
-// with a 16-byte-chunk XOR swizzle (chunk ^= row & 7): conflict-free ds_read_b128 for the
-// bf16 fragments.  MN-major operands are transposed while being written to LDS (4 k-rows x
-// one 16-byte mn-chunk per thread).  bf16 uses v_mfma_f32_16x16x32_bf16, fp32 (parity
+// 16x16 tiles).  K-major operands are staged as [128 rows][128 bytes] with a 16-byte-chunk
+// XOR swizzle (chunk ^= row & 7): conflict-free ds_read_b128 fragments.  MN-major operands
+// (token-major activations in the weight-gradient GEMMs and the attention bmm's) are staged
+// untransposed as [BK k-rows][128] and read through ds_read_b64_tr_b16, the gfx950 LDS
+// transpose read, so no lane ever shuffles data.  bf16 uses v_mfma_f32_16x16x32_bf16, fp32 (parity
 // mode) the exact-f32 v_mfma_f32_16x16x4_f32; both share the 16x16 C/D layout
 // (col = lane&15, row = 4*(lane>>4) + r), so the epilogue is common.
 // Register-staged double buffering: the next K-tile's global loads are in flight while
@@ -121,61 +122,91 @@ __device__ __forceinline__ void store_kmajor(char* lds, const u32x4 (&st)[4]) {
   }
 }
 
-// ---- MN-major tile loader: source rows are k, columns mn (mn contiguous) ----------------
-// bf16: kb = tid>>4 (4 k-rows each), mc = tid&15 (8 mn per chunk)
-// fp32: kb = tid>>5,                  mc = tid&31 (4 mn per chunk)
+// ---- MN-major tile: LDS image [BK k-rows][128 mn] (row = 256 B bf16 / 512 B fp32) -------------
+// Stored untransposed (16-byte chunks copied as loaded); bf16 fragments come out through the
+// gfx950 hardware-transpose read ds_read_b64_tr_b16.  Chunk swizzle per k-row:
+//   bf16: phys = c ^ (2*(k&3) + 8*((k>>3)&1))  -> the 8 rows one 32-lane half of a tr-read
+//         touches land on 16 distinct 16-byte slots (conflict-free)
+//   fp32: phys = c ^ (4*(k&1))                  -> ds_read_b32 rows k, k+1 on disjoint banks
+template <typename T>
+__device__ __forceinline__ int mn_swz(int k) {
+  if constexpr (sizeof(T) == 2) return 2 * (k & 3) + 8 * ((k >> 3) & 1);
+  else return 4 * (k & 1);
+}
+
 template <typename T>
 __device__ __forceinline__ void load_mnmajor(u32x4 (&st)[4], const char* base, long ld, int mn0,
                                              int nmn, int k0, int kend, const GemmP& p,
                                              bool conv3) {
   constexpr int ES = Cfg<T>::ES, EPC = Cfg<T>::EPC;
+  constexpr int CPR = 128 / EPC;  // chunks per k-row: 16 (bf16) / 32 (fp32)
   const int tid = threadIdx.x;
-  const int kb = (ES == 2) ? (tid >> 4) : (tid >> 5);
-  const int mc = (ES == 2) ? (tid & 15) : (tid & 31);
-  const int mn = mn0 + mc * EPC;
-  int j = 0, c = mn;
-  if (conv3) { j = mn / p.conv_c; c = mn - j * p.conv_c; }
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int k = k0 + kb * 4 + q;
+  for (int i = 0; i < 4; ++i) {
+    const int id = tid + 256 * i;
+    const int kr = id / CPR, c = id - kr * CPR;
+    const int k = k0 + kr;
+    const int mn = mn0 + c * EPC;
     u32x4 v = {0u, 0u, 0u, 0u};
     if (k < kend && mn < nmn) {
       long srow = k;
+      int col = mn;
       if (conv3) {
+        const int j = mn / p.conv_c;
+        col = mn - j * p.conv_c;
         const int b = k / p.conv_t, t = k - b * p.conv_t;
         srow = (long)b * p.conv_t + reflect_idx(t + j - p.conv_p, p.conv_t);
       }
-      v = ld16(base + (srow * ld + c) * ES);
+      v = ld16(base + (srow * ld + col) * ES);
     }
-    st[q] = v;
+    st[i] = v;
   }
 }
 
 template <typename T>
 __device__ __forceinline__ void store_mnmajor(char* lds, const u32x4 (&st)[4]) {
-  constexpr int ES = Cfg<T>::ES;
+  constexpr int EPC = Cfg<T>::EPC;
+  constexpr int CPR = 128 / EPC, RB = 128 * sizeof(T);
   const int tid = threadIdx.x;
-  if constexpr (ES == 2) {
-    const int kb = tid >> 4, mc = tid & 15;
-    const int kc = kb >> 1, boff = (kb & 1) * 8;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int w = e >> 1, sh = (e & 1) * 16;
-      const unsigned x0 = (st[0][w] >> sh) & 0xffffu, x1 = (st[1][w] >> sh) & 0xffffu;
-      const unsigned x2 = (st[2][w] >> sh) & 0xffffu, x3 = (st[3][w] >> sh) & 0xffffu;
-      u32x2 val = {x0 | (x1 << 16), x2 | (x3 << 16)};
-      const int row = mc * 8 + e;
-      *(u32x2*)(lds + row * 128 + ((kc ^ (row & 7)) << 4) + boff) = val;
-    }
-  } else {
-    const int kb = tid >> 5, mc = tid & 31;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      u32x4 val = {st[0][e], st[1][e], st[2][e], st[3][e]};
-      const int row = mc * 4 + e;
-      *(u32x4*)(lds + row * 128 + ((kb ^ (row & 7)) << 4)) = val;
-    }
+  for (int i = 0; i < 4; ++i) {
+    const int id = tid + 256 * i;
+    const int kr = id / CPR, c = id - kr * CPR;
+    *(u32x4*)(lds + kr * RB + ((c ^ mn_swz<T>(kr)) << 4)) = st[i];
   }
+}
+
+// ---- fragment readers -------------------------------------------------------------------
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+// bf16 16x16x32 operand, lane l: rows (mn) r0 + (l&15), k = s*32 + 8*(l>>4) + j, j = 0..7
+__device__ __forceinline__ bf16x8 frag_bf16_kmajor(const char* lds, int r0, int s, int lane) {
+  const int r = r0 + (lane & 15);
+  const int ch = s * 4 + (lane >> 4);
+  return *(const bf16x8*)(lds + r * 128 + ((ch ^ (r & 7)) << 4));
+}
+__device__ __forceinline__ bf16x8 frag_bf16_mnmajor(const char* lds, int r0, int s, int lane) {
+  const int li = lane & 15, g = lane >> 4, q = li >> 2, p = li & 3;
+  const int m = r0 + 4 * p;             // this lane supplies columns m..m+3 of k-row (.., q)
+  const int c = m >> 3, boff = (m & 7) * 2;
+  const int k1 = s * 32 + 8 * g + q, k2 = k1 + 4;
+  const char* a1 = lds + k1 * 256 + ((c ^ mn_swz<bf16>(k1)) << 4) + boff;
+  const char* a2 = lds + k2 * 256 + ((c ^ mn_swz<bf16>(k2)) << 4) + boff;
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a1);
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a2);
+  typedef __attribute__((ext_vector_type(8))) short s16x8;
+  const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+// fp32 16x16x4 operand, lane l: row (mn) r0 + (l&15), k = s*4 + (l>>4)
+__device__ __forceinline__ float frag_f32_kmajor(const char* lds, int r0, int s, int lane) {
+  const int r = r0 + (lane & 15);
+  return *(const float*)(lds + r * 128 + ((s ^ (r & 7)) << 4) + (lane >> 4) * 4);
+}
+__device__ __forceinline__ float frag_f32_mnmajor(const char* lds, int r0, int s, int lane) {
+  const int m = r0 + (lane & 15), k = s * 4 + (lane >> 4);
+  return *(const float*)(lds + k * 512 + (((m >> 2) ^ mn_swz<float>(k)) << 4) + (m & 3) * 4);
 }
 
 template <typename T, bool AK, bool BKM>
@@ -254,13 +285,12 @@ __global__ void __launch_bounds__(NT) gemm_kernel(GemmP p) {
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         bf16x8 af[4], bfr[4];
-        const int ch = s * 4 + (lane >> 4);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const int ra = wm * 64 + i * 16 + (lane & 15);
-          af[i] = *(const bf16x8*)(la + ra * 128 + ((ch ^ (ra & 7)) << 4));
-          const int rbw = wn * 64 + i * 16 + (lane & 15);
-          bfr[i] = *(const bf16x8*)(lb + rbw * 128 + ((ch ^ (rbw & 7)) << 4));
+          af[i] = AK ? frag_bf16_kmajor(la, wm * 64 + i * 16, s, lane)
+                     : frag_bf16_mnmajor(la, wm * 64 + i * 16, s, lane);
+          bfr[i] = BKM ? frag_bf16_kmajor(lb, wn * 64 + i * 16, s, lane)
+                       : frag_bf16_mnmajor(lb, wn * 64 + i * 16, s, lane);
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -272,13 +302,12 @@ __global__ void __launch_bounds__(NT) gemm_kernel(GemmP p) {
 #pragma unroll
       for (int s = 0; s < 8; ++s) {
         float af[4], bfr[4];
-        const int eo = (lane >> 4) * 4;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const int ra = wm * 64 + i * 16 + (lane & 15);
-          af[i] = *(const float*)(la + ra * 128 + ((s ^ (ra & 7)) << 4) + eo);
-          const int rbw = wn * 64 + i * 16 + (lane & 15);
-          bfr[i] = *(const float*)(lb + rbw * 128 + ((s ^ (rbw & 7)) << 4) + eo);
+          af[i] = AK ? frag_f32_kmajor(la, wm * 64 + i * 16, s, lane)
+                     : frag_f32_mnmajor(la, wm * 64 + i * 16, s, lane);
+          bfr[i] = BKM ? frag_f32_kmajor(lb, wn * 64 + i * 16, s, lane)
+                       : frag_f32_mnmajor(lb, wn * 64 + i * 16, s, lane);
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i)

@@ -16,6 +16,7 @@
 namespace {
 
 constexpr int WIN = 11;
+constexpr int LOSS_CHUNK = 8192;  // mel elements per MSE block
 constexpr float C1 = 0.01f * 0.01f, C2 = 0.03f * 0.03f;
 
 struct LossP {
@@ -27,6 +28,8 @@ struct LossP {
   float* loss_out; void* d_mel; void* d_post; void* d_dur; void* d_pitch; void* d_energy;
   // workspace carve
   float* per_b;      // [5][B]
+  float* part_mel;   // [2][B][nch] chunk sums of squared mel / postnet errors
+  int nch;
   float* stats;      // [8][B] ymax, ymin, hmax, hmin, cnt_hmax, cnt_hmin, S1, S2
   float* ssim_part;  // [B][nblk_pix]
   float* dmap;       // [3][B][npix]
@@ -89,7 +92,8 @@ __global__ void __launch_bounds__(256) mse_kernel(LossP p) {
   T* dpo = (T*)p.d_post + (long)b * Tm * NM;
   const float cm = 2.f * p.w_mel / ((float)L * NM * B), cp = 2.f * p.w_post / ((float)L * NM * B);
   float s_mel = 0.f, s_post = 0.f;
-  for (int i = threadIdx.x; i < Tm * NM; i += blockDim.x) {
+  const int i0 = blockIdx.y * LOSS_CHUNK, i1 = min(Tm * NM, i0 + LOSS_CHUNK);
+  for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
     const bool valid = (i / NM) < L;
     const float y = mt[i];
     const float d1 = to_f(mo[i]) - y, d2 = to_f(po[i]) - y;
@@ -97,6 +101,13 @@ __global__ void __launch_bounds__(256) mse_kernel(LossP p) {
     dmo[i] = from_f<T>(valid ? cm * d1 : 0.f);
     dpo[i] = from_f<T>(valid ? cp * d2 : 0.f);
   }
+  s_mel = block_sum(s_mel, sh);
+  s_post = block_sum(s_post, sh);
+  if (threadIdx.x == 0) {
+    p.part_mel[(long)b * p.nch + blockIdx.y] = s_mel;
+    p.part_mel[(long)(B + b) * p.nch + blockIdx.y] = s_post;
+  }
+  if (blockIdx.y != 0) return;
   const T* ld = (const T*)p.log_dur + (long)b * Tp;
   const T* pp = (const T*)p.pitch_pred + (long)b * Tp;
   const T* ep = (const T*)p.energy_pred + (long)b * Tp;
@@ -120,14 +131,10 @@ __global__ void __launch_bounds__(256) mse_kernel(LossP p) {
     dpi[i] = from_f<T>(vn ? cpi * e2 : 0.f);
     den[i] = from_f<T>(vn ? ce * e3 : 0.f);
   }
-  s_mel = block_sum(s_mel, sh);
-  s_post = block_sum(s_post, sh);
   s_dur = block_sum(s_dur, sh);
   s_pi = block_sum(s_pi, sh);
   s_en = block_sum(s_en, sh);
   if (threadIdx.x == 0) {
-    p.per_b[0 * B + b] = s_mel / ((float)L * NM);
-    p.per_b[1 * B + b] = s_post / ((float)L * NM);
     p.per_b[2 * B + b] = s_dur / (float)Pl;
     p.per_b[3 * B + b] = s_pi / (float)Ln;
     p.per_b[4 * B + b] = s_en / (float)Ln;
@@ -220,11 +227,32 @@ __global__ void __launch_bounds__(256) ssim_map_kernel(LossP p) {
 }
 
 // ---- 4: finalise all loss values ----------------------------------------------------------
-__global__ void finalize_kernel(LossP p) {
-  if (threadIdx.x != 0) return;
+__global__ void __launch_bounds__(256) finalize_kernel(LossP p) {
+  __shared__ double dsh[256];
   const int B = p.B;
-  double tot = 0.0;
-  for (int i = 0; i < B * p.nblk_pix; ++i) tot += p.ssim_part[i];
+  // deterministic: per-thread strided double sums, then a fixed-shape LDS tree
+  double part = 0.0;
+  for (int i = threadIdx.x; i < B * p.nblk_pix; i += 256) part += p.ssim_part[i];
+  dsh[threadIdx.x] = part;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) dsh[threadIdx.x] += dsh[threadIdx.x + w];
+    __syncthreads();
+  }
+  const double tot = dsh[0];
+  // per-utterance mel / postnet means from the chunk partials
+  for (int b = threadIdx.x; b < B; b += 256) {
+    const int L = (int)min((int64_t)p.Tm, p.mel_len[b]);
+    float sm = 0.f, sp = 0.f;
+    for (int c = 0; c < p.nch; ++c) {
+      sm += p.part_mel[(long)b * p.nch + c];
+      sp += p.part_mel[(long)(B + b) * p.nch + c];
+    }
+    p.per_b[0 * B + b] = sm / ((float)L * p.NM);
+    p.per_b[1 * B + b] = sp / ((float)L * p.NM);
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
   const float ssim_val = (float)(tot / ((double)B * p.npix));
   float l_ssim = 1.f - ssim_val;
   float gate = 1.f;
@@ -323,10 +351,10 @@ __global__ void ssim_apply_kernel(LossP p) {
 
 template <typename T>
 int run_loss(LossP& p, hipStream_t s) {
-  hipLaunchKernelGGL(mse_kernel<T>, dim3(p.B), dim3(256), 0, s, p);
+  hipLaunchKernelGGL(mse_kernel<T>, dim3(p.B, p.nch), dim3(256), 0, s, p);
   hipLaunchKernelGGL(minmax_kernel<T>, dim3(p.B), dim3(256), 0, s, p);
   hipLaunchKernelGGL(ssim_map_kernel<T>, dim3(p.nblk_pix, p.B), dim3(256), 0, s, p);
-  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, s, p);
+  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(256), 0, s, p);
   const unsigned nq = (unsigned)(((long)p.Tm * p.NM + 255) / 256);
   hipLaunchKernelGGL(ssim_grad_kernel<T>, dim3(nq, p.B), dim3(256), 0, s, p);
   hipLaunchKernelGGL(ssim_apply_kernel<T>, dim3(nq, p.B), dim3(256), 0, s, p);
@@ -338,8 +366,10 @@ void carve(LossP& p, float* ws) {
   const int B = p.B;
   p.npix = (p.Tm - (WIN - 1)) * (p.NM - (WIN - 1));
   p.nblk_pix = (p.npix + 255) / 256;
+  p.nch = (p.Tm * p.NM + LOSS_CHUNK - 1) / LOSS_CHUNK;
   float* w = ws;
   p.per_b = w; w += 5L * B;
+  p.part_mel = w; w += 2L * B * p.nch;
   p.stats = w; w += 8L * B;
   p.scal = w; w += 4;
   p.ssim_part = w; w += (long)B * p.nblk_pix;
@@ -353,7 +383,8 @@ void carve(LossP& p, float* ws) {
 extern "C" int64_t fs2_loss_workspace_floats(int B, int Tm, int NM) {
   const long npix = (long)(Tm - (WIN - 1)) * (NM - (WIN - 1));
   const long nblk = (npix + 255) / 256;
-  return 5L * B + 8L * B + 4 + B * nblk + 4 + 3L * B * npix + (long)B * Tm * NM;
+  const long nch = ((long)Tm * NM + LOSS_CHUNK - 1) / LOSS_CHUNK;
+  return 5L * B + 2L * B * nch + 8L * B + 4 + B * nblk + 4 + 3L * B * npix + (long)B * Tm * NM;
 }
 
 extern "C" int fs2_loss_fwd_bwd(const fs2_loss_desc* d, void* stream) {

@@ -158,13 +158,23 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(LnBwdP p) {
   }
 }
 
-// out[n] (+)= sum_b part[b][n]
-__global__ void reduce_partials_kernel(const float* part, int nb, int N, float* out, int accumulate) {
-  const int n = blockIdx.x * blockDim.x + threadIdx.x;
-  if (n >= N) return;
+// out[n] (+)= sum_b part[b][n]: 64 columns x 4 row-slices per block, fixed-order LDS combine
+__global__ void __launch_bounds__(256) reduce_partials_kernel(const float* part, int nb, int N,
+                                                             float* out, int accumulate) {
+  __shared__ float red[4][64];
+  const int c = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  const int n = blockIdx.x * 64 + c;
   float s = 0.f;
-  for (int b = 0; b < nb; ++b) s += part[(long)b * N + n];
-  out[n] = accumulate ? out[n] + s : s;
+  if (n < N) {
+#pragma unroll 8
+    for (int b = sl; b < nb; b += 4) s += part[(long)b * N + n];
+  }
+  red[sl][c] = s;
+  __syncthreads();
+  if (sl == 0 && n < N) {
+    const float t = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
+    out[n] = accumulate ? out[n] + t : t;
+  }
 }
 
 template <typename T>
@@ -179,8 +189,8 @@ __global__ void colsum_partial_kernel(const T* X, long ldx, int M, int N, int ro
   part[(long)blockIdx.y * N + n] = s;
 }
 
-int ln_blocks(int M) { return min(1024, max(1, (M + 15) / 16)); }
-int colsum_blocks(int M) { return min(512, max(1, (M + 63) / 64)); }
+int ln_blocks(int M) { return min(512, max(1, (M + 15) / 16)); }
+int colsum_blocks(int M) { return min(256, max(1, (M + 63) / 64)); }
 
 }  // namespace
 
@@ -230,9 +240,9 @@ extern "C" int fs2_ln_bwd(const void* dy, int64_t lddy, const void* s, int64_t l
   else return FS2_EINVAL;
   FS2_CHECK_LAUNCH();
   if (dgamma) {
-    hipLaunchKernelGGL(reduce_partials_kernel, dim3((D + 255) / 256), dim3(256), 0, st, pg, nb, D,
+    hipLaunchKernelGGL(reduce_partials_kernel, dim3((D + 63) / 64), dim3(256), 0, st, pg, nb, D,
                        dgamma, 1);
-    hipLaunchKernelGGL(reduce_partials_kernel, dim3((D + 255) / 256), dim3(256), 0, st, pb, nb, D,
+    hipLaunchKernelGGL(reduce_partials_kernel, dim3((D + 63) / 64), dim3(256), 0, st, pb, nb, D,
                        dbeta, 1);
     FS2_CHECK_LAUNCH();
   }
@@ -252,7 +262,7 @@ extern "C" int fs2_colsum(const void* X, int64_t ldx, int M, int N, int dtype, f
   else if (dtype == FS2_F32)
     hipLaunchKernelGGL(colsum_partial_kernel<float>, grid, dim3(256), 0, st, (const float*)X, ldx, M, N, rpb, workspace);
   else return FS2_EINVAL;
-  hipLaunchKernelGGL(reduce_partials_kernel, dim3((N + 255) / 256), dim3(256), 0, st, workspace, nb,
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3((N + 63) / 64), dim3(256), 0, st, workspace, nb,
                      N, out, accumulate);
   FS2_CHECK_LAUNCH();
   return 0;

@@ -23,17 +23,34 @@ __global__ void embed_fwd_kernel(const int64_t* tok, const float* table, const f
   if (d == 0) keep[m] = k;
 }
 
-// one block per vocabulary row; deterministic sequential accumulation over tokens
+// grid (V, D/64): 4 waves split the tokens; each wave ballots 64 tokens at a time and adds the
+// matching rows in token order (lane = column); fixed-order combine -> deterministic.
 template <typename T>
-__global__ void embed_bwd_kernel(const int64_t* tok, const T* dX, const float* keep, int M, int D,
-                                 float* dtable) {
+__global__ void __launch_bounds__(256) embed_bwd_kernel(const int64_t* tok, const T* dX,
+                                                        const float* keep, int M, int D,
+                                                        float* dtable) {
+  __shared__ float red[4][64];
   const int v = blockIdx.x;
-  for (int d = threadIdx.x; d < D; d += blockDim.x) {
-    float s = 0.f;
-    for (int m = 0; m < M; ++m)
-      if (tok[m] == v) s += to_f(dX[(long)m * D + d]) * keep[m];
-    dtable[(long)v * D + d] += s;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int d = blockIdx.y * 64 + lane;
+  const int per = (M + 3) / 4;
+  const int m0 = w * per, m1 = min(M, m0 + per);
+  float s = 0.f;
+  for (int base = m0; base < m1; base += 64) {
+    const int m = base + lane;
+    const bool hit = (m < m1) && (tok[m] == v);
+    unsigned long long mask = __ballot(hit);
+    while (mask) {
+      const int bit = __ffsll((long long)mask) - 1;
+      mask &= mask - 1;
+      const int mm = base + bit;
+      if (d < D) s += to_f(dX[(long)mm * D + d]) * keep[mm];
+    }
   }
+  red[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && d < D)
+    dtable[(long)v * D + d] += (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
 }
 
 __global__ void keypad_tokens_kernel(const int64_t* tok, int pad, int M, uint8_t* kp) {
@@ -68,18 +85,31 @@ __global__ void concat_fwd_kernel(const T* feats, const float* spk_table, const 
   cat[i] = from_f<T>(v);
 }
 
+// stage 1: U[b][d] = sum_t dcat[b,t,D+d]   grid (B, D/64), 4 waves split t
 template <typename T>
-__global__ void concat_bwd_spk_kernel(const T* dcat, int ldc, const int64_t* spk, int B, int T_,
-                                      int D, float* dspk) {
-  const int s = blockIdx.x;
-  const int d = blockIdx.y * blockDim.x + threadIdx.x;
-  if (d >= D) return;
+__global__ void __launch_bounds__(256) concat_bwd_utt_kernel(const T* dcat, int ldc, int T_, int D,
+                                                             float* U) {
+  __shared__ float red[4][64];
+  const int b = blockIdx.x;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int d = blockIdx.y * 64 + lane;
+  float s = 0.f;
+  if (d < D)
+    for (int t = w; t < T_; t += 4) s += to_f(dcat[((long)b * T_ + t) * ldc + D + d]);
+  red[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && d < D) U[(long)b * D + d] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+}
+// stage 2: dspk[s][d] += sum_{b: spk[b]==s} U[b][d]  (utterance order)
+__global__ void concat_bwd_spk_kernel(const float* U, const int64_t* spk, int B, int D, int n_spk,
+                                      float* dspk) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_spk * D) return;
+  const int s = i / D, d = i - s * D;
   float acc = 0.f;
-  for (int b = 0; b < B; ++b) {
-    if (spk[b] != s) continue;
-    for (int t = 0; t < T_; ++t) acc += to_f(dcat[((long)b * T_ + t) * ldc + D + d]);
-  }
-  dspk[(long)s * D + d] += acc;
+  for (int b = 0; b < B; ++b)
+    if (spk[b] == s) acc += U[(long)b * D + d];
+  dspk[i] += acc;
 }
 
 template <typename T>
@@ -143,26 +173,37 @@ __global__ void reduce_cols_kernel(const float* part, int nb, int N, float* out,
 // Replicates torch CPU semantics of SB average_over_durations (App. A.10): cumsum of the
 // values accumulated in double and stored as float, cumsum of (values != 0) as int64,
 // differences gathered at the duration cumsum ends/starts, float division.
-__global__ void avg_over_dur_kernel(const float* vals, int Tm, const int64_t* durs, int Tp,
-                                    float* avg, float* vcum, int* nzcum) {
+__global__ void __launch_bounds__(256) avg_over_dur_kernel(const float* vals, int Tm,
+                                                           const int64_t* durs, int Tp,
+                                                           float* avg, float* vcum, int* nzcum) {
+  constexpr int CH = 2048;
+  __shared__ float sv[CH];
+  __shared__ float scum[CH];
+  __shared__ int snz[CH];
+  __shared__ long long cs[1024 + 1];
   const int b = blockIdx.x;
   const float* v = vals + (long)b * Tm;
   float* vc = vcum + (long)b * (Tm + 1);
   int* nc = nzcum + (long)b * (Tm + 1);
-  if (threadIdx.x == 0) {
-    double acc = 0.0;
-    int cnt = 0;
-    vc[0] = 0.f; nc[0] = 0;
-    for (int t = 0; t < Tm; ++t) {
-      acc += (double)v[t];
-      cnt += (v[t] != 0.f);
-      vc[t + 1] = (float)acc;
-      nc[t + 1] = cnt;
+  double acc = 0.0;
+  int cnt = 0;
+  if (threadIdx.x == 0) { vc[0] = 0.f; nc[0] = 0; }
+  for (int c0 = 0; c0 < Tm; c0 += CH) {
+    const int n = min(CH, Tm - c0);
+    for (int i = threadIdx.x; i < n; i += blockDim.x) sv[i] = v[c0 + i];
+    __syncthreads();
+    if (threadIdx.x == 0) {  // sequential: exact torch-CPU (double-accumulated) cumsum order
+      for (int i = 0; i < n; ++i) {
+        acc += (double)sv[i];
+        cnt += (sv[i] != 0.f);
+        scum[i] = (float)acc;
+        snz[i] = cnt;
+      }
     }
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += blockDim.x) { vc[c0 + i + 1] = scum[i]; nc[c0 + i + 1] = snz[i]; }
+    __syncthreads();
   }
-  __syncthreads();
-  // per-phoneme gather; the duration cumsum is recomputed by a block scan of d
-  __shared__ long long cs[1024 + 1];
   if (threadIdx.x == 0) {
     long long c = 0;
     cs[0] = 0;
@@ -340,8 +381,8 @@ extern "C" int fs2_embed_bwd(const int64_t* tokens, const void* dX, const float*
   if (!tokens || !dX || !keep || !dtable) return FS2_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   DISPATCH_T(dtype,
-    hipLaunchKernelGGL(embed_bwd_kernel<bf16>, dim3(V), dim3(128), 0, s, tokens, (const bf16*)dX, keep, M, D, dtable),
-    hipLaunchKernelGGL(embed_bwd_kernel<float>, dim3(V), dim3(128), 0, s, tokens, (const float*)dX, keep, M, D, dtable));
+    hipLaunchKernelGGL(embed_bwd_kernel<bf16>, dim3(V, (D + 63) / 64), dim3(256), 0, s, tokens, (const bf16*)dX, keep, M, D, dtable),
+    hipLaunchKernelGGL(embed_bwd_kernel<float>, dim3(V, (D + 63) / 64), dim3(256), 0, s, tokens, (const float*)dX, keep, M, D, dtable));
   return 0;
 }
 
@@ -379,14 +420,18 @@ extern "C" int fs2_concat_fwd(const void* feats, const float* spk_table, const i
 }
 
 extern "C" int fs2_concat_bwd_spk(const void* dcat, int ldc, const int64_t* spk, int B, int T,
-                                  int D, int n_spk, float* dspk, int dtype, void* stream) {
-  if (n_spk == 0 || D == 0) return 0;
-  if (!dcat || !spk || !dspk) return FS2_EINVAL;
+                                  int D, int n_spk, float* dspk, int dtype, float* workspace,
+                                  void* stream) {
+  if (n_spk == 0 || D == 0 || B == 0) return 0;
+  if (!dcat || !spk || !dspk || !workspace) return FS2_EINVAL;
   hipStream_t s = (hipStream_t)stream;
-  dim3 grid(n_spk, (D + 255) / 256);
+  dim3 grid(B, (D + 63) / 64);
   DISPATCH_T(dtype,
-    hipLaunchKernelGGL(concat_bwd_spk_kernel<bf16>, grid, dim3(256), 0, s, (const bf16*)dcat, ldc, spk, B, T, D, dspk),
-    hipLaunchKernelGGL(concat_bwd_spk_kernel<float>, grid, dim3(256), 0, s, (const float*)dcat, ldc, spk, B, T, D, dspk));
+    hipLaunchKernelGGL(concat_bwd_utt_kernel<bf16>, grid, dim3(256), 0, s, (const bf16*)dcat, ldc, T, D, workspace),
+    hipLaunchKernelGGL(concat_bwd_utt_kernel<float>, grid, dim3(256), 0, s, (const float*)dcat, ldc, T, D, workspace));
+  hipLaunchKernelGGL(concat_bwd_spk_kernel, dim3(nblk((long)n_spk * D)), dim3(256), 0, s, workspace,
+                     spk, B, D, n_spk, dspk);
+  FS2_CHECK_LAUNCH();
   return 0;
 }
 

@@ -51,7 +51,16 @@ class FS2Engine:
         self.w = {}
         self._wspecs = self._weight_specs()
         self._prepared_version = None
-        self.on_grads_ready = None   # optional callback(param_names_done) for DP overlap
+        self.on_grads_ready = None   # optional callback(tag) for DP overlap
+        self.timer = None            # optional KernelTimer: HIP events around tagged launches
+
+    def _tic(self, tag):
+        if self.timer is not None:
+            self.timer.start(tag)
+
+    def _toc(self, tag):
+        if self.timer is not None:
+            self.timer.stop(tag)
 
     # ------------------------------------------------------------------ helpers
     def ws(self, n):
@@ -173,8 +182,11 @@ class FS2Engine:
         del Ao
         F = self._wspecs[prefix + "pos_ffn.0.conv.weight"][0]
         Hc = self.empty(M, F)
+        tag = "ffn_conv1_fwd." + prefix.split(".")[0]
+        self._tic(tag)
         self._fwd(X1, D, M, T, prefix + "pos_ffn.0.conv.weight", Hc, F,
                   bias=P[prefix + "pos_ffn.0.conv.bias"], relu=1)
+        self._toc(tag)
         Y = self.empty(M, D)
         self._fwd(Hc, F, M, T, prefix + "pos_ffn.2.conv.weight", Y, D,
                   bias=P[prefix + "pos_ffn.2.conv.bias"])
@@ -597,7 +609,7 @@ class FS2Engine:
         self._dgrad(dZ, D, Mp, Tp, "concat_proj.w.weight", dcat, 2 * D, n_out=2 * D)
         self._wgrad(dZ, D, ctx["cat"], ldc, Mp, Tp, "concat_proj.w.weight", n_cols=ldc)
         ops.concat_bwd_spk(dcat, 2 * D, ctx["speakers"], B, Tp, D, c.n_speakers,
-                           G["speaker_emb.Embedding.weight"], dt=self.dt)
+                           G["speaker_emb.Embedding.weight"], dt=self.dt, ws=self.ws(B * D))
         dXl = self.empty(Mp, D)
         ops.ln_bwd(dcat, 2 * D, ctx["Xenc_last"], D, ctx["me"], ctx["re"], P["encoder.norm.norm.weight"],
                    P["encoder.norm.norm.bias"], dXl, D, Mp, D, dt=self.dt,

@@ -1,0 +1,26 @@
+"""Algorithmic FLOP counts of the train step over the padded (B, T_max, hidden) layout
+(SURVEY.md section 8d): per FFT layer 8TD^2 + 4T^2D + 2TDF(k0+k1) forward, predictors,
+concat projection, mel linear, PostNet; train = 3x forward (backward = 2x forward)."""
+
+
+def fft_layer_flops(T, D, F, ks):
+    return 8 * T * D * D + 4 * T * T * D + 2 * T * D * F * (ks[0] + ks[1])
+
+
+def forward_flops(cfg, B, Tp, Tm):
+    c = cfg
+    D = c.enc_d_model
+    ks = c.ffn_cnn_kernel_size_list
+    f = c.enc_num_layers * fft_layer_flops(Tp, D, c.enc_ffn_dim, ks)
+    f += c.dec_num_layers * fft_layer_flops(Tm, D, c.dec_ffn_dim, ks)
+    k = c.dur_pred_kernel_size
+    f += 3 * (2 * 2 * Tp * D * k * D + 2 * Tp * D)
+    f += 2 * Tp * (2 * D + 5) * D
+    f += 2 * Tm * D * c.n_mels
+    E, KP, NC = c.postnet_embedding_dim, c.postnet_kernel_size, c.postnet_n_convolutions
+    f += 2 * Tm * KP * (c.n_mels * E + (NC - 2) * E * E + E * c.n_mels)
+    return B * f
+
+
+def train_flops(cfg, B, Tp, Tm):
+    return 3 * forward_flops(cfg, B, Tp, Tm)

@@ -142,32 +142,29 @@ class FS2Config:
     n_speakers: int
 
 
-# backward-completion order of parameter groups (prefix match, first hit wins)
-_GROUP_ORDER = ["postnet.", "linear.", "decoder.norm."]
-
-
 def _group_key(name, n_dec, n_enc):
+    """(group, order within group, layer) -- sorts parameters into backward-completion order."""
     if name.startswith("postnet."):
-        return (0, 0)
+        return (0, 0, 0)
     if name.startswith("linear.") or name.startswith("decoder.norm."):
-        return (1, 0)
+        return (1, 0, 0)
     if name.startswith("decoder.layers."):
         i = int(name.split(".")[2])
-        return (2, n_dec - 1 - i)
+        return (2, n_dec - 1 - i, i)
     if name.split(".")[0] in ("energyEmbed", "energyPred", "pitchEmbed", "pitchPred", "durPred"):
-        return (3, 0)
+        return (3, 0, 0)
     if name.split(".")[0] in ("concat_proj", "speaker_emb") or name.startswith("encoder.norm."):
-        return (4, 0)
+        return (4, 0, 0)
     if name.startswith("encoder.layers."):
         i = int(name.split(".")[2])
-        return (5, n_enc - 1 - i)
-    return (6, 0)  # encPreNet
+        return (5, n_enc - 1 - i, i)
+    return (6, 0, 0)  # encPreNet
 
 
 def group_tag(key):
-    g, i = key
+    g, _, layer = key
     return {0: "postnet", 1: "linear", 3: "variance", 4: "conditioning", 6: "prenet"}.get(
-        g, None) or (f"decoder.layers.{i}" if g == 2 else f"encoder.layers.{i}")
+        g, None) or (f"decoder.layers.{layer}" if g == 2 else f"encoder.layers.{layer}")
 
 
 class FastSpeech2(nn.Module):

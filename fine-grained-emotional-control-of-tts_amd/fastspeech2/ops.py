@@ -122,8 +122,9 @@ def concat_fwd(feats, spk_table, spk, intensity, B, T, D, E, cat, ldc, *, dt):
                                 _p(cat), ldc, dt, _s()), "fs2_concat_fwd")
 
 
-def concat_bwd_spk(dcat, ldc, spk, B, T, D, n_spk, dspk, *, dt):
-    _chk(N.lib().fs2_concat_bwd_spk(_p(dcat), ldc, _p(spk), B, T, D, n_spk, _p(dspk), dt, _s()),
+def concat_bwd_spk(dcat, ldc, spk, B, T, D, n_spk, dspk, *, dt, ws):
+    _chk(N.lib().fs2_concat_bwd_spk(_p(dcat), ldc, _p(spk), B, T, D, n_spk, _p(dspk), dt, _p(ws),
+                                    _s()),
          "fs2_concat_bwd_spk")
 
 

@@ -131,7 +131,8 @@ int fs2_concat_fwd(const void* feats, const float* spk_table, const int64_t* spk
                    int dtype, void* stream);
 /* dSpk[spk[b]] (+)= sum_t dcat[b,t,D:2D]                                                  */
 int fs2_concat_bwd_spk(const void* dcat, int ldc, const int64_t* spk, int B, int T, int D,
-                       int n_spk, float* dspk, int dtype, void* stream);
+                       int n_spk, float* dspk, int dtype, float* workspace /* B*D */,
+                       void* stream);
 
 /* rows: X[m][:] *= keep[m]   (in place)                                                   */
 int fs2_mask_rows(void* X, int64_t ldx, const float* keep, int M, int D, int dtype, void* stream);

@@ -1,0 +1,293 @@
+"""GPU: op-level parity of the HIP kernels (through the C ABI) against torch fp32 references
+and the oracle's golden fixtures.  Tolerances: fp32 mode rel 1e-4 (GEMM-class) / exact for
+integer paths; bf16 mode rel 2e-2 against the fp32 reference of the same bf16 inputs.
+"""
+import math
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DT = [(torch.float32, 0, 1e-4), (torch.bfloat16, 1, 2e-2)]
+
+
+def rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).abs().max() / b.abs().max().clamp(min=1e-12)).item()
+
+
+@pytest.mark.parametrize("dt,code,tol", DT)
+def test_gemm_epilogue(cuda, dt, code, tol):
+    from fastspeech2 import ops
+    torch.manual_seed(0)
+    M, N, K = 300, 200, 256
+    A = torch.randn(M, K, device=cuda).to(dt)
+    W = torch.randn(N, K, device=cuda).to(dt)
+    bias = torch.randn(N, device=cuda)
+    gate = torch.randn(M, N, device=cuda).to(dt)
+    res = torch.randn(M, N, device=cuda).to(dt)
+    rs = (torch.rand(M, device=cuda) > 0.3).float()
+    rs2 = torch.rand(M, device=cuda)
+    C = torch.empty(M, N, device=cuda, dtype=dt)
+    ops.gemm(M, N, K, A, K, W, K, C, N, dt=code, bias=bias, relu=1, gate=gate, ldg=N, row_scale=rs,
+             residual=res, ldr=N, row_scale_post=rs2)
+    ref = torch.relu(A.float() @ W.float().t() + bias) * (gate.float() > 0)
+    ref = (ref * rs[:, None] + res.float()) * rs2[:, None]
+    assert rel(C, ref) < tol
+
+
+@pytest.mark.parametrize("dt,code,tol", DT)
+@pytest.mark.parametrize("KW", [9, 5, 3])
+def test_gemm_implicit_conv_fwd_dgrad_wgrad(cuda, dt, code, tol, KW):
+    from fastspeech2 import ops
+    torch.manual_seed(KW)
+    Bn, T, Cin, O = 3, 37, 64, 96
+    P = (KW - 1) // 2
+    X = torch.randn(Bn, T, Cin, device=cuda).to(dt)
+    Wt = torch.randn(O, Cin, KW, device=cuda).to(dt).float()
+    Wf = Wt.permute(0, 2, 1).contiguous().to(dt)     # [O][KW][C]
+    Wb = Wt.permute(1, 2, 0).contiguous().to(dt)     # [C][KW][O]
+    Xr = X.float().clone().requires_grad_(True)
+    Wr = Wt.clone().requires_grad_(True)
+    out = F.conv1d(F.pad(Xr.transpose(1, 2), (P, P), mode="reflect"), Wr).transpose(1, 2)
+    G = torch.randn(out.shape, device=cuda).to(dt).contiguous()
+    out.backward(G.float())
+    Y = torch.empty(Bn * T, O, device=cuda, dtype=dt)
+    ops.gemm(Bn * T, O, KW * Cin, X, Cin, Wf, KW * Cin, Y, O, dt=code, conv=(1, T, KW, Cin))
+    assert rel(Y, out.detach().reshape(-1, O)) < tol
+    dX = torch.empty(Bn * T, Cin, device=cuda, dtype=dt)
+    ops.gemm(Bn * T, Cin, KW * O, G, O, Wb, KW * O, dX, Cin, dt=code, conv=(2, T, KW, O))
+    assert rel(dX, Xr.grad.reshape(-1, Cin)) < tol
+    dW = torch.zeros(O, Cin, KW, device=cuda)
+    K = ops.round_up(Bn * T, 8)
+    ops.gemm(O, KW * Cin, K, G, O, X, Cin, dW, Cin * KW, dt=code, a_kmajor=0, b_kmajor=0,
+             conv=(3, T, KW, Cin), c_fp32=1, c_conv_kw=KW, kvalid=Bn * T, accumulate=1, split_k=3)
+    assert rel(dW, Wr.grad) < tol
+
+
+@pytest.mark.parametrize("dt,code,tol", DT)
+def test_gemm_batched_attention_shapes(cuda, dt, code, tol):
+    """S = Q K^T, O = P V, dV = P^T dO, dK = dS^T Q over the packed (B,T,3D) QKV layout."""
+    from fastspeech2 import ops
+    torch.manual_seed(1)
+    B, H, T, dh = 3, 2, 45, 32
+    D = H * dh
+    ldt = ops.round_up(T, 8)
+    QKV = torch.randn(B * T, 3 * D, device=cuda).to(dt)
+    q = QKV[:, :D].float().view(B, T, H, dh).permute(0, 2, 1, 3)
+    k = QKV[:, D:2 * D].float().view(B, T, H, dh).permute(0, 2, 1, 3)
+    v = QKV[:, 2 * D:].float().view(B, T, H, dh).permute(0, 2, 1, 3)
+    S = torch.empty(B * H, T, ldt, device=cuda)
+    ops.gemm(T, T, dh, QKV, 3 * D, QKV[:, D:], 3 * D, S, ldt, dt=code, c_fp32=1, batch=B * H,
+             batch_div=H, strides=(T * 3 * D, dh, T * 3 * D, dh, H * T * ldt, T * ldt, 0, 0))
+    assert rel(S[:, :, :T], (q @ k.transpose(-1, -2)).reshape(B * H, T, T)) < tol
+    Pm = torch.zeros(B * H, T, ldt, device=cuda, dtype=dt)
+    Pm[:, :, :T] = torch.softmax(S[:, :, :T], -1).to(dt)
+    O = torch.empty(B * T, D, device=cuda, dtype=dt)
+    ops.gemm(T, dh, ldt, Pm, ldt, QKV[:, 2 * D:], 3 * D, O, D, dt=code, b_kmajor=0, kvalid=T,
+             batch=B * H, batch_div=H, strides=(H * T * ldt, T * ldt, T * 3 * D, dh, T * D, dh, 0, 0))
+    ref = (Pm[:, :, :T].float().view(B, H, T, T) @ v).permute(0, 2, 1, 3).reshape(B * T, D)
+    assert rel(O, ref) < tol
+    dO = torch.randn(B * T, D, device=cuda).to(dt)
+    dQKV = torch.zeros(B * T, 3 * D, device=cuda, dtype=dt)
+    ops.gemm(ldt, dh, ldt, Pm, ldt, dO, D, dQKV[:, 2 * D:], 3 * D, dt=code, a_kmajor=0, b_kmajor=0,
+             kvalid=T, mvalid=T, batch=B * H, batch_div=H,
+             strides=(H * T * ldt, T * ldt, T * D, dh, T * 3 * D, dh, 0, 0))
+    dOh = dO.float().view(B, T, H, dh).permute(0, 2, 1, 3)
+    ref = (Pm[:, :, :T].float().view(B, H, T, T).transpose(-1, -2) @ dOh)
+    assert rel(dQKV[:, 2 * D:], ref.permute(0, 2, 1, 3).reshape(B * T, D)) < tol
+    assert torch.all(dQKV[:, :2 * D] == 0)     # mvalid: no spill into neighbouring columns/rows
+
+
+@pytest.mark.parametrize("dt,code,tol", DT)
+def test_layernorm_fwd_bwd(cuda, dt, code, tol):
+    from fastspeech2 import ops
+    torch.manual_seed(2)
+    M, D = 300, 384
+    x = torch.randn(M, D, device=cuda).to(dt)
+    r = torch.randn(M, D, device=cuda).to(dt)
+    g = torch.randn(D, device=cuda)
+    b = torch.randn(D, device=cuda)
+    keep = (torch.rand(M, device=cuda) > 0.2).float()
+    pa = torch.randn(M, D, device=cuda).to(dt)
+    for tanh in (0, 1):
+        y = torch.empty(M, D, device=cuda, dtype=dt)
+        s = torch.empty(M, D, device=cuda, dtype=dt)
+        mean = torch.empty(M, device=cuda)
+        rstd = torch.empty(M, device=cuda)
+        ops.ln_fwd(x, D, g, b, 1e-5, y, D, mean, rstd, M, D, dt=code, r=r, ldr=D, s_out=s,
+                   do_tanh=tanh, row_mask=keep, post_add=pa, ldp=D)
+        sr = (x.float() + r.float()).requires_grad_(True)
+        gr, br = g.clone().requires_grad_(True), b.clone().requires_grad_(True)
+        o = F.layer_norm(sr, (D,), gr, br, 1e-5)
+        if tanh:
+            o = torch.tanh(o)
+        o = o * keep[:, None] + pa.float()
+        assert rel(y, o) < tol
+        dy = torch.randn(M, D, device=cuda).to(dt)
+        o.backward(dy.float())
+        ds = torch.empty(M, D, device=cuda, dtype=dt)
+        dg = torch.zeros(D, device=cuda)
+        db = torch.zeros(D, device=cuda)
+        ws = torch.empty(int(ops.ln_ws(M, D)), device=cuda)
+        ops.ln_bwd(dy, D, s, D, mean, rstd, g, b, ds, D, M, D, dt=code, ws=ws, do_tanh=tanh,
+                   row_mask=keep, dgamma=dg, dbeta=db)
+        assert rel(ds, sr.grad) < tol * 3
+        assert rel(dg, gr.grad) < tol * 3
+        assert rel(db, br.grad) < tol * 3
+
+
+def test_attention_mask_quirk_against_torch_mha(cuda, golden_dir):
+    """The golden torch-MHA output (reference mask expression) through our kernels, fp32."""
+    from fastspeech2 import ops
+    g = np.load(os.path.join(golden_dir, "mask_tiling.npz"))
+    x = torch.from_numpy(g["x"]).to(cuda)
+    tokens = torch.from_numpy(g["tokens"]).to(cuda)
+    B, T, D = x.shape
+    H = int(g["nhead"])
+    dh = D // H
+    ldt = ops.round_up(T, 8)
+    w_in = torch.from_numpy(g["in_proj_weight"]).to(cuda)
+    b_in = torch.from_numpy(g["in_proj_bias"]).to(cuda)
+    w_out = torch.from_numpy(g["out_proj_weight"]).to(cuda)
+    b_out = torch.from_numpy(g["out_proj_bias"]).to(cuda)
+    X = x.reshape(B * T, D).contiguous()
+    QKV = torch.empty(B * T, 3 * D, device=cuda)
+    ops.gemm(B * T, 3 * D, D, X, D, w_in, D, QKV, 3 * D, dt=0, bias=b_in)
+    S = torch.empty(B * H, T, ldt, device=cuda)
+    ops.gemm(T, T, dh, QKV, 3 * D, QKV[:, D:], 3 * D, S, ldt, dt=0, c_fp32=1, batch=B * H,
+             batch_div=H, strides=(T * 3 * D, dh, T * 3 * D, dh, H * T * ldt, T * ldt, 0, 0))
+    kp = torch.empty(B * T, dtype=torch.uint8, device=cuda)
+    ops.keypad_from_tokens(tokens, 0, B * T, kp)
+    P = torch.empty(B * H, T, ldt, device=cuda)
+    ops.softmax_fwd(S, kp, B, H, T, T, ldt, 1.0 / math.sqrt(dh), 0.0, 0, 1, P, None, dt=0)
+    Att = torch.empty(B * T, D, device=cuda)
+    ops.gemm(T, dh, ldt, P, ldt, QKV[:, 2 * D:], 3 * D, Att, D, dt=0, b_kmajor=0, kvalid=T,
+             batch=B * H, batch_div=H, strides=(H * T * ldt, T * ldt, T * 3 * D, dh, T * D, dh, 0, 0))
+    out = torch.empty(B * T, D, device=cuda)
+    ops.gemm(B * T, D, D, Att, D, w_out, D, out, D, dt=0, bias=b_out)
+    torch.testing.assert_close(out.view(B, T, D).cpu(), torch.from_numpy(g["out"]), rtol=1e-4,
+                               atol=1e-5)
+
+
+@pytest.mark.parametrize("pace", [1.0, 1.1, 0.7])
+def test_length_regulator_bit_exact(cuda, golden_dir, pace):
+    from fastspeech2 import ops
+    g = np.load(os.path.join(golden_dir, "lr_kat.npz"))
+    d = torch.from_numpy(g["durs"]).to(cuda)
+    B, Tp = d.shape
+    exp_fs = g[f"frame_src_{pace}"]
+    Tm = exp_fs.shape[1]
+    ml = torch.empty(B, dtype=torch.int64, device=cuda)
+    cum = torch.empty(B, Tp, dtype=torch.int32, device=cuda)
+    fs = torch.empty(B, Tm, dtype=torch.int32, device=cuda)
+    ops.lr_index(d, 0, pace, B, Tp, Tm, ml, cum, fs)
+    np.testing.assert_array_equal(ml.cpu().numpy(), g[f"mel_len_{pace}"])
+    np.testing.assert_array_equal(fs.cpu().numpy(), exp_fs)
+    # gather + scatter round trip on integer-valued features: exact
+    D = 16
+    X = torch.arange(B * Tp * D, device=cuda, dtype=torch.float32).view(B * Tp, D) % 97
+    pe = torch.zeros(Tm, D, device=cuda)
+    Y = torch.empty(B * Tm, D, device=cuda)
+    keep = torch.empty(B * Tm, device=cuda)
+    ops.lr_gather(X, fs, pe, B, Tp, Tm, D, Y, keep, dt=0)
+    ref = torch.zeros(B, Tm, D)
+    fsc = torch.from_numpy(exp_fs).long()
+    for b in range(B):
+        v = fsc[b] >= 0
+        ref[b, v] = X.cpu().view(B, Tp, D)[b, fsc[b, v]]
+    assert torch.equal(Y.cpu().view(B, Tm, D), ref)
+    dX = torch.empty(B * Tp, D, device=cuda)
+    ops.lr_scatter(Y, cum, keep, B, Tp, Tm, D, dX, dt=0)
+    counts = torch.zeros(B, Tp)
+    n = (np.float32(pace) * g["durs"].astype(np.float32)).astype(np.int64)
+    assert torch.equal(dX.cpu().view(B, Tp, D), X.cpu().view(B, Tp, D) * torch.from_numpy(n)[..., None].float())
+
+
+def test_length_regulator_float_durations(cuda, golden_dir):
+    from fastspeech2 import ops
+    g = np.load(os.path.join(golden_dir, "lr_kat.npz"))
+    d = torch.from_numpy(g["durs_f"]).to(cuda)
+    B, Tp = d.shape
+    Tm = g["frame_src_f"].shape[1]
+    ml = torch.empty(B, dtype=torch.int64, device=cuda)
+    cum = torch.empty(B, Tp, dtype=torch.int32, device=cuda)
+    fs = torch.empty(B, Tm, dtype=torch.int32, device=cuda)
+    ops.lr_index(d, 1, 1.0, B, Tp, Tm, ml, cum, fs)
+    np.testing.assert_array_equal(fs.cpu().numpy(), g["frame_src_f"])
+
+
+def test_avg_over_durations_bit_exact(cuda, golden_dir):
+    from fastspeech2 import ops
+    g = np.load(os.path.join(golden_dir, "avg_kat.npz"))
+    v = torch.from_numpy(g["values"]).to(cuda)
+    d = torch.from_numpy(g["durs"]).to(cuda)
+    B, Tm = v.shape
+    Tp = d.shape[1]
+    out = torch.empty(B, Tp, device=cuda)
+    ops.avg_over_durations(v, Tm, d, B, Tp, out, torch.empty(int(ops.avg_ws(B, Tm)), device=cuda))
+    np.testing.assert_array_equal(out.cpu().numpy(), g["avg"])
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_fused_loss_vs_oracle(cuda, dt):
+    from fastspeech2.loss import fused_loss
+    from oracle.fs2_oracle import LossOracle
+    torch.manual_seed(4)
+    B, Tp, NM = 3, 20, 80
+    d = torch.randint(1, 6, (B, Tp))
+    d[1, 15:] = 0
+    d[2, 9:] = 0
+    mel_len = d.sum(1)
+    Tm = int(mel_len.max())
+    phon_len = (d > 0).sum(1)
+    tgt = torch.randn(B, Tm, NM) * 2 - 4
+    for b in range(B):
+        tgt[b, mel_len[b]:] = 0
+    mel = (torch.randn(B, Tm, NM) * 2 - 4)
+    post = mel + 0.1 * torch.randn(B, Tm, NM)
+    for b in range(B):
+        mel[b, mel_len[b]:] = 0
+    ld, pp, pe = torch.randn(B, Tp), torch.randn(B, Tp), torch.randn(B, Tp)
+    ap, ae = torch.randn(B, Tp), torch.randn(B, Tp)
+    mel, post, ld, pp, pe = [t.to(dt).float() for t in (mel, post, ld, pp, pe)]
+    leaves = [t.clone().requires_grad_(True) for t in (mel, post, ld, pp, pe)]
+    crit = LossOracle(True, 1.0, 1.0, 1.0, 1.0, 1.0, 1.0)
+    lo = crit((leaves[0], leaves[1], leaves[2], leaves[3].unsqueeze(-1), ap.unsqueeze(-1),
+               leaves[4].unsqueeze(-1), ae.unsqueeze(-1), mel_len), (tgt, d, None, None, mel_len,
+                                                                      phon_len), 0)
+    lo["total_loss"].backward()
+    c = lambda t: t.to(cuda)
+    loss, grads = fused_loss(c(mel).to(dt), c(post).to(dt), c(ld).to(dt), c(pp).to(dt),
+                             c(pe).to(dt), c(tgt), c(d), c(ap), c(ae), c(mel_len), c(phon_len),
+                             (1.0,) * 6)
+    keys = ["total_loss", "ssim_loss", "mel_loss", "postnet_mel_loss", "dur_loss", "pitch_loss",
+            "energy_loss"]
+    got = loss.cpu()
+    for i, k in enumerate(keys):
+        assert abs(got[i].item() - lo[k].item()) <= 1e-4 * max(1.0, abs(lo[k].item())), k
+    gtol = 1e-4 if dt == torch.float32 else 2e-2
+    for gg, leaf in zip(grads, leaves):
+        assert rel(gg.cpu().reshape(leaf.shape), leaf.grad) < gtol
+
+
+def test_adamw_matches_torch(cuda):
+    from fastspeech2 import ops
+    torch.manual_seed(5)
+    n = 10000
+    p0 = torch.randn(n, device=cuda)
+    ref = p0.clone().requires_grad_(True)
+    opt = torch.optim.AdamW([ref], lr=1e-3, foreach=False)
+    p, m, v = p0.clone(), torch.zeros(n, device=cuda), torch.zeros(n, device=cuda)
+    for t in range(1, 4):
+        g = torch.randn(n, device=cuda)
+        ref.grad = g.clone()
+        opt.step()
+        b1, b2, lr, wd = 0.9, 0.999, 1e-3, 1e-2
+        ops.adamw(p, g, m, v, n, 1 - lr * wd, 1 - b1, b2, 1 - b2, lr / (1 - b1 ** t),
+                  (1 - b2 ** t) ** 0.5, 1e-8, 1.0)
+    torch.testing.assert_close(p, ref.detach(), rtol=1e-6, atol=1e-7)

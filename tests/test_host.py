@@ -1,0 +1,129 @@
+"""CPU: host logic of the product package and the C ABI (no kernel launches).
+
+* libfs2_hip.so loads and exports every function include/fs2_hip.h declares;
+* host-side argument validation of fs2_gemm (returns before any launch);
+* the drop-in module's constructor, parameter count and state_dict keys equal the oracle's
+  (SB naming) and identical init under the same seed;
+* synthetic batches have the reference collate's layout (dataset.py:62-133);
+* algorithmic FLOP count matches SURVEY.md section 8d;
+* data-parallel gradient bucketing is contiguous and complete.
+"""
+import ctypes
+import os
+import re
+
+import pytest
+import torch
+
+from conftest import ROOT
+
+
+def _header_functions():
+    src = open(os.path.join(ROOT, "include", "fs2_hip.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(fs2_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    from fastspeech2 import _native
+    lib = _native.load()
+    declared = _header_functions()
+    assert len(declared) >= 30
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert set(declared) == set(_native.SIGNATURES), "ctypes table out of sync with the header"
+    assert lib.fs2_version().startswith(b"fs2_hip")
+
+
+def test_gemm_host_validation_rejects_bad_args():
+    from fastspeech2 import _native as N
+    lib = N.load()
+    buf = (ctypes.c_char * 4096)()
+    p = ctypes.addressof(buf)
+    p16 = (p + 15) // 16 * 16
+    d = N.GemmDesc(M=16, N=16, K=12, dtype=N.BF16, A=p16, lda=16, a_kmajor=1, B=p16, ldb=16,
+                   b_kmajor=1, C=p16, ldc=16)
+    assert lib.fs2_gemm(ctypes.byref(d), None) == -1          # K not a multiple of 8 (bf16)
+    d.K, d.lda = 16, 12
+    assert lib.fs2_gemm(ctypes.byref(d), None) == -2          # pitch not 16-byte aligned
+    d.lda, d.conv_mode, d.conv_t, d.conv_kw, d.conv_c = 16, 1, 3, 9, 16
+    assert lib.fs2_gemm(ctypes.byref(d), None) == -1          # reflect pad 4 >= T=3
+    d.conv_mode = 0
+    d.A = p16 + 2
+    assert lib.fs2_gemm(ctypes.byref(d), None) == -2          # misaligned pointer
+    assert lib.fs2_loss_fwd_bwd(None, None) == -1
+    assert lib.fs2_gemm_workspace if hasattr(lib, "fs2_gemm_workspace") else True
+
+
+def _tiny_cfg():
+    return dict(enc_num_layers=2, enc_num_head=2, enc_d_model=32, enc_ffn_dim=64, enc_k_dim=32,
+                enc_v_dim=32, enc_dropout=0.1, dec_num_layers=2, dec_num_head=2, dec_d_model=32,
+                dec_ffn_dim=64, dec_k_dim=32, dec_v_dim=32, dec_dropout=0.1,
+                normalize_before=False, ffn_type="1dcnn", ffn_cnn_kernel_size_list=[9, 1],
+                n_char=20, n_mels=16, postnet_embedding_dim=32, postnet_kernel_size=5,
+                postnet_n_convolutions=5, postnet_dropout=0.5, padding_idx=0,
+                dur_pred_kernel_size=3, pitch_pred_kernel_size=3, energy_pred_kernel_size=3,
+                variance_predictor_dropout=0.5)
+
+
+def test_dropin_module_matches_oracle_keys_and_init(cfg_all):
+    from fastspeech2.model import FastSpeech2
+    from oracle.fs2_oracle import FastSpeech2Oracle
+    kw = cfg_all["model"]["fastspeech2"]
+    torch.manual_seed(0)
+    o = FastSpeech2Oracle(**kw, n_speakers=4)
+    torch.manual_seed(0)
+    m = FastSpeech2(**kw, n_speakers=4)
+    so, sm = o.state_dict(), m.state_dict()
+    assert list(so) == list(sm)
+    for k in so:
+        assert so[k].shape == sm[k].shape and torch.equal(so[k], sm[k]), k
+    assert sum(p.numel() for p in m.parameters()) == 85_295_299
+    # reference checkpoints interchange
+    m.load_state_dict(o.state_dict())
+
+
+def test_backward_groups_contiguous_and_complete():
+    """Flat layout = backward-completion order; group ranges tile the buffer."""
+    from fastspeech2.model import FastSpeech2, _group_key, group_tag
+    m = FastSpeech2(**_tiny_cfg(), n_speakers=4)
+    names = [n for n, _ in m.named_parameters()]
+    keys = sorted({_group_key(n, 2, 2) for n in names})
+    tags = [group_tag(k) for k in keys]
+    assert tags == ["postnet", "linear", "decoder.layers.1", "decoder.layers.0", "variance",
+                    "conditioning", "encoder.layers.1", "encoder.layers.0", "prenet"]
+
+
+def test_grad_bucketer_partition():
+    from fastspeech2.train import GradBucketer
+    flat = torch.zeros(1000)
+    ranges = [("a", 0, 100), ("b", 100, 400), ("c", 400, 420), ("d", 420, 1000)]
+    bk = GradBucketer(flat, ranges, bucket_bytes=300 * 4)
+    assert bk.buckets == [(0, 400, "b"), (400, 1000, "d")]
+    cover = sorted((s, e) for s, e, _ in bk.buckets)
+    assert cover[0][0] == 0 and cover[-1][1] == 1000
+    assert all(cover[i][1] == cover[i + 1][0] for i in range(len(cover) - 1))
+
+
+def test_synthetic_batch_layout():
+    from fastspeech2.synthetic import make_batch
+    b = make_batch(B=8, seed=3)
+    pl = b["phon_len"]
+    assert torch.all(pl[:-1] >= pl[1:])                       # collate sorts descending
+    assert torch.equal(b["duration"].sum(1), b["mel_len"])    # durations sum to mel length
+    assert int(b["mel_len"].max()) == b["mel"].shape[1] <= 1000
+    for i in range(8):
+        L, P = int(b["mel_len"][i]), int(pl[i])
+        assert torch.all(b["phoneme"][i, :P] > 0) and torch.all(b["phoneme"][i, P:] == 0)
+        assert torch.all(b["mel"][i, L:] == 0) and torch.all(b["pitch"][i, L:] == 0)
+        assert torch.all(b["intensity"][i, P:] == 0)
+    mx = make_batch(B=4, max_shape=True)
+    assert mx["mel"].shape[1] == 1000 and mx["phoneme"].shape[1] == 200
+
+
+def test_flop_count_matches_survey(cfg_all):
+    from fastspeech2.model import FastSpeech2
+    from fastspeech2.flops import forward_flops
+    m = FastSpeech2(**cfg_all["model"]["fastspeech2"], n_speakers=4)
+    f = forward_flops(m.cfg, 1, 200, 1000)
+    assert abs(f / 1e9 - 112.9) < 0.5     # 112.9 GFLOP per utterance forward
