@@ -19,7 +19,16 @@
 // the current tile's MFMAs run; one barrier per K-tile.
 #include "fs2_common.h"
 
+#include <cstdlib>
+#include <cstring>
+
 namespace {
+
+// host-side A/B switch for kernel variants (read once)
+bool getenv_flag(const char* name) {
+  const char* v = std::getenv(name);
+  return v && v[0] && std::strcmp(v, "0") != 0;
+}
 
 constexpr int BM = 128, BN = 128, NT = 256;
 constexpr int TILE_BYTES = 128 * 128;  // one operand, one stage
@@ -38,6 +47,7 @@ struct GemmP {
   int batch_div;
   long sA1, sA2, sB1, sB2, sC1, sC2, sR1, sR2;
   int tiles_m, tiles_n;
+  int vec_ok;
 };
 
 __device__ __forceinline__ u32x4 add_bf16x8(u32x4 a, u32x4 b) {
@@ -91,6 +101,9 @@ __device__ __forceinline__ void load_kmajor(u32x4 (&st)[4], const char* base, lo
         if (cmode == 1) {
           const int ts = reflect_idx(t + j - P, T_);
           v = ld16(base + ((long)(b * T_ + ts) * ld + c) * ES);
+        } else if (cmode == 4) {  // shift conv over the padded domain, zero outside [0,T)
+          const int ts = t - j;
+          if (ts >= 0 && ts < T_) v = ld16(base + ((long)(b * T_ + ts) * ld + c) * ES);
         } else {  // cmode == 2: transposed conv with reflect fold
           const int t1 = t - j + P;
           if (t1 >= 0 && t1 < T_) v = ld16(base + ((long)(b * T_ + t1) * ld + c) * ES);
@@ -176,6 +189,78 @@ __device__ __forceinline__ void store_mnmajor(char* lds, const u32x4 (&st)[4]) {
   }
 }
 
+// ---- LDS-DMA (global_load_lds_dwordx4) staging, bf16 -----------------------------------
+// Each wave-instruction writes 1 KiB of LDS at a wave-uniform base (lane l -> bytes 16l..16l+15),
+// so the XOR swizzles above are applied on the SOURCE address: lane l fetches the logical
+// chunk that belongs at its physical slot.  Out-of-range chunks read a zero line.
+__device__ __attribute__((aligned(64))) char g_fs2_zero[64];
+
+typedef __attribute__((address_space(1))) void gptr_t;
+typedef __attribute__((address_space(3))) void lptr_t;
+
+__device__ __forceinline__ void glds16(const char* src, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const gptr_t*)src, (lptr_t*)lds_wave_base, 16, 0, 0);
+}
+
+// K-major tile (128 rows x 128 B): 16 x 1 KiB pieces, wave w issues pieces 4w..4w+3 (8 rows each)
+__device__ __forceinline__ void glds_kmajor(char* lds, const char* base, long ld, int row0,
+                                            int nrows, int k0, int kend, const GemmP& p,
+                                            int cmode, const int (&rb)[4], const int (&rt)[4],
+                                            int wave, int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int piece = wave * 4 + i;
+    const int r = piece * 8 + (lane >> 3);
+    const int lc = (lane & 7) ^ (r & 7);
+    const int row = row0 + r;
+    const int k = k0 + lc * 8;
+    const char* src = g_fs2_zero;
+    if (row < nrows && k < kend) {
+      if (cmode == 0) {
+        src = base + ((long)row * ld + k) * 2;
+      } else {  // cmode 1: reflect-padded implicit conv / cmode 4: zero-padded shift
+        const int C = p.conv_c, T_ = p.conv_t;
+        const int j = k / C, c = k - j * C;
+        if (cmode == 1) {
+          const int ts = reflect_idx(rt[i] + j - p.conv_p, T_);
+          src = base + ((long)(rb[i] * T_ + ts) * ld + c) * 2;
+        } else {
+          const int ts = rt[i] - j;
+          if (ts >= 0 && ts < T_) src = base + ((long)(rb[i] * T_ + ts) * ld + c) * 2;
+        }
+      }
+    }
+    glds16(src, lds + piece * 1024);
+  }
+}
+
+// MN-major tile (64 k-rows x 256 B): wave w issues pieces 4w..4w+3 (4 k-rows each)
+__device__ __forceinline__ void glds_mnmajor(char* lds, const char* base, long ld, int mn0,
+                                             int nmn, int k0, int kend, const GemmP& p,
+                                             bool conv3, int wave, int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int piece = wave * 4 + i;
+    const int kr = piece * 4 + (lane >> 4);
+    const int lc = (lane & 15) ^ mn_swz<bf16>(kr);
+    const int k = k0 + kr;
+    const int mn = mn0 + lc * 8;
+    const char* src = g_fs2_zero;
+    if (k < kend && mn < nmn) {
+      long srow = k;
+      int col = mn;
+      if (conv3) {
+        const int j = mn / p.conv_c;
+        col = mn - j * p.conv_c;
+        const int b = k / p.conv_t, t = k - b * p.conv_t;
+        srow = (long)b * p.conv_t + reflect_idx(t + j - p.conv_p, p.conv_t);
+      }
+      src = base + (srow * ld + col) * 2;
+    }
+    glds16(src, lds + piece * 1024);
+  }
+}
+
 // ---- fragment readers -------------------------------------------------------------------
 typedef __attribute__((ext_vector_type(4))) short s16x4;
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
@@ -209,7 +294,48 @@ __device__ __forceinline__ float frag_f32_mnmajor(const char* lds, int r0, int s
   return *(const float*)(lds + k * 512 + (((m >> 2) ^ mn_swz<float>(k)) << 4) + (m & 3) * 4);
 }
 
-template <typename T, bool AK, bool BKM>
+// 8 consecutive elements <-> float[8] (16-byte bf16 / 2x16-byte fp32 when complete)
+template <typename T>
+__device__ __forceinline__ void load8(float (&o)[8], const T* src, int nn) {
+  if (nn == 8) {
+    if constexpr (sizeof(T) == 2) {
+      const u32x4 u = *(const u32x4*)src;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        o[2 * w] = __builtin_bit_cast(float, u[w] << 16);
+        o[2 * w + 1] = __builtin_bit_cast(float, u[w] & 0xffff0000u);
+      }
+    } else {
+      const f32x4 a = *(const f32x4*)src, b = *(const f32x4*)(src + 4);
+      o[0] = a[0]; o[1] = a[1]; o[2] = a[2]; o[3] = a[3];
+      o[4] = b[0]; o[5] = b[1]; o[6] = b[2]; o[7] = b[3];
+    }
+  } else {
+    for (int e = 0; e < 8; ++e) o[e] = e < nn ? to_f(src[e]) : 0.f;
+  }
+}
+template <typename T>
+__device__ __forceinline__ void store8(T* dst, const float (&v)[8], int nn) {
+  if (nn == 8) {
+    if constexpr (sizeof(T) == 2) {
+      u32x4 u;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const bf16 a = (bf16)v[2 * w], b = (bf16)v[2 * w + 1];
+        u[w] = (unsigned)__builtin_bit_cast(unsigned short, a) |
+               ((unsigned)__builtin_bit_cast(unsigned short, b) << 16);
+      }
+      *(u32x4*)dst = u;
+    } else {
+      *(f32x4*)dst = f32x4{v[0], v[1], v[2], v[3]};
+      *(f32x4*)(dst + 4) = f32x4{v[4], v[5], v[6], v[7]};
+    }
+  } else {
+    for (int e = 0; e < nn; ++e) dst[e] = from_f<T>(v[e]);
+  }
+}
+
+template <typename T, bool AK, bool BKM, bool GA, bool GB>
 __global__ void __launch_bounds__(NT) gemm_kernel(GemmP p) {
   constexpr int ES = Cfg<T>::ES, BK = Cfg<T>::BK;
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE_BYTES];
@@ -237,13 +363,15 @@ __global__ void __launch_bounds__(NT) gemm_kernel(GemmP p) {
 
   // conv row coordinates for the K-major A loader (rows fixed per block)
   int rb[4] = {0, 0, 0, 0}, rt[4] = {0, 0, 0, 0};
-  const int amode = (p.conv_mode == 1 || p.conv_mode == 2) ? p.conv_mode : 0;
+  const int amode = (p.conv_mode == 1 || p.conv_mode == 2 || p.conv_mode == 4) ? p.conv_mode : 0;
   if (AK && amode) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int row = m0 + (tid >> 3) + 32 * i;
-      rb[i] = row / p.conv_t;
-      rt[i] = row - rb[i] * p.conv_t;
+      // register staging: row (tid>>3) + 32 i ; LDS-DMA: piece rows (4*wave + i)*8 + (lane>>3)
+      const int row = m0 + (GA ? (wave * 4 + i) * 8 + (lane >> 3) : (tid >> 3) + 32 * i);
+      const int rpu = amode == 4 ? p.conv_t + 2 * p.conv_p : p.conv_t;  // rows per utterance
+      rb[i] = row / rpu;
+      rt[i] = row - rb[i] * rpu;
     }
   }
   const bool bconv3 = (p.conv_mode == 3);
@@ -256,29 +384,44 @@ __global__ void __launch_bounds__(NT) gemm_kernel(GemmP p) {
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   u32x4 stA[4], stB[4];
-  auto load_tiles = [&](int k0) {
-    if constexpr (AK) load_kmajor<T>(stA, Ab, p.lda, m0, p.M, k0, kend, p, amode, rb, rt);
-    else load_mnmajor<T>(stA, Ab, p.lda, m0, p.M, k0, min(kend, kvalid), p, false);
-    if constexpr (BKM) load_kmajor<T>(stB, Bb, p.ldb, n0, p.N, k0, kend, p, 0, zero4, zero4);
-    else load_mnmajor<T>(stB, Bb, p.ldb, n0, p.N, k0, min(kend, kvalid), p, bconv3);
+  // issue the loads of one K-tile: LDS-DMA straight into the stage (GA/GB) or into registers
+  auto load_tiles = [&](int k0, int stage) {
+    char* la = smem + stage * 2 * TILE_BYTES;
+    char* lb = la + TILE_BYTES;
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+    if constexpr (GA) {
+      if constexpr (AK) glds_kmajor(la, Ab, p.lda, m0, p.M, k0, kend, p, amode, rb, rt, wv, lane);
+      else glds_mnmajor(la, Ab, p.lda, m0, p.M, k0, min(kend, kvalid), p, false, wv, lane);
+    } else {
+      if constexpr (AK) load_kmajor<T>(stA, Ab, p.lda, m0, p.M, k0, kend, p, amode, rb, rt);
+      else load_mnmajor<T>(stA, Ab, p.lda, m0, p.M, k0, min(kend, kvalid), p, false);
+    }
+    if constexpr (GB) {
+      if constexpr (BKM) glds_kmajor(lb, Bb, p.ldb, n0, p.N, k0, kend, p, 0, zero4, zero4, wv, lane);
+      else glds_mnmajor(lb, Bb, p.ldb, n0, p.N, k0, min(kend, kvalid), p, bconv3, wv, lane);
+    } else {
+      if constexpr (BKM) load_kmajor<T>(stB, Bb, p.ldb, n0, p.N, k0, kend, p, 0, zero4, zero4);
+      else load_mnmajor<T>(stB, Bb, p.ldb, n0, p.N, k0, min(kend, kvalid), p, bconv3);
+    }
   };
+  // write register-staged operands to LDS (no-op for LDS-DMA operands)
   auto store_tiles = [&](int stage) {
     char* la = smem + stage * 2 * TILE_BYTES;
     char* lb = la + TILE_BYTES;
-    if constexpr (AK) store_kmajor<T>(la, stA); else store_mnmajor<T>(la, stA);
-    if constexpr (BKM) store_kmajor<T>(lb, stB); else store_mnmajor<T>(lb, stB);
+    if constexpr (!GA) { if constexpr (AK) store_kmajor<T>(la, stA); else store_mnmajor<T>(la, stA); }
+    if constexpr (!GB) { if constexpr (BKM) store_kmajor<T>(lb, stB); else store_mnmajor<T>(lb, stB); }
   };
 
   const int nk = (kend > kbeg) ? (kend - kbeg + BK - 1) / BK : 0;
   if (nk > 0) {
-    load_tiles(kbeg);
+    load_tiles(kbeg, 0);
     store_tiles(0);
   }
   __syncthreads();
 
   for (int kt = 0; kt < nk; ++kt) {
     const int stage = kt & 1;
-    if (kt + 1 < nk) load_tiles(kbeg + (kt + 1) * BK);
+    if (kt + 1 < nk) load_tiles(kbeg + (kt + 1) * BK, stage ^ 1);
     const char* la = smem + stage * 2 * TILE_BYTES;
     const char* lb = la + TILE_BYTES;
     if constexpr (ES == 2) {
@@ -326,48 +469,459 @@ __global__ void __launch_bounds__(NT) gemm_kernel(GemmP p) {
   const char* Rb = p.residual ? p.residual + (zb * p.sR1 + zh * p.sR2) * ES : nullptr;
   const bool atomic = p.split_k > 1;
   const int cc = p.c_conv_kw > 0 ? p.N / p.c_conv_kw : 0;
+  if (!p.vec_ok) {  // scalar path: scattered (conv-remapped) or atomic fp32 gradient outputs
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < 4; ++i) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int m = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
-      if (m >= p.mvalid) continue;
-      const float rs = p.row_scale ? p.row_scale[m] : 1.f;
-      const float rs2 = p.row_scale_post ? p.row_scale_post[m] : 1.f;
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+        if (m >= p.mvalid) continue;
+        const float rs = p.row_scale ? p.row_scale[m] : 1.f;
+        const float rs2 = p.row_scale_post ? p.row_scale_post[m] : 1.f;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int n = n0 + wn * 64 + j * 16 + (lane & 15);
-        if (n >= p.nvalid) continue;
-        float v = acc[i][j][r];
-        if (p.bias) v += p.bias[n];
-        if (p.relu) v = fmaxf(v, 0.f);
-        if (p.gate) v = (to_f(((const T*)p.gate)[(long)m * p.ldg + n]) > 0.f) ? v : 0.f;
-        v *= rs;
-        if (Rb) v += to_f(((const T*)Rb)[(long)m * p.ldr + n]);
-        v *= rs2;
-        long col = n;
-        if (cc > 0) { const int jj = n / cc; col = (long)(n - jj * cc) * p.c_conv_kw + jj; }
-        const long off = (long)m * p.ldc + col;
-        if (p.c_fp32) {
-          float* Cf = (float*)Cb;
-          if (atomic) atomicAdd(Cf + off, v);
-          else if (p.accumulate) Cf[off] += v;
-          else Cf[off] = v;
-        } else {
-          ((T*)Cb)[off] = from_f<T>(v);
+        for (int j = 0; j < 4; ++j) {
+          const int n = n0 + wn * 64 + j * 16 + (lane & 15);
+          if (n >= p.nvalid) continue;
+          float v = acc[i][j][r];
+          if (p.bias) v += p.bias[n];
+          if (p.relu) v = fmaxf(v, 0.f);
+          if (p.gate) v = (to_f(((const T*)p.gate)[(long)m * p.ldg + n]) > 0.f) ? v : 0.f;
+          v *= rs;
+          if (Rb) v += to_f(((const T*)Rb)[(long)m * p.ldr + n]);
+          v *= rs2;
+          long col = n;
+          if (cc > 0) { const int jj = n / cc; col = (long)(n - jj * cc) * p.c_conv_kw + jj; }
+          const long off = (long)m * p.ldc + col;
+          if (p.c_fp32) {
+            float* Cf = (float*)Cb;
+            if (atomic) atomicAdd(Cf + off, v);
+            else if (p.accumulate) Cf[off] += v;
+            else Cf[off] = v;
+          } else {
+            ((T*)Cb)[off] = from_f<T>(v);
+          }
         }
       }
     }
+    return;
   }
+  // vector path: accumulators -> LDS (fp32 128x128, column bit 4 flipped on rows with bit 2
+  // set so the two 16-lane row groups of a ds_write_b32 half hit disjoint banks), then each
+  // thread owns 8 consecutive columns of a row: 16-byte loads of bias / gate / residual and
+  // 16-byte stores -- one 256-byte segment per 16 threads.
+  float* cs = (float*)smem;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+        const int col = wn * 64 + j * 16 + (lane & 15);
+        cs[row * 128 + (col ^ (((row >> 2) & 1) << 4))] = acc[i][j][r];
+      }
+  __syncthreads();
+  const int c8 = (tid & 15) * 8;
+  const int n = n0 + c8;
+#pragma unroll 2
+  for (int pass = 0; pass < 8; ++pass) {
+    const int row = (tid >> 4) + 16 * pass;
+    const int m = m0 + row;
+    if (m >= p.mvalid || n >= p.nvalid) continue;
+    const int sw = ((row >> 2) & 1) << 4;
+    const f32x4 lo = *(const f32x4*)&cs[row * 128 + (c8 ^ sw)];
+    const f32x4 hi = *(const f32x4*)&cs[row * 128 + ((c8 + 4) ^ sw)];
+    float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    const int nn = min(8, p.nvalid - n);
+    const float rs = p.row_scale ? p.row_scale[m] : 1.f;
+    const float rs2 = p.row_scale_post ? p.row_scale_post[m] : 1.f;
+    if (p.bias) {
+      if (nn == 8) {
+        const f32x4 b0 = *(const f32x4*)(p.bias + n), b1 = *(const f32x4*)(p.bias + n + 4);
+        v[0] += b0[0]; v[1] += b0[1]; v[2] += b0[2]; v[3] += b0[3];
+        v[4] += b1[0]; v[5] += b1[1]; v[6] += b1[2]; v[7] += b1[3];
+      } else {
+        for (int e = 0; e < nn; ++e) v[e] += p.bias[n + e];
+      }
+    }
+    float g[8], rr[8];
+    if (p.gate) load8<T>(g, (const T*)p.gate + (long)m * p.ldg + n, nn);
+    if (Rb) load8<T>(rr, (const T*)Rb + (long)m * p.ldr + n, nn);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float x = v[e];
+      if (p.relu) x = fmaxf(x, 0.f);
+      if (p.gate) x = (g[e] > 0.f) ? x : 0.f;
+      x *= rs;
+      if (Rb) x += rr[e];
+      v[e] = x * rs2;
+    }
+    const long off = (long)m * p.ldc + n;
+    if (p.c_fp32) {
+      float* Cf = (float*)Cb + off;
+      if (nn == 8) {
+        f32x4 o0 = {v[0], v[1], v[2], v[3]}, o1 = {v[4], v[5], v[6], v[7]};
+        if (p.accumulate) { o0 += *(const f32x4*)Cf; o1 += *(const f32x4*)(Cf + 4); }
+        *(f32x4*)Cf = o0;
+        *(f32x4*)(Cf + 4) = o1;
+      } else {
+        for (int e = 0; e < nn; ++e) Cf[e] = p.accumulate ? Cf[e] + v[e] : v[e];
+      }
+    } else {
+      store8<T>((T*)Cb + off, v, nn);
+    }
+  }
+}
+
+// ============================================================================================
+// "Big" bf16 kernel: 256x128 tile, 8 waves (4 x 2, 64x64 per wave), BK = 64, three-stage
+// LDS-DMA ring (48 KiB per stage, prefetch distance 2) paced by COUNTED vmcnt waits and raw
+// s_barrier (a __syncthreads() would drain the in-flight prefetch), XCD-aware tile order.
+// Used for every bf16 GEMM with enough tiles except the reflect-fold dgrad operand.
+// ============================================================================================
+constexpr int BBM = 256, BNT = 512;
+constexpr int BIG_A = 256 * 128;          // A stage bytes (32 KiB)
+constexpr int BIG_B = 128 * 128;          // B stage bytes (16 KiB)
+constexpr int BIG_STAGE = BIG_A + BIG_B;  // 48 KiB
+constexpr int BIG_LDS = 3 * BIG_STAGE;    // 144 KiB (the 256x128 fp32 epilogue tile fits)
+
+// MN-major rows of 256 mn (512 B): same chunk swizzle on the low 4 chunk bits
+__device__ __forceinline__ bf16x8 frag_bf16_mnmajor512(const char* lds, int r0, int s, int lane) {
+  const int li = lane & 15, g = lane >> 4, q = li >> 2, p = li & 3;
+  const int m = r0 + 4 * p;
+  const int c = m >> 3, boff = (m & 7) * 2;
+  const int k1 = s * 32 + 8 * g + q, k2 = k1 + 4;
+  const char* a1 = lds + k1 * 512 + ((c ^ mn_swz<bf16>(k1)) << 4) + boff;
+  const char* a2 = lds + k2 * 512 + ((c ^ mn_swz<bf16>(k2)) << 4) + boff;
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a1);
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a2);
+  typedef __attribute__((ext_vector_type(8))) short s16x8;
+  const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// MN-major tile of 64 k-rows x (ROWB bytes): 1 KiB pieces of 1024/ROWB rows
+template <int ROWB>
+__device__ __forceinline__ void glds_mn_piece(char* lds, const char* base, long ld, int mn0, int nmn,
+                                              int k0, int kend, const GemmP& p, bool conv3,
+                                              int piece, int lane) {
+  constexpr int CPR = ROWB / 16, RPP = 1024 / ROWB;
+  const int kr = piece * RPP + lane / CPR;
+  const int lc = (lane % CPR) ^ mn_swz<bf16>(kr);
+  const int k = k0 + kr;
+  const int mn = mn0 + lc * 8;
+  const char* src = g_fs2_zero;
+  if (k < kend && mn < nmn) {
+    long srow = k;
+    int col = mn;
+    if (conv3) {
+      const int j = mn / p.conv_c;
+      col = mn - j * p.conv_c;
+      const int b = k / p.conv_t, t = k - b * p.conv_t;
+      srow = (long)b * p.conv_t + reflect_idx(t + j - p.conv_p, p.conv_t);
+    }
+    src = base + (srow * ld + col) * 2;
+  }
+  glds16(src, lds + piece * 1024);
+}
+
+// K-major piece: 8 rows x 128 B
+__device__ __forceinline__ void glds_k_piece(char* lds, const char* base, long ld, int row0,
+                                             int nrows, int k0, int kend, const GemmP& p,
+                                             int cmode, int b, int t, int piece, int lane) {
+  const int r = piece * 8 + (lane >> 3);
+  const int lc = (lane & 7) ^ (r & 7);
+  const int row = row0 + r;
+  const int k = k0 + lc * 8;
+  const char* src = g_fs2_zero;
+  if (row < nrows && k < kend) {
+    if (cmode == 0) {
+      src = base + ((long)row * ld + k) * 2;
+    } else {
+      const int C = p.conv_c, T_ = p.conv_t;
+      const int j = k / C, c = k - j * C;
+      const int ts = reflect_idx(t + j - p.conv_p, T_);
+      src = base + ((long)(b * T_ + ts) * ld + c) * 2;
+    }
+  }
+  glds16(src, lds + piece * 1024);
+}
+
+template <bool AK, bool BKM>
+__global__ void __launch_bounds__(BNT) gemm_big_kernel(GemmP p) {
+  __shared__ __attribute__((aligned(16))) char smem[BIG_LDS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  // XCD-aware bijective remap: blocks b and b+8 share an XCD; give each XCD a contiguous run
+  const int nwg = p.tiles_m * p.tiles_n;
+  const int orig = blockIdx.x;
+  const int xcd = orig & 7, q = nwg >> 3, r8 = nwg & 7;
+  const int bid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (orig >> 3);
+  const int tm = bid / p.tiles_n, tn = bid - tm * p.tiles_n;
+  const int m0 = tm * BBM, n0 = tn * 128;
+  const int z = blockIdx.z;
+  const long zb = z / p.batch_div, zh = z - zb * p.batch_div;
+  const char* Ab = p.A + (zb * p.sA1 + zh * p.sA2) * 2;
+  const char* Bb = p.B + (zb * p.sB1 + zh * p.sB2) * 2;
+  const int K = p.K;
+  const int kva = min(K, p.kvalid);
+  const int amode = (p.conv_mode == 1 || p.conv_mode == 4) ? p.conv_mode : 0;
+  const bool bconv3 = p.conv_mode == 3;
+  const bool tap_uniform = amode && (p.conv_c % 64) == 0;  // a 64-wide k-tile sits in one tap
+  const int rpu = amode == 4 ? p.conv_t + 2 * p.conv_p : p.conv_t;  // rows per utterance
+  const char* zero = g_fs2_zero;
+
+  // ---- per-lane, per-piece source state, hoisted out of the K loop ----
+  // A K-major: pieces 4w+i (8 rows each), lane row r = piece*8 + (lane>>3), chunk lc
+  const char* arow[4];
+  int abt[4], at[4], alc[4];
+  bool aval[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if constexpr (AK) {
+      const int r = (wave * 4 + i) * 8 + (lane >> 3);
+      alc[i] = (lane & 7) ^ (r & 7);
+      const int row = m0 + r;
+      aval[i] = row < p.M;
+      const int rr = aval[i] ? row : 0;
+      const int b = amode ? rr / rpu : 0;
+      abt[i] = b * p.conv_t;       // source row base (unpadded utterance)
+      at[i] = rr - b * rpu;        // position inside the (padded) utterance
+      arow[i] = Ab + (long)rr * p.lda * 2;
+    } else {  // MN-major (512-byte k-rows): piece = 2 k-rows
+      const int kr = (wave * 4 + i) * 2 + (lane >> 5);
+      alc[i] = (lane & 31) ^ mn_swz<bf16>(kr);
+      at[i] = kr;
+      const int mn = m0 + alc[i] * 8;
+      aval[i] = mn < p.M;
+      arow[i] = Ab + (long)(aval[i] ? mn : 0) * 2;
+      abt[i] = 0;
+    }
+  }
+  const char* brow[2];
+  int blc[2], bkr[2];
+  bool bval[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    if constexpr (BKM) {
+      const int r = (wave * 2 + i) * 8 + (lane >> 3);
+      blc[i] = (lane & 7) ^ (r & 7);
+      const int row = n0 + r;
+      bval[i] = row < p.N;
+      brow[i] = Bb + (long)(bval[i] ? row : 0) * p.ldb * 2;
+      bkr[i] = 0;
+    } else {  // MN-major (256-byte k-rows): piece = 4 k-rows
+      const int kr = (wave * 2 + i) * 4 + (lane >> 4);
+      blc[i] = (lane & 15) ^ mn_swz<bf16>(kr);
+      bkr[i] = kr;
+      const int mn = n0 + blc[i] * 8;
+      bval[i] = mn < p.N;
+      int col = mn;
+      if (bconv3 && bval[i]) { const int j = mn / p.conv_c; col = mn - j * p.conv_c; blc[i] = j; }
+      else if (bconv3) blc[i] = 0;
+      brow[i] = Bb + (long)(bval[i] ? col : 0) * 2;
+    }
+  }
+
+  auto issue = [&](int kt, int stage) {   // 6 LDS-DMA pieces per wave, branch-free sources
+    const int k0 = kt * 64;
+    char* la = smem + stage * BIG_STAGE;
+    char* lb = la + BIG_A;
+    int jt = 0, c0 = 0;
+    if (tap_uniform) { jt = k0 / p.conv_c; c0 = k0 - jt * p.conv_c; }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const char* src;
+      if constexpr (AK) {
+        const int k = k0 + alc[i] * 8;
+        bool ok = aval[i] && k < K;
+        if (!amode) {
+          src = arow[i] + (long)k * 2;
+        } else {
+          int j, c;
+          if (tap_uniform) { j = jt; c = c0 + alc[i] * 8; }
+          else { j = k / p.conv_c; c = k - j * p.conv_c; }
+          int ts;
+          if (amode == 1) {
+            ts = reflect_idx(at[i] + j - p.conv_p, p.conv_t);
+          } else {
+            ts = at[i] - j;
+            ok = ok && ts >= 0 && ts < p.conv_t;
+            ts = ok ? ts : 0;
+          }
+          src = Ab + ((long)(abt[i] + ts) * p.lda + c) * 2;
+        }
+        src = ok ? src : zero;
+      } else {
+        const int k = k0 + at[i];
+        const bool ok = aval[i] && k < kva;
+        src = ok ? arow[i] + (long)k * p.lda * 2 : zero;
+      }
+      glds16(src, la + (wave * 4 + i) * 1024);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const char* src;
+      if constexpr (BKM) {
+        const int k = k0 + blc[i] * 8;
+        src = (bval[i] && k < K) ? brow[i] + (long)k * 2 : zero;
+      } else {
+        const int k = k0 + bkr[i];
+        const bool ok = bval[i] && k < kva;
+        long srow = k;
+        if (bconv3) {
+          const int b = k / p.conv_t, t = k - b * p.conv_t;
+          srow = (long)b * p.conv_t + reflect_idx(t + blc[i] - p.conv_p, p.conv_t);
+        }
+        src = ok ? brow[i] + srow * p.ldb * 2 : zero;
+      }
+      glds16(src, lb + (wave * 2 + i) * 1024);
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (K + 63) / 64;
+  if (nk > 0) issue(0, 0);
+  if (nk > 1) issue(1, 1);
+  for (int kt = 0; kt < nk; ++kt) {
+    // tile kt landed for this wave (leave tile kt+1's 6 pieces in flight) ...
+    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // ... and for every wave; every wave is also done reading stage (kt+2)%3 == (kt-1)%3
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (kt + 2 < nk) issue(kt + 2, (kt + 2) % 3);
+    const char* la = smem + (kt % 3) * BIG_STAGE;
+    const char* lb = la + BIG_A;
+    // all fragments of both k-steps first (distinct registers), then 32 MFMAs
+    bf16x8 af[2][4], bfr[2][4];
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        af[s][i] = AK ? frag_bf16_kmajor(la, wm * 64 + i * 16, s, lane)
+                      : frag_bf16_mnmajor512(la, wm * 64 + i * 16, s, lane);
+        bfr[s][i] = BKM ? frag_bf16_kmajor(lb, wn * 64 + i * 16, s, lane)
+                        : frag_bf16_mnmajor(lb, wn * 64 + i * 16, s, lane);
+      }
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[s][i], bfr[s][j], acc[i][j], 0, 0, 0);
+    // pin the order: every fragment read of the tile is issued before the first MFMA, so the
+    // step-1 reads land while step-0 MFMAs run (hipcc otherwise recycles 2 registers and
+    // waits lgkmcnt(0) in front of every MFMA group)
+    __builtin_amdgcn_sched_group_barrier(0x100, AK && BKM ? 16 : (AK || BKM ? 24 : 32), 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 32, 0);
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // ---- epilogue: fp32 tile through LDS, 16-byte vector pass (same ops as gemm_kernel) ----
+  char* Cb = p.C + (zb * p.sC1 + zh * p.sC2) * (p.c_fp32 ? 4 : 2);
+  const char* Rb = p.residual ? p.residual + (zb * p.sR1 + zh * p.sR2) * 2 : nullptr;
+  float* cs = (float*)smem;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+        const int col = wn * 64 + j * 16 + (lane & 15);
+        cs[row * 128 + (col ^ (((row >> 2) & 1) << 4))] = acc[i][j][r];
+      }
+  __syncthreads();
+  const int c8 = (tid & 15) * 8;
+  const int n = n0 + c8;
+#pragma unroll 2
+  for (int pass = 0; pass < 8; ++pass) {
+    const int row = (tid >> 4) + 32 * pass;
+    const int m = m0 + row;
+    if (m >= p.mvalid || n >= p.nvalid) continue;
+    const int sw = ((row >> 2) & 1) << 4;
+    const f32x4 lo = *(const f32x4*)&cs[row * 128 + (c8 ^ sw)];
+    const f32x4 hi = *(const f32x4*)&cs[row * 128 + ((c8 + 4) ^ sw)];
+    float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    const int nn = min(8, p.nvalid - n);
+    const float rs = p.row_scale ? p.row_scale[m] : 1.f;
+    const float rs2 = p.row_scale_post ? p.row_scale_post[m] : 1.f;
+    if (p.bias) {
+      if (nn == 8) {
+        const f32x4 b0 = *(const f32x4*)(p.bias + n), b1 = *(const f32x4*)(p.bias + n + 4);
+        v[0] += b0[0]; v[1] += b0[1]; v[2] += b0[2]; v[3] += b0[3];
+        v[4] += b1[0]; v[5] += b1[1]; v[6] += b1[2]; v[7] += b1[3];
+      } else {
+        for (int e = 0; e < nn; ++e) v[e] += p.bias[n + e];
+      }
+    }
+    float g[8], rr[8];
+    if (p.gate) load8<bf16>(g, (const bf16*)p.gate + (long)m * p.ldg + n, nn);
+    if (Rb) load8<bf16>(rr, (const bf16*)Rb + (long)m * p.ldr + n, nn);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float x = v[e];
+      if (p.relu) x = fmaxf(x, 0.f);
+      if (p.gate) x = (g[e] > 0.f) ? x : 0.f;
+      x *= rs;
+      if (Rb) x += rr[e];
+      v[e] = x * rs2;
+    }
+    const long off = (long)m * p.ldc + n;
+    if (p.c_fp32) {
+      float* Cf = (float*)Cb + off;
+      if (nn == 8) {
+        f32x4 o0 = {v[0], v[1], v[2], v[3]}, o1 = {v[4], v[5], v[6], v[7]};
+        if (p.accumulate) { o0 += *(const f32x4*)Cf; o1 += *(const f32x4*)(Cf + 4); }
+        *(f32x4*)Cf = o0;
+        *(f32x4*)(Cf + 4) = o1;
+      } else {
+        for (int e = 0; e < nn; ++e) Cf[e] = p.accumulate ? Cf[e] + v[e] : v[e];
+      }
+    } else {
+      store8<bf16>((bf16*)Cb + off, v, nn);
+    }
+  }
+}
+
+template <typename T, bool GA, bool GB>
+void launch4(const GemmP& p, dim3 grid, hipStream_t s, int ak, int bk) {
+  if (ak && bk) hipLaunchKernelGGL((gemm_kernel<T, true, true, GA, GB>), grid, dim3(NT), 0, s, p);
+  else if (ak && !bk) hipLaunchKernelGGL((gemm_kernel<T, true, false, GA, GB>), grid, dim3(NT), 0, s, p);
+  else if (!ak && bk) hipLaunchKernelGGL((gemm_kernel<T, false, true, GA, GB>), grid, dim3(NT), 0, s, p);
+  else hipLaunchKernelGGL((gemm_kernel<T, false, false, GA, GB>), grid, dim3(NT), 0, s, p);
 }
 
 template <typename T>
 int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
   dim3 grid(p.tiles_m * p.tiles_n, 1, gz);
-  if (ak && bk) hipLaunchKernelGGL((gemm_kernel<T, true, true>), grid, dim3(NT), 0, s, p);
-  else if (ak && !bk) hipLaunchKernelGGL((gemm_kernel<T, true, false>), grid, dim3(NT), 0, s, p);
-  else if (!ak && bk) hipLaunchKernelGGL((gemm_kernel<T, false, true>), grid, dim3(NT), 0, s, p);
-  else hipLaunchKernelGGL((gemm_kernel<T, false, false>), grid, dim3(NT), 0, s, p);
+  if constexpr (sizeof(T) == 2) {
+    // bf16: LDS-DMA for both operands, except the reflect-fold dgrad operand (register staged)
+    const int big_tiles = ((p.M + BBM - 1) / BBM) * p.tiles_n * gz;
+    if (p.conv_mode != 2 && p.vec_ok && p.split_k <= 1 && big_tiles >= 240 &&
+        !getenv_flag("FS2_GEMM_NO_BIG")) {
+      GemmP q = p;
+      q.tiles_m = (p.M + BBM - 1) / BBM;
+      dim3 g2(q.tiles_m * q.tiles_n, 1, gz);
+      if (ak && bk) hipLaunchKernelGGL((gemm_big_kernel<true, true>), g2, dim3(BNT), 0, s, q);
+      else if (ak && !bk) hipLaunchKernelGGL((gemm_big_kernel<true, false>), g2, dim3(BNT), 0, s, q);
+      else if (!ak && bk) hipLaunchKernelGGL((gemm_big_kernel<false, true>), g2, dim3(BNT), 0, s, q);
+      else hipLaunchKernelGGL((gemm_big_kernel<false, false>), g2, dim3(BNT), 0, s, q);
+    } else if (p.conv_mode == 2) launch4<T, false, true>(p, grid, s, ak, bk);
+    else launch4<T, true, true>(p, grid, s, ak, bk);
+  } else {
+    launch4<T, false, false>(p, grid, s, ak, bk);
+  }
   FS2_CHECK_LAUNCH();
   return 0;
 }
@@ -415,10 +969,13 @@ extern "C" int fs2_gemm(const fs2_gemm_desc* d, void* stream) {
   if (!d->b_kmajor && (p.N % epc)) return FS2_EINVAL;
   if (p.conv_mode) {
     if (p.conv_t <= 0 || p.conv_kw <= 0 || p.conv_c <= 0 || (p.conv_c % epc)) return FS2_EINVAL;
-    if (p.conv_p >= p.conv_t) return FS2_EINVAL;  // torch reflect pad needs pad < T
+    if (p.conv_mode != 4 && p.conv_p >= p.conv_t) return FS2_EINVAL;  // reflect pad needs pad < T
     if ((p.conv_mode == 1 || p.conv_mode == 2) && (!d->a_kmajor || p.K != p.conv_kw * p.conv_c))
       return FS2_EINVAL;
     if ((p.conv_mode == 1 || p.conv_mode == 2) && (p.M % p.conv_t)) return FS2_EINVAL;
+    if (p.conv_mode == 4 && (p.M % (p.conv_t + 2 * p.conv_p))) return FS2_EINVAL;
+    if (p.conv_mode == 4 && !d->a_kmajor) return FS2_EINVAL;
+    if (p.conv_mode == 4 && p.K != p.conv_kw * p.conv_c) return FS2_EINVAL;
     if (p.conv_mode == 3 && (d->b_kmajor || p.N != p.conv_kw * p.conv_c)) return FS2_EINVAL;
   }
   if (p.c_conv_kw > 0 && (p.N % p.c_conv_kw)) return FS2_EINVAL;
@@ -428,6 +985,16 @@ extern "C" int fs2_gemm(const fs2_gemm_desc* d, void* stream) {
     p.split_k = (p.K + p.k_per_split - 1) / p.k_per_split;
   }
   if (p.accumulate && !p.c_fp32) return FS2_EINVAL;
+  {
+    const int oes = p.c_fp32 ? 4 : es;
+    const int ov = 16 / oes;  // output elements per 16 bytes
+    bool v = p.c_conv_kw == 0 && p.split_k <= 1 && aligned16(p.C) && (p.ldc % 8) == 0;
+    if (batch > 1) v = v && ((p.sC1 | p.sC2) % ov) == 0 && ((p.sR1 | p.sR2) % epc) == 0;
+    if (p.bias) v = v && aligned16(p.bias);
+    if (p.gate) v = v && aligned16(p.gate) && (p.ldg % 8) == 0;
+    if (p.residual) v = v && aligned16(p.residual) && (p.ldr % 8) == 0;
+    p.vec_ok = v;
+  }
   const int gz = p.split_k > 1 ? p.split_k : batch;
   hipStream_t s = (hipStream_t)stream;
   if (d->dtype == FS2_BF16) return launch_gemm<bf16>(p, gz, s, d->a_kmajor, d->b_kmajor);

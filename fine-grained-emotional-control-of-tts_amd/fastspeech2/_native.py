@@ -74,6 +74,7 @@ Fl = ctypes.c_float
 SIGNATURES = {
     "fs2_gemm": (I, [ctypes.POINTER(GemmDesc), P]),
     "fs2_colsum": (I, [P, I64, I, I, I, P, I, P, P]),
+    "fs2_conv_fold": (I, [P, I, I, I, I, P, I64, P, I64, P, P, I, P]),
     "fs2_colsum_workspace_floats": (I64, [I, I]),
     "fs2_ln_fwd": (I, [P, I64, P, I64, Fl, U32, P, P, P, Fl, I, Fl, U32, P, P, I64, P, I64, P, P,
                        I, I, I, U32, P]),

@@ -123,9 +123,21 @@ class FS2Engine:
     def _dgrad(self, dY, lddy, M, T, wname, out, ldo, n_out=None, **epi):
         O, C, KW = self._wspecs[wname]
         _, Wb = self.w[wname]
-        conv = (2, T, KW, O) if KW > 1 else None
-        ops.gemm(M, n_out or C, KW * O, dY, lddy, Wb, KW * O, out, ldo, dt=self.dt, conv=conv,
-                 **epi)
+        if KW == 1:
+            ops.gemm(M, n_out or C, O, dY, lddy, Wb, O, out, ldo, dt=self.dt, **epi)
+            return
+        # reflect "same" conv data gradient = zero-padded shift conv over the padded domain
+        # (T+2P rows per utterance, fp32) + the reflect fold, which also applies the epilogue
+        P = (KW - 1) // 2
+        B = M // T
+        Mp = B * (T + 2 * P)
+        Xpad = torch.empty(Mp, C, dtype=torch.float32, device=self.dev)
+        ops.gemm(Mp, C, KW * O, dY, lddy, Wb, KW * O, Xpad, C, dt=self.dt, conv=(4, T, KW, O),
+                 c_fp32=1)
+        assert set(epi) <= {"residual", "ldr", "row_scale", "row_scale_post"}, epi
+        ops.conv_fold(Xpad, B, T, P, C, out, ldo, dt=self.dt, residual=epi.get("residual"),
+                      ldr=epi.get("ldr", 0), row_scale=epi.get("row_scale"),
+                      row_scale_post=epi.get("row_scale_post"))
 
     def _wgrad(self, dY, lddy, X, ldx, M, T, wname, n_cols=None):
         """grad[O][C][KW] += sum_m dY[m][o] * X[reflect(t+j-P)][c]   (fp32, accumulate)."""

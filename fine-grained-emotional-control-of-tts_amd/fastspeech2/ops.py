@@ -58,6 +58,12 @@ def gemm(M, N_, K, A, lda, B, ldb, C, ldc, *, dt, a_kmajor=1, b_kmajor=1, conv=N
     _chk(N.lib().fs2_gemm(ctypes.byref(d), _s()), "fs2_gemm")
 
 
+def conv_fold(Xpad, B, T, P, C, out, ldo, *, dt, residual=None, ldr=0, row_scale=None,
+              row_scale_post=None):
+    _chk(N.lib().fs2_conv_fold(_p(Xpad), B, T, P, C, _p(out), ldo, _p(residual), ldr,
+                               _p(row_scale), _p(row_scale_post), dt, _s()), "fs2_conv_fold")
+
+
 def colsum(X, ldx, M, N_, out, *, dt, ws, accumulate=1):
     _chk(N.lib().fs2_colsum(_p(X), ldx, M, N_, dt, _p(out), accumulate, _p(ws), _s()), "fs2_colsum")
 

@@ -49,6 +49,8 @@ typedef struct fs2_gemm_desc {
    *   1: A fwd   A(m=(b,t), k=(j,c)) = X[b, reflect(t+j-P), c]                  (a_kmajor)
    *   2: A dgrad A(m=(b,s), k=(j,o)) = sum_{t: reflect(t+j-P)=s} dY[b, t, o]     (a_kmajor)
    *   3: B wgrad B(k=(b,t), n=(j,c)) = X[b, reflect(t+j-P), c]                  (!b_kmajor)
+   *   4: A shift A(m=(b,p), k=(j,o)) = dY[b, p-j, o] (0 outside [0,T)), T+2P rows per
+   *      utterance: the data gradient in the padded domain, finished by fs2_conv_fold
    * P = (conv_kw-1)/2, conv_c = channels per tap, conv_t = tokens per utterance.          */
   int conv_mode, conv_t, conv_kw, conv_c;
   void* C; int64_t ldc; int c_fp32;           /* output; c_fp32: float output else dtype     */
@@ -67,6 +69,13 @@ typedef struct fs2_gemm_desc {
 } fs2_gemm_desc;
 
 int fs2_gemm(const fs2_gemm_desc* d, void* stream);
+
+/* reflect-padding adjoint + dgrad epilogue (K16): Xpad fp32 [B][T+2P][C] from conv_mode 4,
+ *   out[b,s] = ((Xpad[s+P] + Xpad[P-s]{1<=s<=P} + Xpad[2(T-1)-s+P]{T-1-P<=s<=T-2}) * rs
+ *              + residual) * rs2                                                           */
+int fs2_conv_fold(const float* Xpad, int B, int T, int P, int C, void* out, int64_t ldo,
+                  const void* residual, int64_t ldr, const float* row_scale,
+                  const float* row_scale_post, int dtype, void* stream);
 
 /* column sums: out[n] (+)= sum_m X[m][n]   (bias gradients; SB Linear/Conv1d bias, K16) */
 int fs2_colsum(const void* X, int64_t ldx, int M, int N, int dtype, float* out, int accumulate,

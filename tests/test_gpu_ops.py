@@ -291,3 +291,31 @@ def test_adamw_matches_torch(cuda):
         ops.adamw(p, g, m, v, n, 1 - lr * wd, 1 - b1, b2, 1 - b2, lr / (1 - b1 ** t),
                   (1 - b2 ** t) ** 0.5, 1e-8, 1.0)
     torch.testing.assert_close(p, ref.detach(), rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("dt,code,tol", DT)
+@pytest.mark.parametrize("KW,T", [(9, 37), (5, 6), (3, 2)])
+def test_conv_dgrad_shift_plus_fold(cuda, dt, code, tol, KW, T):
+    """conv_mode 4 (zero-padded shift conv over T+2P rows) + fs2_conv_fold == reflect-conv
+    data gradient, with the fused epilogue ((dX * rs) + residual) * rs2."""
+    from fastspeech2 import ops
+    torch.manual_seed(KW + T)
+    Bn, Cin, O = 3, 64, 96
+    P = (KW - 1) // 2
+    Wt = torch.randn(O, Cin, KW, device=cuda).to(dt).float()
+    Wb = Wt.permute(1, 2, 0).contiguous().to(dt)
+    Xr = torch.randn(Bn, T, Cin, device=cuda).requires_grad_(True)
+    out = F.conv1d(F.pad(Xr.transpose(1, 2), (P, P), mode="reflect"), Wt).transpose(1, 2)
+    G = torch.randn(out.shape, device=cuda).to(dt).contiguous()
+    out.backward(G.float())
+    Mp = Bn * (T + 2 * P)
+    Xpad = torch.empty(Mp, Cin, device=cuda)
+    ops.gemm(Mp, Cin, KW * O, G, O, Wb, KW * O, Xpad, Cin, dt=code, conv=(4, T, KW, O), c_fp32=1)
+    res = torch.randn(Bn * T, Cin, device=cuda).to(dt)
+    rs = (torch.rand(Bn * T, device=cuda) > 0.3).float()
+    rs2 = torch.rand(Bn * T, device=cuda)
+    dX = torch.empty(Bn * T, Cin, device=cuda, dtype=dt)
+    ops.conv_fold(Xpad, Bn, T, P, Cin, dX, Cin, dt=code, residual=res, ldr=Cin, row_scale=rs,
+                  row_scale_post=rs2)
+    ref = (Xr.grad.reshape(-1, Cin) * rs[:, None] + res.float()) * rs2[:, None]
+    assert rel(dX, ref) < tol
