@@ -48,6 +48,7 @@ struct GemmP {
   long sA1, sA2, sB1, sB2, sC1, sC2, sR1, sR2;
   int tiles_m, tiles_n;
   int vec_ok;
+  int vec_align;  // vector epilogue possible if K were not split
 };
 
 __device__ __forceinline__ u32x4 add_bf16x8(u32x4 a, u32x4 b) {
@@ -660,13 +661,21 @@ __global__ void __launch_bounds__(BNT) gemm_big_kernel(GemmP p) {
   const int bid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (orig >> 3);
   const int tm = bid / p.tiles_n, tn = bid - tm * p.tiles_n;
   const int m0 = tm * BBM, n0 = tn * 128;
-  const int z = blockIdx.z;
+  const int z = p.split_k > 1 ? 0 : blockIdx.z;
   const long zb = z / p.batch_div, zh = z - zb * p.batch_div;
   const char* Ab = p.A + (zb * p.sA1 + zh * p.sA2) * 2;
   const char* Bb = p.B + (zb * p.sB1 + zh * p.sB2) * 2;
   const int K = p.K;
   const int kva = min(K, p.kvalid);
   const int amode = (p.conv_mode == 1 || p.conv_mode == 4) ? p.conv_mode : 0;
+  // split-K: this block reduces k-tiles [kt0, kt1) and accumulates with fp32 atomics
+  const int nk_all = (K + 63) / 64;
+  int kt0 = 0, kt1 = nk_all;
+  if (p.split_k > 1) {
+    const int kps = (nk_all + p.split_k - 1) / p.split_k;
+    kt0 = blockIdx.z * kps;
+    kt1 = min(nk_all, kt0 + kps);
+  }
   const bool bconv3 = p.conv_mode == 3;
   const bool tap_uniform = amode && (p.conv_c % 64) == 0;  // a 64-wide k-tile sits in one tap
   const int rpu = amode == 4 ? p.conv_t + 2 * p.conv_p : p.conv_t;  // rows per utterance
@@ -786,19 +795,19 @@ __global__ void __launch_bounds__(BNT) gemm_big_kernel(GemmP p) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = (K + 63) / 64;
-  if (nk > 0) issue(0, 0);
-  if (nk > 1) issue(1, 1);
-  for (int kt = 0; kt < nk; ++kt) {
-    // tile kt landed for this wave (leave tile kt+1's 6 pieces in flight) ...
-    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  const int nk = kt1 - kt0;
+  if (nk > 0) issue(kt0, 0);
+  if (nk > 1) issue(kt0 + 1, 1);
+  for (int it = 0; it < nk; ++it) {
+    // tile it landed for this wave (leave tile it+1's 6 pieces in flight) ...
+    if (it + 1 < nk) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    // ... and for every wave; every wave is also done reading stage (kt+2)%3 == (kt-1)%3
+    // ... and for every wave; every wave is also done reading stage (it+2)%3 == (it-1)%3
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if (kt + 2 < nk) issue(kt + 2, (kt + 2) % 3);
-    const char* la = smem + (kt % 3) * BIG_STAGE;
+    if (it + 2 < nk) issue(kt0 + it + 2, (it + 2) % 3);
+    const char* la = smem + (it % 3) * BIG_STAGE;
     const char* lb = la + BIG_A;
     // all fragments of both k-steps first (distinct registers), then 32 MFMAs
     bf16x8 af[2][4], bfr[2][4];
@@ -842,6 +851,24 @@ __global__ void __launch_bounds__(BNT) gemm_big_kernel(GemmP p) {
         cs[row * 128 + (col ^ (((row >> 2) & 1) << 4))] = acc[i][j][r];
       }
   __syncthreads();
+  if (!p.vec_ok) {  // weight gradients: fp32, conv column remap n=(j,c) -> c*KW + j, atomics
+    const int cc = p.c_conv_kw > 0 ? p.N / p.c_conv_kw : 0;
+    const bool atomic = p.split_k > 1;
+    float* Cf = (float*)Cb;
+    for (int idx = tid; idx < BBM * 128; idx += BNT) {
+      const int row = idx >> 7, col = idx & 127;
+      const int m = m0 + row, n = n0 + col;
+      if (m >= p.mvalid || n >= p.nvalid) continue;
+      float v = cs[row * 128 + (col ^ (((row >> 2) & 1) << 4))];
+      long c2 = n;
+      if (cc > 0) { const int jj = n / cc; c2 = (long)(n - jj * cc) * p.c_conv_kw + jj; }
+      const long off = (long)m * p.ldc + c2;
+      if (atomic) atomicAdd(Cf + off, v);
+      else if (p.accumulate) Cf[off] += v;
+      else Cf[off] = v;
+    }
+    return;
+  }
   const int c8 = (tid & 15) * 8;
   const int n = n0 + c8;
 #pragma unroll 2
@@ -907,12 +934,34 @@ int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
   dim3 grid(p.tiles_m * p.tiles_n, 1, gz);
   if constexpr (sizeof(T) == 2) {
     // bf16: LDS-DMA for both operands, except the reflect-fold dgrad operand (register staged)
-    const int big_tiles = ((p.M + BBM - 1) / BBM) * p.tiles_n * gz;
-    if (p.conv_mode != 2 && p.vec_ok && p.split_k <= 1 && big_tiles >= 240 &&
-        !getenv_flag("FS2_GEMM_NO_BIG")) {
+    static const bool no_big = getenv_flag("FS2_GEMM_NO_BIG");
+    const int tiles_big = ((p.M + BBM - 1) / BBM) * p.tiles_n;
+    const int batch = p.split_k > 1 ? 1 : gz;
+    // weight-gradient GEMMs (fp32 accumulate, no epilogue ops): the big kernel picks its own
+    // K split; split > 1 takes the LDS-staged atomic epilogue (row-contiguous atomics)
+    const bool wgrad = p.c_fp32 && (p.accumulate || p.split_k > 1) && batch == 1 && !p.gate &&
+                       !p.residual && !p.bias && !p.row_scale && !p.row_scale_post && !p.relu &&
+                       p.c_conv_kw == 0 && p.vec_align;
+    int split_big = 1;
+    if (wgrad) {
+      const int nk = (p.K + 63) / 64;
+      split_big = max(1, min((480 + tiles_big - 1) / tiles_big, nk / 8));
+    }
+    const bool use_big = !no_big && p.conv_mode != 2 &&
+                         ((p.vec_ok && p.split_k <= 1 && tiles_big * batch >= 240) ||
+                          (wgrad && tiles_big * split_big >= 160));
+    if (use_big) {
       GemmP q = p;
       q.tiles_m = (p.M + BBM - 1) / BBM;
-      dim3 g2(q.tiles_m * q.tiles_n, 1, gz);
+      if (wgrad) {
+        q.split_k = split_big;
+        q.k_per_split = ((p.K + split_big - 1) / split_big + 63) / 64 * 64;
+        q.split_k = (p.K + q.k_per_split - 1) / q.k_per_split;
+        split_big = q.split_k;
+        q.vec_ok = split_big == 1;
+        q.accumulate = 1;
+      }
+      dim3 g2(q.tiles_m * q.tiles_n, 1, wgrad ? split_big : gz);
       if (ak && bk) hipLaunchKernelGGL((gemm_big_kernel<true, true>), g2, dim3(BNT), 0, s, q);
       else if (ak && !bk) hipLaunchKernelGGL((gemm_big_kernel<true, false>), g2, dim3(BNT), 0, s, q);
       else if (!ak && bk) hipLaunchKernelGGL((gemm_big_kernel<false, true>), g2, dim3(BNT), 0, s, q);
@@ -988,12 +1037,13 @@ extern "C" int fs2_gemm(const fs2_gemm_desc* d, void* stream) {
   {
     const int oes = p.c_fp32 ? 4 : es;
     const int ov = 16 / oes;  // output elements per 16 bytes
-    bool v = p.c_conv_kw == 0 && p.split_k <= 1 && aligned16(p.C) && (p.ldc % 8) == 0;
+    bool v = p.c_conv_kw == 0 && aligned16(p.C) && (p.ldc % 8) == 0;
     if (batch > 1) v = v && ((p.sC1 | p.sC2) % ov) == 0 && ((p.sR1 | p.sR2) % epc) == 0;
     if (p.bias) v = v && aligned16(p.bias);
     if (p.gate) v = v && aligned16(p.gate) && (p.ldg % 8) == 0;
     if (p.residual) v = v && aligned16(p.residual) && (p.ldr % 8) == 0;
-    p.vec_ok = v;
+    p.vec_align = v;
+    p.vec_ok = v && p.split_k <= 1;
   }
   const int gz = p.split_k > 1 ? p.split_k : batch;
   hipStream_t s = (hipStream_t)stream;

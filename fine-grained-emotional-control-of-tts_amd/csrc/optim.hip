@@ -32,8 +32,8 @@ __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
 }
 
 template <typename T>
-__global__ void weight_prep_kernel(const float* W, int O, int C, int KW, T* Wf, int ldf, T* Wb,
-                                   int ldb) {
+__global__ void weight_prep_kernel(const float* W, int O, int C, int KW, int okc, T* Wf, int ldf,
+                                   T* Wb, int ldb) {
   // one thread per (row of Wf / Wb, padded column): write-coalesced on Wf
   const long n = (long)O * ldf;
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -42,7 +42,7 @@ __global__ void weight_prep_kernel(const float* W, int O, int C, int KW, T* Wf, 
     float v = 0.f;
     if (col < KW * C) {
       const int j = col / C, c = col - j * C;
-      v = W[((long)o * C + c) * KW + j];
+      v = okc ? W[(long)o * KW * C + col] : W[((long)o * C + c) * KW + j];
     }
     Wf[i] = from_f<T>(v);
   }
@@ -53,7 +53,7 @@ __global__ void weight_prep_kernel(const float* W, int O, int C, int KW, T* Wf, 
       float v = 0.f;
       if (col < KW * O) {
         const int j = col / O, o = col - j * O;
-        v = W[((long)o * C + c) * KW + j];
+        v = okc ? W[((long)o * KW + j) * C + c] : W[((long)o * C + c) * KW + j];
       }
       Wb[i] = from_f<T>(v);
     }
@@ -76,17 +76,17 @@ extern "C" int fs2_adamw(float* param, const float* grad, float* exp_avg, float*
   return 0;
 }
 
-extern "C" int fs2_weight_prep(const float* W, int O, int C, int KW, void* Wf, int ldf, void* Wb,
-                               int ldb, int dtype, void* stream) {
+extern "C" int fs2_weight_prep(const float* W, int O, int C, int KW, int w_okc, void* Wf, int ldf,
+                               void* Wb, int ldb, int dtype, void* stream) {
   if (!W || !Wf || ldf < KW * C || (Wb && ldb < KW * O)) return FS2_EINVAL;
   const long n = max((long)O * ldf, Wb ? (long)C * ldb : 0L);
   const dim3 g((unsigned)((n + 255) / 256)), b(256);
   hipStream_t s = (hipStream_t)stream;
   if (dtype == FS2_BF16)
-    hipLaunchKernelGGL(weight_prep_kernel<bf16>, g, b, 0, s, W, O, C, KW, (bf16*)Wf, ldf,
+    hipLaunchKernelGGL(weight_prep_kernel<bf16>, g, b, 0, s, W, O, C, KW, w_okc, (bf16*)Wf, ldf,
                        (bf16*)Wb, ldb);
   else if (dtype == FS2_F32)
-    hipLaunchKernelGGL(weight_prep_kernel<float>, g, b, 0, s, W, O, C, KW, (float*)Wf, ldf,
+    hipLaunchKernelGGL(weight_prep_kernel<float>, g, b, 0, s, W, O, C, KW, w_okc, (float*)Wf, ldf,
                        (float*)Wb, ldb);
   else return FS2_EINVAL;
   FS2_CHECK_LAUNCH();

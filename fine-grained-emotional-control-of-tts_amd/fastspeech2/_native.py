@@ -102,7 +102,7 @@ SIGNATURES = {
     "fs2_loss_fwd_bwd": (I, [ctypes.POINTER(LossDesc), P]),
     "fs2_loss_workspace_floats": (I64, [I, I, I]),
     "fs2_adamw": (I, [P, P, P, P, I64, Fl, Fl, Fl, Fl, Fl, Fl, Fl, Fl, P]),
-    "fs2_weight_prep": (I, [P, I, I, I, P, I, P, I, I, P]),
+    "fs2_weight_prep": (I, [P, I, I, I, I, P, I, P, I, I, P]),
     "fs2_fill": (I, [P, I64, Fl, I, P]),
     "fs2_add": (I, [P, P, I64, Fl, I, P]),
     "fs2_cast": (I, [P, I, P, I, I64, P]),

@@ -110,7 +110,8 @@ class FS2Engine:
             if name not in self.w:
                 self.w[name] = (self.empty(O, ldf), self.empty(C, ldb))
             Wf, Wb = self.w[name]
-            ops.weight_prep(self.params[name], O, C, KW, Wf, ldf, Wb, ldb, dt=self.dt)
+            ops.weight_prep(self.params[name], O, C, KW, Wf, ldf, Wb, ldb, dt=self.dt,
+                            w_okc=int(KW > 1))
         self._prepared_version = ver
 
     def _fwd(self, X, ldx, M, T, wname, out, ldo, **epi):
@@ -140,7 +141,7 @@ class FS2Engine:
                       row_scale_post=epi.get("row_scale_post"))
 
     def _wgrad(self, dY, lddy, X, ldx, M, T, wname, n_cols=None):
-        """grad[O][C][KW] += sum_m dY[m][o] * X[reflect(t+j-P)][c]   (fp32, accumulate)."""
+        """grad[O][KW][C] += sum_m dY[m][o] * X[reflect(t+j-P)][c]   (fp32, accumulate)."""
         O, C, KW = self._wspecs[wname]
         Ncols = n_cols or KW * C
         K = round_up(M, self.epc)
@@ -149,9 +150,10 @@ class FS2Engine:
         if tiles < 256:
             split = max(1, min(-(-512 // tiles), K // (_BK[self.dt] * 4)))
         conv = (3, T, KW, C) if KW > 1 else None
+        # conv weight gradients land contiguous in the [O][KW][C] flat layout (model._kw_major)
         ops.gemm(O, Ncols, K, dY, lddy, X, ldx, self.grads[wname], C * KW, dt=self.dt, a_kmajor=0,
-                 b_kmajor=0, conv=conv, c_fp32=1, c_conv_kw=KW if KW > 1 else 0, kvalid=M,
-                 nvalid=KW * C, accumulate=1, split_k=split)
+                 b_kmajor=0, conv=conv, c_fp32=1, kvalid=M, nvalid=KW * C, accumulate=1,
+                 split_k=split)
 
     def _bias_grad(self, dY, lddy, M, n, gname):
         ops.colsum(dY, lddy, M, n, self.grads[gname], dt=self.dt, ws=self.ws(ops.colsum_ws(M, n)))

@@ -161,6 +161,11 @@ def _group_key(name, n_dec, n_enc):
     return (6, 0, 0)  # encPreNet
 
 
+def _kw_major(name, shape):
+    """Conv weights (O, C, KW>1) live in the flat buffer as [O][KW][C]."""
+    return len(shape) == 3 and shape[2] > 1 and name.endswith("conv.weight")
+
+
 def group_tag(key):
     g, _, layer = key
     return {0: "postnet", 1: "linear", 3: "variance", 4: "conditioning", 6: "prenet"}.get(
@@ -243,9 +248,17 @@ class FastSpeech2(nn.Module):
         views = {}
         for n, o, k, shape, _ in layout:
             p = params[n]
-            flat[o:o + k].copy_(p.detach().reshape(-1).float())
-            p.data = flat[o:o + k].view(shape)
-            views[n] = gflat[o:o + k].view(shape)
+            if _kw_major(n, shape):
+                # conv weight (O, C, KW) stored [O][KW][C] so GEMM operand images and weight
+                # gradients are contiguous; torch sees the same shape through a permuted view
+                O, C, KW = shape
+                flat[o:o + k].copy_(p.detach().permute(0, 2, 1).reshape(-1).float())
+                p.data = flat[o:o + k].view(O, KW, C).permute(0, 2, 1)
+                views[n] = gflat[o:o + k].view(O, KW, C).permute(0, 2, 1)
+            else:
+                flat[o:o + k].copy_(p.detach().reshape(-1).float())
+                p.data = flat[o:o + k].view(shape)
+                views[n] = gflat[o:o + k].view(shape)
         self._flat, self._gflat, self._grad_views, self._layout = flat, gflat, views, layout
         self._param_version += 1
         self._engine = None

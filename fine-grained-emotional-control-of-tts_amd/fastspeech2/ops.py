@@ -195,8 +195,8 @@ def adamw(param, grad, m, v, n, decay_mul, omb1, beta2, omb2, step_size, bc2_sqr
                            step_size, bc2_sqrt, eps, gscale, _s()), "fs2_adamw")
 
 
-def weight_prep(W, O, C, KW, Wf, ldf, Wb, ldb, *, dt):
-    _chk(N.lib().fs2_weight_prep(_p(W), O, C, KW, _p(Wf), ldf, _p(Wb), ldb, dt, _s()),
+def weight_prep(W, O, C, KW, Wf, ldf, Wb, ldb, *, dt, w_okc=0):
+    _chk(N.lib().fs2_weight_prep(_p(W), O, C, KW, w_okc, _p(Wf), ldf, _p(Wb), ldb, dt, _s()),
          "fs2_weight_prep")
 
 

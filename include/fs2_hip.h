@@ -215,10 +215,11 @@ int fs2_adamw(float* param, const float* grad, float* exp_avg, float* exp_avg_sq
               float decay_mul, float one_minus_beta1, float beta2, float one_minus_beta2,
               float step_size, float bc2_sqrt, float eps, float grad_scale, void* stream);
 
-/* torch weight W[O][C][KW] (fp32) -> fwd copy Wf[O][KW][C] and dgrad copy Wb[C][KW][O]
- * in dtype, each with row pitch padded to ldf / ldb elements (zeros in the pad).          */
-int fs2_weight_prep(const float* W, int O, int C, int KW, void* Wf, int ldf, void* Wb, int ldb,
-                    int dtype, void* stream);
+/* master weight W (fp32) -> fwd copy Wf[O][KW][C] and dgrad copy Wb[C][KW][O] in dtype, each
+ * with row pitch padded to ldf / ldb elements (zeros in the pad).  W is stored torch-style
+ * [O][C][KW] (w_okc = 0) or [O][KW][C] (w_okc = 1, the flat-buffer layout of conv weights). */
+int fs2_weight_prep(const float* W, int O, int C, int KW, int w_okc, void* Wf, int ldf, void* Wb,
+                    int ldb, int dtype, void* stream);
 
 /* utilities */
 int fs2_fill(void* X, int64_t n, float value, int dtype, void* stream);
