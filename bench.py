@@ -64,6 +64,18 @@ def cpu_baseline(cfg_all, args):
                       f"median of 2 steps after 1 warm-up; oracle/fs2_oracle.py"}
 
 
+def pmc_traffic():
+    """HBM bytes per launch of the roofline kernel from the newest committed PMC summary
+    (profiles/r*_roofline_traffic.json, written by tools/rocprof_summary.py traffic from two
+    separate rocprofv3 --pmc passes of this same bench command)."""
+    import glob
+    hits = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_roofline_traffic.json")))
+    if not hits:
+        return None, None
+    d = json.load(open(hits[-1]))
+    return d["hbm_bytes_per_launch"], os.path.relpath(hits[-1], ROOT)
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -119,6 +131,7 @@ def main():
         n, ms = ks.get("ffn_conv1_fwd.decoder", (0, float("nan")))
         kflop = 2.0 * (args.batch * Tm) * F * (KW * D)
         achieved = kflop / (ms * 1e-3) / 1e12 if n else None
+        traffic, traffic_src = pmc_traffic()
         step_ms = elapsed / args.steps * 1e3
         step_tflops = train_flops(c, args.batch, Tp, Tm) * world / (step_ms * 1e-3) / 1e12
         line = {
@@ -138,7 +151,8 @@ def main():
             "roofline": {"bound": "mfma", "kernel": "decoder FFN conv1 (k=9) implicit-GEMM fwd",
                          "achieved": achieved, "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": (achieved / MFMA_BF16_PEAK_TFLOPS) if achieved else None,
-                         "traffic": None, "launches": n, "avg_ms": ms,
+                         "traffic": traffic, "traffic_source": traffic_src,
+                         "launches": n, "avg_ms": ms,
                          "flop_per_launch": kflop},
             "step_mfma_frac": step_tflops / (MFMA_BF16_PEAK_TFLOPS * world),
             "kernel_ms": {k: v[1] for k, v in ks.items()},

@@ -1,0 +1,105 @@
+"""Summarise rocprofv3 output for profiles/.
+
+    python tools/rocprof_summary.py stats  <dir> <steps> [out.txt]
+        per-kernel time per train step from <dir>/**/*kernel_stats.csv
+    python tools/rocprof_summary.py kernel <dir> <kernel-substr> <grid> <min_us>
+        average duration of the matching dispatches in <dir>/**/*kernel_trace.csv (cross-check
+        of bench.py's live HIP-event timing of the roofline kernel)
+    python tools/rocprof_summary.py traffic <fetch_dir> <write_dir> <kernel-substr> <grid> <min_us> [out.json]
+        HBM bytes per launch of one kernel (dispatches matching name substring, grid size and
+        a minimum duration, which separates GEMMs of the same tiling but different K)
+        from two separate --pmc passes (FETCH_SIZE and WRITE_SIZE do not fit one TCC pass).
+
+Counter units and gfx950 corrections (MI355X_MICROARCH.md, HBM section; counter_defs.yaml):
+FETCH_SIZE and WRITE_SIZE are kilobytes (expression / 1024); on gfx950 FETCH_SIZE reports
+half the bytes of wide coalesced reads (16 B/lane global_load and buffer_load ... lds), so
+bytes_read = 2 * 1024 * FETCH_SIZE; WRITE_SIZE is exact for 16 B/lane stores and fp32 atomics.
+"""
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def _find(d, suffix):
+    hits = sorted(glob.glob(os.path.join(d, "**", "*" + suffix), recursive=True))
+    if not hits:
+        raise SystemExit(f"no *{suffix} under {d}")
+    return hits
+
+
+def stats(d, steps, out=None):
+    rows = []
+    for f in _find(d, "kernel_stats.csv"):
+        rows += list(csv.DictReader(open(f)))
+    tot = sum(float(r["TotalDurationNs"]) for r in rows)
+    lines = [f"kernel time per step: {tot / steps / 1e6:.3f} ms  ({steps} steps profiled, "
+             f"includes warm-up launches if the run had any)"]
+    for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"])):
+        lines.append(f'{float(r["TotalDurationNs"]) / steps / 1e6:8.3f} ms/step '
+                     f'{float(r["AverageNs"]) / 1e3:9.1f} us avg {int(r["Calls"]):6d} calls  '
+                     f'{r["Name"][:110]}')
+    txt = "\n".join(lines)
+    if out:
+        open(out, "w").write(txt + "\n")
+    print(txt)
+
+
+def kernel(d, name_sub, grid, min_us):
+    durs = []
+    for f in _find(d, "kernel_trace.csv"):
+        for r in csv.DictReader(open(f)):
+            if name_sub not in r["Kernel_Name"] or int(r["Grid_Size_X"]) != grid:
+                continue
+            us = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+            if us >= min_us:
+                durs.append(us)
+    if not durs:
+        raise SystemExit("no matching dispatches")
+    print(f"{name_sub} grid {grid} (>= {min_us} us): {len(durs)} dispatches, "
+          f"avg {sum(durs) / len(durs):.1f} us, min {min(durs):.1f}, max {max(durs):.1f}")
+
+
+def _per_dispatch(d, counter, name_sub, grid, min_us):
+    vals = {}
+    for f in _find(d, "counter_collection.csv"):
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] != counter or name_sub not in r["Kernel_Name"]:
+                continue
+            if int(r["Grid_Size"]) != grid:
+                continue
+            if (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) < min_us * 1e3:
+                continue
+            key = (f, r["Dispatch_Id"])
+            vals[key] = vals.get(key, 0.0) + float(r["Counter_Value"])
+    if not vals:
+        raise SystemExit(f"no {counter} rows for {name_sub!r} grid {grid} under {d}")
+    return list(vals.values())
+
+
+def traffic(fdir, wdir, name_sub, grid, min_us, out=None):
+    fk = _per_dispatch(fdir, "FETCH_SIZE", name_sub, grid, min_us)
+    wk = _per_dispatch(wdir, "WRITE_SIZE", name_sub, grid, min_us)
+    rd = 2.0 * 1024.0 * sum(fk) / len(fk)
+    wr = 1024.0 * sum(wk) / len(wk)
+    res = {"kernel_substr": name_sub, "grid_size": grid, "min_us": min_us,
+           "dispatches": [len(fk), len(wk)],
+           "read_bytes_per_launch": rd, "write_bytes_per_launch": wr,
+           "hbm_bytes_per_launch": rd + wr,
+           "correction": "read = 2*1024*FETCH_SIZE (gfx950 half-count), write = 1024*WRITE_SIZE"}
+    if out:
+        json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "stats":
+        stats(sys.argv[2], int(sys.argv[3]), sys.argv[4] if len(sys.argv) > 4 else None)
+    elif sys.argv[1] == "kernel":
+        kernel(sys.argv[2], sys.argv[3], int(sys.argv[4]), float(sys.argv[5]))
+    elif sys.argv[1] == "traffic":
+        traffic(sys.argv[2], sys.argv[3], sys.argv[4], int(sys.argv[5]), float(sys.argv[6]),
+                sys.argv[7] if len(sys.argv) > 7 else None)
+    else:
+        raise SystemExit(__doc__)
