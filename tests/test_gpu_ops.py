@@ -319,3 +319,42 @@ def test_conv_dgrad_shift_plus_fold(cuda, dt, code, tol, KW, T):
                   row_scale_post=rs2)
     ref = (Xr.grad.reshape(-1, Cin) * rs[:, None] + res.float()) * rs2[:, None]
     assert rel(dX, ref) < tol
+
+
+@pytest.mark.parametrize("Bn,T", [(32, 640), (1, 640)])
+def test_gemm_big_tile_paths_bf16(cuda, Bn, T):
+    """BASELINE-sized GEMMs that take the 256x128 LDS-DMA kernel (gemm_big_kernel): implicit
+    reflect conv k=9 forward with bias+ReLU, zero-padded shift-conv data gradient + fold, and
+    the weight gradient into the [O][KW][C] layout -- split-K with atomics at Bn=32, the
+    single-split vector accumulate epilogue at Bn=1.  bf16 inputs, fp32 reference on the same
+    bf16 values, rel 2e-2."""
+    from fastspeech2 import ops
+    torch.manual_seed(Bn)
+    Cin, O, KW = 384, 1536, 9
+    P = (KW - 1) // 2
+    M = Bn * T
+    X = torch.randn(Bn, T, Cin, device=cuda).to(torch.bfloat16)
+    Wt = (torch.randn(O, Cin, KW, device=cuda) * 0.05).to(torch.bfloat16).float()
+    bias = torch.randn(O, device=cuda)
+    Wf = Wt.permute(0, 2, 1).contiguous().to(torch.bfloat16)
+    Wb = Wt.permute(1, 2, 0).contiguous().to(torch.bfloat16)
+    Xr = X.float().clone().requires_grad_(True)
+    Wr = Wt.clone().requires_grad_(True)
+    pre = F.conv1d(F.pad(Xr.transpose(1, 2), (P, P), mode="reflect"), Wr, bias).transpose(1, 2)
+    out = torch.relu(pre)
+    G = torch.randn(out.shape, device=cuda).to(torch.bfloat16).contiguous()
+    pre.backward(G.float())          # data/weight gradients of the conv itself (no ReLU gate)
+    Y = torch.empty(M, O, device=cuda, dtype=torch.bfloat16)
+    ops.gemm(M, O, KW * Cin, X, Cin, Wf, KW * Cin, Y, O, dt=1, conv=(1, T, KW, Cin), bias=bias,
+             relu=1)
+    assert rel(Y, out.detach().reshape(-1, O)) < 2e-2
+    Mp = Bn * (T + 2 * P)
+    Xpad = torch.empty(Mp, Cin, device=cuda)
+    ops.gemm(Mp, Cin, KW * O, G, O, Wb, KW * O, Xpad, Cin, dt=1, conv=(4, T, KW, O), c_fp32=1)
+    dX = torch.empty(M, Cin, device=cuda, dtype=torch.bfloat16)
+    ops.conv_fold(Xpad, Bn, T, P, Cin, dX, Cin, dt=1)
+    assert rel(dX, Xr.grad.reshape(-1, Cin)) < 2e-2
+    dW = torch.full((O, KW, Cin), 0.5, device=cuda)        # accumulates onto existing values
+    ops.gemm(O, KW * Cin, ops.round_up(M, 8), G, O, X, Cin, dW, KW * Cin, dt=1, a_kmajor=0,
+             b_kmajor=0, conv=(3, T, KW, Cin), c_fp32=1, kvalid=M, accumulate=1)
+    assert rel(dW - 0.5, Wr.grad.permute(0, 2, 1)) < 2e-2
