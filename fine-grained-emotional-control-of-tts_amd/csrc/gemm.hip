@@ -44,6 +44,7 @@ struct GemmP {
   const char* residual; long ldr;
   const float* row_scale_post;
   int accumulate; int split_k; int k_per_split;
+  long split_stride;  // >0: split z stores its partial to C + z*split_stride (no atomics)
   int batch_div;
   long sA1, sA2, sB1, sB2, sC1, sC2, sR1, sR2;
   int tiles_m, tiles_n;
@@ -467,8 +468,9 @@ __global__ void __launch_bounds__(NT) gemm_kernel(GemmP p) {
   // ---- epilogue ----
   const int OES = p.c_fp32 ? 4 : ES;
   char* Cb = p.C + (zb * p.sC1 + zh * p.sC2) * OES;
+  if (p.split_stride > 0 && p.split_k > 1) Cb += (long)blockIdx.z * p.split_stride * OES;
   const char* Rb = p.residual ? p.residual + (zb * p.sR1 + zh * p.sR2) * ES : nullptr;
-  const bool atomic = p.split_k > 1;
+  const bool atomic = p.split_k > 1 && p.split_stride == 0;
   const int cc = p.c_conv_kw > 0 ? p.N / p.c_conv_kw : 0;
   if (!p.vec_ok) {  // scalar path: scattered (conv-remapped) or atomic fp32 gradient outputs
 #pragma unroll
@@ -838,6 +840,7 @@ __global__ void __launch_bounds__(BNT) gemm_big_kernel(GemmP p) {
 
   // ---- epilogue: fp32 tile through LDS, 16-byte vector pass (same ops as gemm_kernel) ----
   char* Cb = p.C + (zb * p.sC1 + zh * p.sC2) * (p.c_fp32 ? 4 : 2);
+  if (p.split_stride > 0 && p.split_k > 1) Cb += (long)blockIdx.z * p.split_stride * 4;
   const char* Rb = p.residual ? p.residual + (zb * p.sR1 + zh * p.sR2) * 2 : nullptr;
   float* cs = (float*)smem;
 #pragma unroll
@@ -853,7 +856,7 @@ __global__ void __launch_bounds__(BNT) gemm_big_kernel(GemmP p) {
   __syncthreads();
   if (!p.vec_ok) {  // weight gradients: fp32, conv column remap n=(j,c) -> c*KW + j, atomics
     const int cc = p.c_conv_kw > 0 ? p.N / p.c_conv_kw : 0;
-    const bool atomic = p.split_k > 1;
+    const bool atomic = p.split_k > 1 && p.split_stride == 0;
     float* Cf = (float*)Cb;
     for (int idx = tid; idx < BBM * 128; idx += BNT) {
       const int row = idx >> 7, col = idx & 127;
@@ -939,7 +942,8 @@ int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
     const int batch = p.split_k > 1 ? 1 : gz;
     // weight-gradient GEMMs (fp32 accumulate, no epilogue ops): the big kernel picks its own
     // K split; split > 1 takes the LDS-staged atomic epilogue (row-contiguous atomics)
-    const bool wgrad = p.c_fp32 && (p.accumulate || p.split_k > 1) && batch == 1 && !p.gate &&
+    const bool wgrad = p.split_stride == 0 && p.c_fp32 && (p.accumulate || p.split_k > 1) &&
+                       batch == 1 && !p.gate &&
                        !p.residual && !p.bias && !p.row_scale && !p.row_scale_post && !p.relu &&
                        p.c_conv_kw == 0 && p.vec_align;
     int split_big = 1;
@@ -947,8 +951,10 @@ int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
       const int nk = (p.K + 63) / 64;
       split_big = max(1, min((480 + tiles_big - 1) / tiles_big, nk / 8));
     }
+    const bool slices = p.split_stride > 0 && p.split_k > 1;  // caller-chosen split, plain stores
     const bool use_big = !no_big && p.conv_mode != 2 &&
                          ((p.vec_ok && p.split_k <= 1 && tiles_big * batch >= 240) ||
+                          (slices && p.vec_ok && tiles_big * p.split_k >= 160) ||
                           (wgrad && tiles_big * split_big >= 160));
     if (use_big) {
       GemmP q = p;
@@ -961,7 +967,7 @@ int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
         q.vec_ok = split_big == 1;
         q.accumulate = 1;
       }
-      dim3 g2(q.tiles_m * q.tiles_n, 1, wgrad ? split_big : gz);
+      dim3 g2(q.tiles_m * q.tiles_n, 1, wgrad ? split_big : (slices ? p.split_k : gz));
       if (ak && bk) hipLaunchKernelGGL((gemm_big_kernel<true, true>), g2, dim3(BNT), 0, s, q);
       else if (ak && !bk) hipLaunchKernelGGL((gemm_big_kernel<true, false>), g2, dim3(BNT), 0, s, q);
       else if (!ak && bk) hipLaunchKernelGGL((gemm_big_kernel<false, true>), g2, dim3(BNT), 0, s, q);
@@ -1001,6 +1007,7 @@ extern "C" int fs2_gemm(const fs2_gemm_desc* d, void* stream) {
   p.row_scale_post = d->row_scale_post;
   p.accumulate = d->accumulate;
   p.split_k = d->split_k > 1 ? d->split_k : 1;
+  p.split_stride = d->split_stride > 0 ? d->split_stride : 0;
   p.batch_div = d->batch_div > 0 ? d->batch_div : 1;
   p.sA1 = d->sA1; p.sA2 = d->sA2; p.sB1 = d->sB1; p.sB2 = d->sB2;
   p.sC1 = d->sC1; p.sC2 = d->sC2; p.sR1 = d->sR1; p.sR2 = d->sR2;
@@ -1028,10 +1035,16 @@ extern "C" int fs2_gemm(const fs2_gemm_desc* d, void* stream) {
     if (p.conv_mode == 3 && (d->b_kmajor || p.N != p.conv_kw * p.conv_c)) return FS2_EINVAL;
   }
   if (p.c_conv_kw > 0 && (p.N % p.c_conv_kw)) return FS2_EINVAL;
+  int split_req = p.split_k;
   if (p.split_k > 1) {
     if (!p.c_fp32 || batch > 1) return FS2_EINVAL;
-    p.k_per_split = ((p.K + p.split_k - 1) / p.split_k + bk - 1) / bk * bk;
-    p.split_k = (p.K + p.k_per_split - 1) / p.k_per_split;
+    if (p.split_stride > 0 && (p.accumulate || p.split_stride < (long)(p.mvalid - 1) * p.ldc + p.nvalid))
+      return FS2_EINVAL;
+    // k-tiles per split (64-wide for bf16 in both kernels, 32 for fp32)
+    const int nkt = (p.K + bk - 1) / bk;
+    const int kps = (nkt + p.split_k - 1) / p.split_k;
+    p.k_per_split = kps * bk;
+    p.split_k = (nkt + kps - 1) / kps;
   }
   if (p.accumulate && !p.c_fp32) return FS2_EINVAL;
   {
@@ -1043,7 +1056,17 @@ extern "C" int fs2_gemm(const fs2_gemm_desc* d, void* stream) {
     if (p.gate) v = v && aligned16(p.gate) && (p.ldg % 8) == 0;
     if (p.residual) v = v && aligned16(p.residual) && (p.ldr % 8) == 0;
     p.vec_align = v;
-    p.vec_ok = v && p.split_k <= 1;
+    p.vec_ok = v && (p.split_k <= 1 || p.split_stride > 0);
+  }
+  hipStream_t s0 = (hipStream_t)stream;
+  if (p.split_stride > 0) {
+    // slices the shortened split leaves unwritten read as zero
+    const int oes = p.c_fp32 ? 4 : es;
+    for (int z = max(p.split_k, 1); z < split_req; ++z)
+      if (hipMemset2DAsync(p.C + (long)z * p.split_stride * oes, p.ldc * oes, 0,
+                           (size_t)p.nvalid * oes, p.mvalid, s0) != hipSuccess)
+        return FS2_EINVAL;
+    if (p.split_k <= 1) p.split_stride = 0;
   }
   const int gz = p.split_k > 1 ? p.split_k : batch;
   hipStream_t s = (hipStream_t)stream;

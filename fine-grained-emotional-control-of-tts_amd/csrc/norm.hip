@@ -195,29 +195,27 @@ __global__ void colsum_partial_kernel(const T* X, long ldx, int M, int N, int ro
 // where Xp (fp32, T+2P rows per utterance) is the zero-padded shift-conv GEMM output
 // (fs2_gemm conv_mode 4), fused with the dgrad epilogue: out = (dX*rs + residual)*rs2.
 template <typename T>
-__global__ void conv_fold_kernel(const float* Xp, int T_, int P, int C, T* out, long ldo,
-                                 const T* res, long ldr, const float* rs, const float* rs2,
-                                 long n) {
+__global__ void conv_fold_kernel(const float* Xp, int nsplit, long sstride, int T_, int P, int C,
+                                 T* out, long ldo, const T* res, long ldr, const float* rs,
+                                 const float* rs2, long n) {
   const long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
   if (i >= n) return;
   const long m = i / C;
   const int c = (int)(i - m * C);
   const int b = (int)(m / T_), s = (int)(m - (long)b * T_);
   const long rb = (long)b * (T_ + 2 * P);
-  const f32x4 a = *(const f32x4*)(Xp + (rb + s + P) * C + c);
-  float v[4] = {a[0], a[1], a[2], a[3]};
-  if (s >= 1 && s <= P) {
-    const f32x4 e = *(const f32x4*)(Xp + (rb + P - s) * C + c);
-    v[0] += e[0]; v[1] += e[1]; v[2] += e[2]; v[3] += e[3];
-  }
-  if (s >= T_ - 1 - P && s <= T_ - 2) {
-    const f32x4 e = *(const f32x4*)(Xp + (rb + 2 * (T_ - 1) - s + P) * C + c);
-    v[0] += e[0]; v[1] += e[1]; v[2] += e[2]; v[3] += e[3];
+  const bool lo = s >= 1 && s <= P, hi = s >= T_ - 1 - P && s <= T_ - 2;
+  f32x4 a = {0.f, 0.f, 0.f, 0.f};
+  for (int z = 0; z < nsplit; ++z) {
+    const float* X = Xp + z * sstride;
+    a += *(const f32x4*)(X + (rb + s + P) * C + c);
+    if (lo) a += *(const f32x4*)(X + (rb + P - s) * C + c);
+    if (hi) a += *(const f32x4*)(X + (rb + 2 * (T_ - 1) - s + P) * C + c);
   }
   const float r1 = rs ? rs[m] : 1.f, r2 = rs2 ? rs2[m] : 1.f;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
-    float x = v[e] * r1;
+    float x = a[e] * r1;
     if (res) x += to_f(res[m * ldr + c + e]);
     out[m * ldo + c + e] = from_f<T>(x * r2);
   }
@@ -302,21 +300,26 @@ extern "C" int fs2_colsum(const void* X, int64_t ldx, int M, int N, int dtype, f
   return 0;
 }
 
-extern "C" int fs2_conv_fold(const float* Xpad, int B, int T, int P, int C, void* out,
-                             int64_t ldo, const void* residual, int64_t ldr,
-                             const float* row_scale, const float* row_scale_post, int dtype,
-                             void* stream) {
+extern "C" int fs2_conv_fold(const float* Xpad, int nsplit, int64_t split_stride, int B, int T,
+                             int P, int C, void* out, int64_t ldo, const void* residual,
+                             int64_t ldr, const float* row_scale, const float* row_scale_post,
+                             int dtype, void* stream) {
   const long n = (long)B * T * C;
   if (n == 0) return 0;
+  if (nsplit < 1) nsplit = 1;
   if (!Xpad || !out || (C % 4) || P < 0 || (P > 0 && P >= T)) return FS2_EINVAL;
+  if (nsplit > 1 && (split_stride < (long)B * (T + 2 * P) * C || (split_stride % 4)))
+    return FS2_EINVAL;
   const dim3 g((unsigned)((n / 4 + 255) / 256)), b(256);
   hipStream_t s = (hipStream_t)stream;
   if (dtype == FS2_BF16)
-    hipLaunchKernelGGL(conv_fold_kernel<bf16>, g, b, 0, s, Xpad, T, P, C, (bf16*)out, (long)ldo,
-                       (const bf16*)residual, (long)ldr, row_scale, row_scale_post, n);
+    hipLaunchKernelGGL(conv_fold_kernel<bf16>, g, b, 0, s, Xpad, nsplit, (long)split_stride, T,
+                       P, C, (bf16*)out, (long)ldo, (const bf16*)residual, (long)ldr, row_scale,
+                       row_scale_post, n);
   else if (dtype == FS2_F32)
-    hipLaunchKernelGGL(conv_fold_kernel<float>, g, b, 0, s, Xpad, T, P, C, (float*)out, (long)ldo,
-                       (const float*)residual, (long)ldr, row_scale, row_scale_post, n);
+    hipLaunchKernelGGL(conv_fold_kernel<float>, g, b, 0, s, Xpad, nsplit, (long)split_stride, T,
+                       P, C, (float*)out, (long)ldo, (const float*)residual, (long)ldr, row_scale,
+                       row_scale_post, n);
   else return FS2_EINVAL;
   FS2_CHECK_LAUNCH();
   return 0;

@@ -38,6 +38,7 @@ class GemmDesc(ctypes.Structure):
         ("residual", ctypes.c_void_p), ("ldr", ctypes.c_int64),
         ("row_scale_post", ctypes.c_void_p),
         ("accumulate", ctypes.c_int), ("split_k", ctypes.c_int),
+        ("split_stride", ctypes.c_int64),
         ("batch", ctypes.c_int), ("batch_div", ctypes.c_int),
         ("sA1", ctypes.c_int64), ("sA2", ctypes.c_int64), ("sB1", ctypes.c_int64),
         ("sB2", ctypes.c_int64), ("sC1", ctypes.c_int64), ("sC2", ctypes.c_int64),
@@ -74,7 +75,7 @@ Fl = ctypes.c_float
 SIGNATURES = {
     "fs2_gemm": (I, [ctypes.POINTER(GemmDesc), P]),
     "fs2_colsum": (I, [P, I64, I, I, I, P, I, P, P]),
-    "fs2_conv_fold": (I, [P, I, I, I, I, P, I64, P, I64, P, P, I, P]),
+    "fs2_conv_fold": (I, [P, I, I64, I, I, I, I, P, I64, P, I64, P, P, I, P]),
     "fs2_colsum_workspace_floats": (I64, [I, I]),
     "fs2_ln_fwd": (I, [P, I64, P, I64, Fl, U32, P, P, P, Fl, I, Fl, U32, P, P, I64, P, I64, P, P,
                        I, I, I, U32, P]),

@@ -33,6 +33,17 @@ class _Salt:
         return self.n
 
 
+def dgrad_split(Mp, C, K, dt):
+    """K split for the shift-conv data gradient when its output tiles underfill the chip (the
+    encoder, T=200: 78 tiles of 256x128 for 256 CUs).  Slices are summed by fs2_conv_fold."""
+    if dt != 1:
+        return 1
+    tiles = -(-Mp // 256) * -(-C // 128)
+    if tiles >= 240:
+        return 1
+    return max(1, min(-(-480 // tiles), (K // 64) // 8))
+
+
 class FS2Engine:
     def __init__(self, model, act_dtype=torch.float32):
         self.m = model
@@ -132,13 +143,15 @@ class FS2Engine:
         P = (KW - 1) // 2
         B = M // T
         Mp = B * (T + 2 * P)
-        Xpad = torch.empty(Mp, C, dtype=torch.float32, device=self.dev)
+        split = dgrad_split(Mp, C, KW * O, self.dt)
+        Xpad = torch.empty(split, Mp, C, dtype=torch.float32, device=self.dev)
         ops.gemm(Mp, C, KW * O, dY, lddy, Wb, KW * O, Xpad, C, dt=self.dt, conv=(4, T, KW, O),
-                 c_fp32=1)
+                 c_fp32=1, split_k=split, split_stride=Mp * C if split > 1 else 0)
         assert set(epi) <= {"residual", "ldr", "row_scale", "row_scale_post"}, epi
         ops.conv_fold(Xpad, B, T, P, C, out, ldo, dt=self.dt, residual=epi.get("residual"),
                       ldr=epi.get("ldr", 0), row_scale=epi.get("row_scale"),
-                      row_scale_post=epi.get("row_scale_post"))
+                      row_scale_post=epi.get("row_scale_post"), nsplit=split,
+                      split_stride=Mp * C)
 
     def _wgrad(self, dY, lddy, X, ldx, M, T, wname, n_cols=None):
         """grad[O][KW][C] += sum_m dY[m][o] * X[reflect(t+j-P)][c]   (fp32, accumulate)."""

@@ -37,8 +37,8 @@ def round_up(x, m):
 
 def gemm(M, N_, K, A, lda, B, ldb, C, ldc, *, dt, a_kmajor=1, b_kmajor=1, conv=None, c_fp32=0,
          c_conv_kw=0, bias=None, relu=0, gate=None, ldg=0, row_scale=None, residual=None, ldr=0,
-         row_scale_post=None, accumulate=0, split_k=1, kvalid=0, mvalid=0, nvalid=0, batch=1,
-         batch_div=1, strides=None):
+         row_scale_post=None, accumulate=0, split_k=1, split_stride=0, kvalid=0, mvalid=0,
+         nvalid=0, batch=1, batch_div=1, strides=None):
     d = N.GemmDesc()
     d.M, d.N, d.K, d.kvalid, d.mvalid, d.nvalid, d.dtype = M, N_, K, kvalid, mvalid, nvalid, dt
     d.A, d.lda, d.a_kmajor = _p(A), lda, a_kmajor
@@ -51,7 +51,7 @@ def gemm(M, N_, K, A, lda, B, ldb, C, ldc, *, dt, a_kmajor=1, b_kmajor=1, conv=N
     d.row_scale = _p(row_scale)
     d.residual, d.ldr = _p(residual), ldr
     d.row_scale_post = _p(row_scale_post)
-    d.accumulate, d.split_k = accumulate, split_k
+    d.accumulate, d.split_k, d.split_stride = accumulate, split_k, split_stride
     d.batch, d.batch_div = batch, batch_div
     if strides is not None:
         (d.sA1, d.sA2, d.sB1, d.sB2, d.sC1, d.sC2, d.sR1, d.sR2) = strides
@@ -59,8 +59,9 @@ def gemm(M, N_, K, A, lda, B, ldb, C, ldc, *, dt, a_kmajor=1, b_kmajor=1, conv=N
 
 
 def conv_fold(Xpad, B, T, P, C, out, ldo, *, dt, residual=None, ldr=0, row_scale=None,
-              row_scale_post=None):
-    _chk(N.lib().fs2_conv_fold(_p(Xpad), B, T, P, C, _p(out), ldo, _p(residual), ldr,
+              row_scale_post=None, nsplit=1, split_stride=0):
+    _chk(N.lib().fs2_conv_fold(_p(Xpad), nsplit, split_stride, B, T, P, C, _p(out), ldo,
+                               _p(residual), ldr,
                                _p(row_scale), _p(row_scale_post), dt, _s()), "fs2_conv_fold")
 
 

@@ -63,6 +63,9 @@ typedef struct fs2_gemm_desc {
   const float* row_scale_post;                /* [M]: v *= row_scale_post[m]                 */
   int accumulate;       /* fp32 output only: C += v (split_k > 1 implies atomic accumulate)   */
   int split_k;          /* >1: K split over blockIdx.z, fp32 atomics into C                  */
+  int64_t split_stride; /* >0 (with split_k > 1, !accumulate): split z stores its fp32 partial
+                         * to C + z*split_stride elements instead -- no atomics; slices a
+                         * shortened split leaves unused are zeroed.  Consumers sum slices.    */
   /* batched: z in [0,batch): offset(z) = (z / batch_div)*s1 + (z % batch_div)*s2 (elements) */
   int batch, batch_div;
   int64_t sA1, sA2, sB1, sB2, sC1, sC2, sR1, sR2;
@@ -70,12 +73,13 @@ typedef struct fs2_gemm_desc {
 
 int fs2_gemm(const fs2_gemm_desc* d, void* stream);
 
-/* reflect-padding adjoint + dgrad epilogue (K16): Xpad fp32 [B][T+2P][C] from conv_mode 4,
+/* reflect-padding adjoint + dgrad epilogue (K16): Xpad fp32 [B][T+2P][C] from conv_mode 4
+ * (nsplit split-K slices split_stride floats apart, summed here; nsplit <= 1: one slice),
  *   out[b,s] = ((Xpad[s+P] + Xpad[P-s]{1<=s<=P} + Xpad[2(T-1)-s+P]{T-1-P<=s<=T-2}) * rs
  *              + residual) * rs2                                                           */
-int fs2_conv_fold(const float* Xpad, int B, int T, int P, int C, void* out, int64_t ldo,
-                  const void* residual, int64_t ldr, const float* row_scale,
-                  const float* row_scale_post, int dtype, void* stream);
+int fs2_conv_fold(const float* Xpad, int nsplit, int64_t split_stride, int B, int T, int P,
+                  int C, void* out, int64_t ldo, const void* residual, int64_t ldr,
+                  const float* row_scale, const float* row_scale_post, int dtype, void* stream);
 
 /* column sums: out[n] (+)= sum_m X[m][n]   (bias gradients; SB Linear/Conv1d bias, K16) */
 int fs2_colsum(const void* X, int64_t ldx, int M, int N, int dtype, float* out, int accumulate,

@@ -295,9 +295,12 @@ def test_adamw_matches_torch(cuda):
 
 @pytest.mark.parametrize("dt,code,tol", DT)
 @pytest.mark.parametrize("KW,T", [(9, 37), (5, 6), (3, 2)])
-def test_conv_dgrad_shift_plus_fold(cuda, dt, code, tol, KW, T):
+@pytest.mark.parametrize("split", [1, 4])
+def test_conv_dgrad_shift_plus_fold(cuda, dt, code, tol, KW, T, split):
     """conv_mode 4 (zero-padded shift conv over T+2P rows) + fs2_conv_fold == reflect-conv
-    data gradient, with the fused epilogue ((dX * rs) + residual) * rs2."""
+    data gradient, with the fused epilogue ((dX * rs) + residual) * rs2.  split > 1: split-K
+    partials stored to separate slices (a shortened split zeroes the unused ones; the slices
+    start as NaN to prove it) and summed by the fold."""
     from fastspeech2 import ops
     torch.manual_seed(KW + T)
     Bn, Cin, O = 3, 64, 96
@@ -309,24 +312,26 @@ def test_conv_dgrad_shift_plus_fold(cuda, dt, code, tol, KW, T):
     G = torch.randn(out.shape, device=cuda).to(dt).contiguous()
     out.backward(G.float())
     Mp = Bn * (T + 2 * P)
-    Xpad = torch.empty(Mp, Cin, device=cuda)
-    ops.gemm(Mp, Cin, KW * O, G, O, Wb, KW * O, Xpad, Cin, dt=code, conv=(4, T, KW, O), c_fp32=1)
+    Xpad = torch.full((split, Mp, Cin), float("nan"), device=cuda)
+    ops.gemm(Mp, Cin, KW * O, G, O, Wb, KW * O, Xpad, Cin, dt=code, conv=(4, T, KW, O), c_fp32=1,
+             split_k=split, split_stride=Mp * Cin if split > 1 else 0)
     res = torch.randn(Bn * T, Cin, device=cuda).to(dt)
     rs = (torch.rand(Bn * T, device=cuda) > 0.3).float()
     rs2 = torch.rand(Bn * T, device=cuda)
     dX = torch.empty(Bn * T, Cin, device=cuda, dtype=dt)
     ops.conv_fold(Xpad, Bn, T, P, Cin, dX, Cin, dt=code, residual=res, ldr=Cin, row_scale=rs,
-                  row_scale_post=rs2)
+                  row_scale_post=rs2, nsplit=split, split_stride=Mp * Cin)
     ref = (Xr.grad.reshape(-1, Cin) * rs[:, None] + res.float()) * rs2[:, None]
     assert rel(dX, ref) < tol
 
 
-@pytest.mark.parametrize("Bn,T", [(32, 640), (1, 640)])
+@pytest.mark.parametrize("Bn,T", [(32, 640), (1, 640), (32, 200)])
 def test_gemm_big_tile_paths_bf16(cuda, Bn, T):
     """BASELINE-sized GEMMs that take the 256x128 LDS-DMA kernel (gemm_big_kernel): implicit
     reflect conv k=9 forward with bias+ReLU, zero-padded shift-conv data gradient + fold, and
     the weight gradient into the [O][KW][C] layout -- split-K with atomics at Bn=32, the
-    single-split vector accumulate epilogue at Bn=1.  bf16 inputs, fp32 reference on the same
+    single-split vector accumulate epilogue at Bn=1; T=200 (encoder) takes the split-slice
+    data gradient.  bf16 inputs, fp32 reference on the same
     bf16 values, rel 2e-2."""
     from fastspeech2 import ops
     torch.manual_seed(Bn)
@@ -349,10 +354,13 @@ def test_gemm_big_tile_paths_bf16(cuda, Bn, T):
              relu=1)
     assert rel(Y, out.detach().reshape(-1, O)) < 2e-2
     Mp = Bn * (T + 2 * P)
-    Xpad = torch.empty(Mp, Cin, device=cuda)
-    ops.gemm(Mp, Cin, KW * O, G, O, Wb, KW * O, Xpad, Cin, dt=1, conv=(4, T, KW, O), c_fp32=1)
+    from fastspeech2.engine import dgrad_split
+    split = dgrad_split(Mp, Cin, KW * O, 1)
+    Xpad = torch.empty(split, Mp, Cin, device=cuda)
+    ops.gemm(Mp, Cin, KW * O, G, O, Wb, KW * O, Xpad, Cin, dt=1, conv=(4, T, KW, O), c_fp32=1,
+             split_k=split, split_stride=Mp * Cin if split > 1 else 0)
     dX = torch.empty(M, Cin, device=cuda, dtype=torch.bfloat16)
-    ops.conv_fold(Xpad, Bn, T, P, Cin, dX, Cin, dt=1)
+    ops.conv_fold(Xpad, Bn, T, P, Cin, dX, Cin, dt=1, nsplit=split, split_stride=Mp * Cin)
     assert rel(dX, Xr.grad.reshape(-1, Cin)) < 2e-2
     dW = torch.full((O, KW, Cin), 0.5, device=cuda)        # accumulates onto existing values
     ops.gemm(O, KW * Cin, ops.round_up(M, 8), G, O, X, Cin, dW, KW * Cin, dt=1, a_kmajor=0,
