@@ -23,6 +23,39 @@ __device__ __forceinline__ float bf16_bits_to_f(unsigned short u) {
   return __builtin_bit_cast(float, ((unsigned int)u) << 16);
 }
 
+// ---- 16-byte vector access: VEC<T> elements per lane (8 bf16 / 4 fp32), fp32 in registers ----
+template <typename T> struct Vec { static constexpr int N = 16 / (int)sizeof(T); };
+template <typename T>
+__device__ __forceinline__ void vload(float* o, const T* src) {
+  if constexpr (sizeof(T) == 2) {
+    const u32x4 u = *(const u32x4*)src;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      o[2 * w] = __builtin_bit_cast(float, u[w] << 16);
+      o[2 * w + 1] = __builtin_bit_cast(float, u[w] & 0xffff0000u);
+    }
+  } else {
+    const f32x4 a = *(const f32x4*)src;
+    o[0] = a[0]; o[1] = a[1]; o[2] = a[2]; o[3] = a[3];
+  }
+}
+template <typename T>
+__device__ __forceinline__ void vstore(T* dst, const float* v) {
+  if constexpr (sizeof(T) == 2) {
+    u32x4 u;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const bf16 a = (bf16)v[2 * w], b = (bf16)v[2 * w + 1];
+      u[w] = (unsigned)__builtin_bit_cast(unsigned short, a) |
+             ((unsigned)__builtin_bit_cast(unsigned short, b) << 16);
+    }
+    *(u32x4*)dst = u;
+  } else {
+    *(f32x4*)dst = f32x4{v[0], v[1], v[2], v[3]};
+  }
+}
+__device__ __forceinline__ bool aligned16_dev(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
 // ---- wave reductions (64 lanes) ----
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

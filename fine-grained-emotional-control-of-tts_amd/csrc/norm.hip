@@ -83,15 +83,16 @@ struct LnBwdP {
   const float* gamma; const float* beta; int do_tanh; float p_o; uint32_t salt_o;
   const float* row_mask; int relu_gate_in; char* ds; long ldds; char* dr; float p_r;
   uint32_t salt_r; float* part_g; float* part_b; int M, D; uint32_t seed; int rows_per_block;
+  float* part_c; long pstride;  // partial rows are pstride floats apart (scalar kernel)
 };
 
 template <typename T>
 __global__ void __launch_bounds__(256) ln_bwd_kernel(LnBwdP p) {
   __shared__ float red[2][4][1024];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  float pg[MAXJ], pb[MAXJ];
+  float pg[MAXJ], pb[MAXJ], pc[MAXJ];
 #pragma unroll
-  for (int j = 0; j < MAXJ; ++j) { pg[j] = 0.f; pb[j] = 0.f; }
+  for (int j = 0; j < MAXJ; ++j) { pg[j] = 0.f; pb[j] = 0.f; pc[j] = 0.f; }
   const float inv_o = p.p_o > 0.f ? 1.f / (1.f - p.p_o) : 1.f;
   const float inv_r = p.p_r > 0.f ? 1.f / (1.f - p.p_r) : 1.f;
   const int rbeg = blockIdx.x * p.rows_per_block;
@@ -140,6 +141,9 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(LnBwdP p) {
           if (p.p_r > 0.f)
             w = fs2_keep(p.seed, p.salt_r, (uint64_t)row * p.D + d, p.p_r) ? w * inv_r : 0.f;
           dr[d] = from_f<T>(w);
+          pc[j] += w;
+        } else {
+          pc[j] += v;
         }
       }
     }
@@ -152,28 +156,20 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(LnBwdP p) {
     }
     __syncthreads();
     for (int d = threadIdx.x; d < p.D; d += 256) {
-      p.part_g[(long)blockIdx.x * p.D + d] = red[0][0][d] + red[0][1][d] + red[0][2][d] + red[0][3][d];
-      p.part_b[(long)blockIdx.x * p.D + d] = red[1][0][d] + red[1][1][d] + red[1][2][d] + red[1][3][d];
+      p.part_g[(long)blockIdx.x * p.pstride + d] = (red[0][0][d] + red[0][1][d]) + (red[0][2][d] + red[0][3][d]);
+      p.part_b[(long)blockIdx.x * p.pstride + d] = (red[1][0][d] + red[1][1][d]) + (red[1][2][d] + red[1][3][d]);
     }
   }
-}
-
-// out[n] (+)= sum_b part[b][n]: 64 columns x 4 row-slices per block, fixed-order LDS combine
-__global__ void __launch_bounds__(256) reduce_partials_kernel(const float* part, int nb, int N,
-                                                             float* out, int accumulate) {
-  __shared__ float red[4][64];
-  const int c = threadIdx.x & 63, sl = threadIdx.x >> 6;
-  const int n = blockIdx.x * 64 + c;
-  float s = 0.f;
-  if (n < N) {
-#pragma unroll 8
-    for (int b = sl; b < nb; b += 4) s += part[(long)b * N + n];
-  }
-  red[sl][c] = s;
-  __syncthreads();
-  if (sl == 0 && n < N) {
-    const float t = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
-    out[n] = accumulate ? out[n] + t : t;
+  if (p.part_c) {
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < MAXJ; ++j) {
+      const int d = lane + 64 * j;
+      if (d < p.D) red[0][wave][d] = pc[j];
+    }
+    __syncthreads();
+    for (int d = threadIdx.x; d < p.D; d += 256)
+      p.part_c[(long)blockIdx.x * p.pstride + d] = (red[0][0][d] + red[0][1][d]) + (red[0][2][d] + red[0][3][d]);
   }
 }
 
@@ -189,6 +185,262 @@ __global__ void colsum_partial_kernel(const T* X, long ldx, int M, int N, int ro
   part[(long)blockIdx.y * N + n] = s;
 }
 
+
+// ---- 16-byte vectorised variants (D % VEC == 0, 16-B aligned rows): lane owns NCH chunks of
+// VEC consecutive features, so a D=384 bf16 row is one 768-B wave access instead of six
+// 128-B ones.  Same arithmetic, dropout indices and rounding points as the scalar kernels.
+template <typename T, int NCH>
+__global__ void __launch_bounds__(256) ln_fwd_vec_kernel(LnFwdP p) {
+  constexpr int V = Vec<T>::N;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= p.M) return;
+  const T* x = (const T*)p.x + (long)row * p.ldx;
+  const T* r = p.r ? (const T*)p.r + (long)row * p.ldr : nullptr;
+  const float inv_r = p.p_r > 0.f ? 1.f / (1.f - p.p_r) : 1.f;
+  float v[NCH][V];
+  float sum = 0.f;
+#pragma unroll
+  for (int ch = 0; ch < NCH; ++ch) {
+    const int d0 = (lane + 64 * ch) * V;
+    if (d0 < p.D) {
+      vload<T>(v[ch], x + d0);
+      if (r) {
+        float rv[V];
+        vload<T>(rv, r + d0);
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+          float q = rv[e];
+          if (p.p_r > 0.f)
+            q = fs2_keep(p.seed, p.salt_r, (uint64_t)row * p.D + d0 + e, p.p_r) ? q * inv_r : 0.f;
+          v[ch][e] += q;
+        }
+      }
+      if (p.s_out) {
+        vstore<T>((T*)p.s_out + (long)row * p.D + d0, v[ch]);
+        if (r) {  // statistics of the stored (rounded) s, as the backward re-reads it
+#pragma unroll
+          for (int e = 0; e < V; ++e) v[ch][e] = to_f(from_f<T>(v[ch][e]));
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < V; ++e) sum += v[ch][e];
+    }
+  }
+  const float mean = wave_sum(sum) / (float)p.D;
+  float sq = 0.f;
+#pragma unroll
+  for (int ch = 0; ch < NCH; ++ch) {
+    const int d0 = (lane + 64 * ch) * V;
+    if (d0 < p.D) {
+#pragma unroll
+      for (int e = 0; e < V; ++e) { const float c = v[ch][e] - mean; sq += c * c; }
+    }
+  }
+  const float var = wave_sum(sq) / (float)p.D;
+  const float rstd = 1.f / sqrtf(var + p.eps);
+  if (lane == 0) { p.mean[row] = mean; p.rstd[row] = rstd; }
+  const float inv_o = p.p_o > 0.f ? 1.f / (1.f - p.p_o) : 1.f;
+  const float rm = p.row_mask ? p.row_mask[row] : 1.f;
+  T* y = (T*)p.y + (long)row * p.ldy;
+  const T* pa = p.post_add ? (const T*)p.post_add + (long)row * p.ldp : nullptr;
+#pragma unroll
+  for (int ch = 0; ch < NCH; ++ch) {
+    const int d0 = (lane + 64 * ch) * V;
+    if (d0 < p.D) {
+      float g[V], b[V], o[V], a[V];
+      vload<float>(g, p.gamma + d0);
+      vload<float>(b, p.beta + d0);
+      if constexpr (V == 8) { vload<float>(g + 4, p.gamma + d0 + 4); vload<float>(b + 4, p.beta + d0 + 4); }
+      if (pa) vload<T>(a, pa + d0);
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        float q = (v[ch][e] - mean) * rstd * g[e] + b[e];
+        if (p.do_tanh) q = tanhf(q);
+        if (p.p_o > 0.f)
+          q = fs2_keep(p.seed, p.salt_o, (uint64_t)row * p.D + d0 + e, p.p_o) ? q * inv_o : 0.f;
+        q *= rm;
+        if (pa) q += a[e];
+        o[e] = q;
+      }
+      vstore<T>(y + d0, o);
+    }
+  }
+}
+
+// part layout: [gridDim.x][npart * D] (gamma, beta, then optionally the column sum of the
+// emitted gradient -- the bias gradient of the layer that produced the residual branch)
+template <typename T, int NCH>
+__global__ void __launch_bounds__(256) ln_bwd_vec_kernel(LnBwdP p, float* part, int npart,
+                                                         int kind0) {
+  constexpr int V = Vec<T>::N;
+  __shared__ float red[4][1024];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float pg[NCH][V], pb[NCH][V], pc[NCH][V];
+#pragma unroll
+  for (int ch = 0; ch < NCH; ++ch)
+#pragma unroll
+    for (int e = 0; e < V; ++e) { pg[ch][e] = 0.f; pb[ch][e] = 0.f; pc[ch][e] = 0.f; }
+  const float inv_o = p.p_o > 0.f ? 1.f / (1.f - p.p_o) : 1.f;
+  const float inv_r = p.p_r > 0.f ? 1.f / (1.f - p.p_r) : 1.f;
+  const int rbeg = blockIdx.x * p.rows_per_block;
+  const int rend = min(p.M, rbeg + p.rows_per_block);
+  for (int row = rbeg + wave; row < rend; row += 4) {
+    const T* dy = (const T*)p.dy + (long)row * p.lddy;
+    const T* s = (const T*)p.s + (long)row * p.lds;
+    const float mean = p.mean[row], rstd = p.rstd[row];
+    const float rm = p.row_mask ? p.row_mask[row] : 1.f;
+    float g[NCH][V], xh[NCH][V], sv[NCH][V];
+    float a1 = 0.f, a2 = 0.f;
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) {
+      const int d0 = (lane + 64 * ch) * V;
+      if (d0 < p.D) {
+        float dv[V], gm[V], bt[V];
+        vload<T>(sv[ch], s + d0);
+        vload<T>(dv, dy + d0);
+        vload<float>(gm, p.gamma + d0);
+        if constexpr (V == 8) vload<float>(gm + 4, p.gamma + d0 + 4);
+        if (p.do_tanh) {
+          vload<float>(bt, p.beta + d0);
+          if constexpr (V == 8) vload<float>(bt + 4, p.beta + d0 + 4);
+        }
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+          xh[ch][e] = (sv[ch][e] - mean) * rstd;
+          float gg = dv[e] * rm;
+          if (p.p_o > 0.f)
+            gg = fs2_keep(p.seed, p.salt_o, (uint64_t)row * p.D + d0 + e, p.p_o) ? gg * inv_o : 0.f;
+          if (p.do_tanh) {
+            const float t = tanhf(xh[ch][e] * gm[e] + bt[e]);
+            gg *= (1.f - t * t);
+          }
+          pg[ch][e] += gg * xh[ch][e];
+          pb[ch][e] += gg;
+          g[ch][e] = gg * gm[e];
+          a1 += g[ch][e];
+          a2 += g[ch][e] * xh[ch][e];
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < V; ++e) { g[ch][e] = 0.f; xh[ch][e] = 0.f; sv[ch][e] = 0.f; }
+      }
+    }
+    a1 = wave_sum(a1) / (float)p.D;
+    a2 = wave_sum(a2) / (float)p.D;
+    T* ds = (T*)p.ds + (long)row * p.ldds;
+    T* dr = p.dr ? (T*)p.dr + (long)row * p.D : nullptr;
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) {
+      const int d0 = (lane + 64 * ch) * V;
+      if (d0 < p.D) {
+        float o[V], w[V];
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+          float q = rstd * (g[ch][e] - a1 - xh[ch][e] * a2);
+          if (p.relu_gate_in && !(sv[ch][e] > 0.f)) q = 0.f;
+          o[e] = q;
+          if (dr) {
+            float t = q;
+            if (p.p_r > 0.f)
+              t = fs2_keep(p.seed, p.salt_r, (uint64_t)row * p.D + d0 + e, p.p_r) ? t * inv_r : 0.f;
+            w[e] = t;
+          }
+        }
+        vstore<T>(ds + d0, o);
+        if (dr) vstore<T>(dr + d0, w);
+#pragma unroll
+        for (int e = 0; e < V; ++e) pc[ch][e] += dr ? w[e] : o[e];
+      }
+    }
+  }
+  if (!part) return;
+  // fixed-order combine of the 4 waves' partials, one pass per partial kind
+  for (int k = 0; k < npart; ++k) {
+    const int kind = kind0 + k;  // 0 gamma, 1 beta, 2 column sum
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) {
+      const int d0 = (lane + 64 * ch) * V;
+      if (d0 < p.D) {
+#pragma unroll
+        for (int e = 0; e < V; ++e)
+          red[wave][d0 + e] = kind == 0 ? pg[ch][e] : (kind == 1 ? pb[ch][e] : pc[ch][e]);
+      }
+    }
+    __syncthreads();
+    for (int d = threadIdx.x; d < p.D; d += 256)
+      part[((long)blockIdx.x * npart + k) * p.D + d] =
+          (red[0][d] + red[1][d]) + (red[2][d] + red[3][d]);
+    __syncthreads();
+  }
+}
+
+// out_k[d] (+)= sum_b part[b][k*D + d] for k < npart: 16 columns x 16 row-slices per block,
+// fixed-order LDS combine (deterministic)
+__global__ void __launch_bounds__(256) reduce_parts_kernel(const float* part, int nb, int D,
+                                                          int npart, float* o0, float* o1,
+                                                          float* o2, int accumulate) {
+  __shared__ float red[16][17];
+  const int c = threadIdx.x & 15, sl = threadIdx.x >> 4;
+  const int ncols = npart * D;
+  const int n = blockIdx.x * 16 + c;
+  float s = 0.f;
+  if (n < ncols) {
+#pragma unroll 4
+    for (int b = sl; b < nb; b += 16) s += part[(long)b * ncols + n];
+  }
+  red[sl][c] = s;
+  __syncthreads();
+  if (sl == 0 && n < ncols) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t += red[i][c];
+    const int k = n / D, d = n - k * D;
+    float* o = k == 0 ? o0 : (k == 1 ? o1 : o2);
+    o[d] = accumulate ? o[d] + t : t;
+  }
+}
+
+// column sums, 16-B loads: thread = (row sub-lane, column chunk of VEC)
+template <typename T>
+__global__ void __launch_bounds__(256) colsum_vec_kernel(const T* X, long ldx, int M, int N,
+                                                        int rows_per_block, float* part) {
+  constexpr int V = Vec<T>::N;
+  __shared__ float red[256 * V];
+  const int ncc = N / V, nsub = 256 / ncc;
+  const int t = threadIdx.x, rsub = t / ncc, cc = t - rsub * ncc;
+  const int rbeg = blockIdx.x * rows_per_block;
+  const int rend = min(M, rbeg + rows_per_block);
+  float acc[V];
+#pragma unroll
+  for (int e = 0; e < V; ++e) acc[e] = 0.f;
+  if (rsub < nsub) {
+    int m = rbeg + rsub;
+    for (; m + 3 * nsub < rend; m += 4 * nsub) {
+      float a[4][V];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) vload<T>(a[u], X + (long)(m + u * nsub) * ldx + cc * V);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int e = 0; e < V; ++e) acc[e] += a[u][e];
+    }
+    for (; m < rend; m += nsub) {
+      float a[V];
+      vload<T>(a, X + (long)m * ldx + cc * V);
+#pragma unroll
+      for (int e = 0; e < V; ++e) acc[e] += a[e];
+    }
+#pragma unroll
+    for (int e = 0; e < V; ++e) red[rsub * N + cc * V + e] = acc[e];
+  }
+  __syncthreads();
+  for (int n = t; n < N; n += 256) {
+    float s = 0.f;
+    for (int i = 0; i < nsub; ++i) s += red[i * N + n];
+    part[(long)blockIdx.x * N + n] = s;
+  }
+}
 
 // Adjoint of SB Conv1d's reflect "same" padding for the data gradient (K16):
 //   dX[b,s] = Xp[b,s+P] + [1<=s<=P] Xp[b,P-s] + [T-1-P<=s<=T-2] Xp[b,2(T-1)-s+P]
@@ -221,12 +473,13 @@ __global__ void conv_fold_kernel(const float* Xp, int nsplit, long sstride, int 
   }
 }
 
-int ln_blocks(int M) { return min(512, max(1, (M + 15) / 16)); }
-int colsum_blocks(int M) { return min(256, max(1, (M + 63) / 64)); }
+int ln_blocks(int M) { return min(4096, max(1, (M + 31) / 32)); }
+int colsum_blocks(int M) { return min(512, max(1, (M + 63) / 64)); }
+bool a16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 }  // namespace
 
-extern "C" int64_t fs2_ln_workspace_floats(int M, int D) { return 2L * ln_blocks(M) * D; }
+extern "C" int64_t fs2_ln_workspace_floats(int M, int D) { return 3L * ln_blocks(M) * D; }
 extern "C" int64_t fs2_colsum_workspace_floats(int M, int N) { return (int64_t)colsum_blocks(M) * N; }
 
 extern "C" int fs2_ln_fwd(const void* x, int64_t ldx, const void* r, int64_t ldr, float p_r,
@@ -242,9 +495,24 @@ extern "C" int fs2_ln_fwd(const void* x, int64_t ldx, const void* r, int64_t ldr
            rstd, M, D, seed};
   dim3 grid((M + 3) / 4);
   hipStream_t s = (hipStream_t)stream;
-  if (dtype == FS2_BF16) hipLaunchKernelGGL(ln_fwd_kernel<bf16>, grid, dim3(256), 0, s, p);
-  else if (dtype == FS2_F32) hipLaunchKernelGGL(ln_fwd_kernel<float>, grid, dim3(256), 0, s, p);
-  else return FS2_EINVAL;
+  const int V = dtype == FS2_BF16 ? 8 : 4;
+  const int nch = (D / V + 63) / 64;
+  const bool vec = (D % V) == 0 && nch <= 4 && a16(x) && (ldx % V) == 0 && a16(y) &&
+                   (ldy % V) == 0 && a16(gamma) && a16(beta) && (!r || (a16(r) && ldr % V == 0)) &&
+                   (!s_out || a16(s_out)) && (!post_add || (a16(post_add) && ldp % V == 0));
+  if (dtype == FS2_BF16) {
+    if (!vec) hipLaunchKernelGGL(ln_fwd_kernel<bf16>, grid, dim3(256), 0, s, p);
+    else if (nch == 1) hipLaunchKernelGGL((ln_fwd_vec_kernel<bf16, 1>), grid, dim3(256), 0, s, p);
+    else if (nch == 2) hipLaunchKernelGGL((ln_fwd_vec_kernel<bf16, 2>), grid, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((ln_fwd_vec_kernel<bf16, 4>), grid, dim3(256), 0, s, p);
+  } else if (dtype == FS2_F32) {
+    if (!vec) hipLaunchKernelGGL(ln_fwd_kernel<float>, grid, dim3(256), 0, s, p);
+    else if (nch == 1) hipLaunchKernelGGL((ln_fwd_vec_kernel<float, 1>), grid, dim3(256), 0, s, p);
+    else if (nch == 2) hipLaunchKernelGGL((ln_fwd_vec_kernel<float, 2>), grid, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((ln_fwd_vec_kernel<float, 4>), grid, dim3(256), 0, s, p);
+  } else {
+    return FS2_EINVAL;
+  }
   FS2_CHECK_LAUNCH();
   return 0;
 }
@@ -254,28 +522,50 @@ extern "C" int fs2_ln_bwd(const void* dy, int64_t lddy, const void* s, int64_t l
                           const float* beta, int do_tanh, float p_o, uint32_t salt_o,
                           const float* row_mask, int relu_gate_in, void* ds, int64_t ldds,
                           void* dr, float p_r, uint32_t salt_r, float* dgamma, float* dbeta,
-                          int M, int D, int dtype, uint32_t seed, float* workspace,
+                          float* dcol, int M, int D, int dtype, uint32_t seed, float* workspace,
                           void* stream) {
   if (M <= 0) return 0;
   if (D <= 0 || D > 64 * MAXJ || !dy || !s || !ds || !gamma || !beta) return FS2_EINVAL;
-  if ((dgamma || dbeta) && (!dgamma || !dbeta || !workspace)) return FS2_EINVAL;
+  if ((dgamma || dbeta) && (!dgamma || !dbeta)) return FS2_EINVAL;
+  if ((dgamma || dcol) && !workspace) return FS2_EINVAL;
   const int nb = ln_blocks(M);
   const int rpb = (M + nb - 1) / nb;
+  // partial rows [nb][npart*D]: (gamma, beta)?, col?
+  const int npart = (dgamma ? 2 : 0) + (dcol ? 1 : 0);
   float* pg = dgamma ? workspace : nullptr;
-  float* pb = dgamma ? workspace + (long)nb * D : nullptr;
+  float* pb = dgamma ? workspace + D : nullptr;
+  float* pcl = dcol ? workspace + (dgamma ? 2 * D : 0) : nullptr;
   LnBwdP p{(const char*)dy, lddy, (const char*)s, lds, mean, rstd, gamma, beta, do_tanh, p_o,
            salt_o, row_mask, relu_gate_in, (char*)ds, ldds, (char*)dr, p_r, salt_r, pg, pb, M,
-           D, seed, rpb};
+           D, seed, rpb, pcl, (long)npart * D};
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == FS2_BF16) hipLaunchKernelGGL(ln_bwd_kernel<bf16>, dim3(nb), dim3(256), 0, st, p);
-  else if (dtype == FS2_F32) hipLaunchKernelGGL(ln_bwd_kernel<float>, dim3(nb), dim3(256), 0, st, p);
-  else return FS2_EINVAL;
+  const int V = dtype == FS2_BF16 ? 8 : 4;
+  const int nch = (D / V + 63) / 64;
+  const bool vec = (D % V) == 0 && nch <= 4 && a16(dy) && (lddy % V) == 0 && a16(s) &&
+                   (lds % V) == 0 && a16(ds) && (ldds % V) == 0 && (!dr || a16(dr)) &&
+                   a16(gamma) && a16(beta);
+  float* part = npart ? workspace : nullptr;
+  const int kind0 = dgamma ? 0 : 2;
+  if (dtype == FS2_BF16) {
+    if (!vec) hipLaunchKernelGGL(ln_bwd_kernel<bf16>, dim3(nb), dim3(256), 0, st, p);
+    else if (nch == 1) hipLaunchKernelGGL((ln_bwd_vec_kernel<bf16, 1>), dim3(nb), dim3(256), 0, st, p, part, npart, kind0);
+    else if (nch == 2) hipLaunchKernelGGL((ln_bwd_vec_kernel<bf16, 2>), dim3(nb), dim3(256), 0, st, p, part, npart, kind0);
+    else hipLaunchKernelGGL((ln_bwd_vec_kernel<bf16, 4>), dim3(nb), dim3(256), 0, st, p, part, npart, kind0);
+  } else if (dtype == FS2_F32) {
+    if (!vec) hipLaunchKernelGGL(ln_bwd_kernel<float>, dim3(nb), dim3(256), 0, st, p);
+    else if (nch == 1) hipLaunchKernelGGL((ln_bwd_vec_kernel<float, 1>), dim3(nb), dim3(256), 0, st, p, part, npart, kind0);
+    else if (nch == 2) hipLaunchKernelGGL((ln_bwd_vec_kernel<float, 2>), dim3(nb), dim3(256), 0, st, p, part, npart, kind0);
+    else hipLaunchKernelGGL((ln_bwd_vec_kernel<float, 4>), dim3(nb), dim3(256), 0, st, p, part, npart, kind0);
+  } else {
+    return FS2_EINVAL;
+  }
   FS2_CHECK_LAUNCH();
-  if (dgamma) {
-    hipLaunchKernelGGL(reduce_partials_kernel, dim3((D + 63) / 64), dim3(256), 0, st, pg, nb, D,
-                       dgamma, 1);
-    hipLaunchKernelGGL(reduce_partials_kernel, dim3((D + 63) / 64), dim3(256), 0, st, pb, nb, D,
-                       dbeta, 1);
+  if (npart) {
+    float* o0 = dgamma ? dgamma : dcol;
+    float* o1 = dgamma ? dbeta : nullptr;
+    float* o2 = dgamma ? dcol : nullptr;
+    hipLaunchKernelGGL(reduce_parts_kernel, dim3((npart * D + 15) / 16), dim3(256), 0, st,
+                       workspace, nb, D, npart, o0, o1, o2, 1);
     FS2_CHECK_LAUNCH();
   }
   return 0;
@@ -288,14 +578,23 @@ extern "C" int fs2_colsum(const void* X, int64_t ldx, int M, int N, int dtype, f
   hipStream_t st = (hipStream_t)stream;
   const int nb = colsum_blocks(M);
   const int rpb = (M + nb - 1) / nb;
-  dim3 grid((N + 255) / 256, nb);
-  if (dtype == FS2_BF16)
-    hipLaunchKernelGGL(colsum_partial_kernel<bf16>, grid, dim3(256), 0, st, (const bf16*)X, ldx, M, N, rpb, workspace);
-  else if (dtype == FS2_F32)
-    hipLaunchKernelGGL(colsum_partial_kernel<float>, grid, dim3(256), 0, st, (const float*)X, ldx, M, N, rpb, workspace);
-  else return FS2_EINVAL;
-  hipLaunchKernelGGL(reduce_partials_kernel, dim3((N + 63) / 64), dim3(256), 0, st, workspace, nb,
-                     N, out, accumulate);
+  const int V = dtype == FS2_BF16 ? 8 : 4;
+  const bool vec = (N % V) == 0 && N / V <= 256 && a16(X) && (ldx % V) == 0;
+  if (dtype == FS2_BF16) {
+    if (vec)
+      hipLaunchKernelGGL(colsum_vec_kernel<bf16>, dim3(nb), dim3(256), 0, st, (const bf16*)X, (long)ldx, M, N, rpb, workspace);
+    else
+      hipLaunchKernelGGL(colsum_partial_kernel<bf16>, dim3((N + 255) / 256, nb), dim3(256), 0, st, (const bf16*)X, ldx, M, N, rpb, workspace);
+  } else if (dtype == FS2_F32) {
+    if (vec)
+      hipLaunchKernelGGL(colsum_vec_kernel<float>, dim3(nb), dim3(256), 0, st, (const float*)X, (long)ldx, M, N, rpb, workspace);
+    else
+      hipLaunchKernelGGL(colsum_partial_kernel<float>, dim3((N + 255) / 256, nb), dim3(256), 0, st, (const float*)X, ldx, M, N, rpb, workspace);
+  } else {
+    return FS2_EINVAL;
+  }
+  hipLaunchKernelGGL(reduce_parts_kernel, dim3((N + 15) / 16), dim3(256), 0, st, workspace, nb, N,
+                     1, out, nullptr, nullptr, accumulate);
   FS2_CHECK_LAUNCH();
   return 0;
 }

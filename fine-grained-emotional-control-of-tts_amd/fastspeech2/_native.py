@@ -79,8 +79,8 @@ SIGNATURES = {
     "fs2_colsum_workspace_floats": (I64, [I, I]),
     "fs2_ln_fwd": (I, [P, I64, P, I64, Fl, U32, P, P, P, Fl, I, Fl, U32, P, P, I64, P, I64, P, P,
                        I, I, I, U32, P]),
-    "fs2_ln_bwd": (I, [P, I64, P, I64, P, P, P, P, I, Fl, U32, P, I, P, I64, P, Fl, U32, P, P, I,
-                       I, I, U32, P, P]),
+    "fs2_ln_bwd": (I, [P, I64, P, I64, P, P, P, P, I, Fl, U32, P, I, P, I64, P, Fl, U32, P, P, P,
+                       I, I, I, U32, P, P]),
     "fs2_ln_workspace_floats": (I64, [I, I]),
     "fs2_softmax_fwd": (I, [P, P, I, I, I, I, I, Fl, Fl, U32, U32, P, P, I, P]),
     "fs2_softmax_bwd": (I, [P, P, I, I, I, I, I, Fl, Fl, U32, U32, P, I, P]),

@@ -240,12 +240,11 @@ class FS2Engine:
         ops.ln_bwd(dX2, D, ctx["s2"], D, ctx["mean2"], ctx["rstd2"], P[prefix + "norm2.norm.weight"],
                    P[prefix + "norm2.norm.bias"], ds2, D, M, D, dt=self.dt, ws=lnws, seed=seed,
                    dr=dY, p_r=p_drop, salt_r=ctx["s_r2"], dgamma=G[prefix + "norm2.norm.weight"],
-                   dbeta=G[prefix + "norm2.norm.bias"])
+                   dbeta=G[prefix + "norm2.norm.bias"], dcol=G[prefix + "pos_ffn.2.conv.bias"])
         w2 = prefix + "pos_ffn.2.conv.weight"
         dHc = self.empty(M, F)
         self._dgrad(dY, D, M, T, w2, dHc, F, gate=ctx["Hc"], ldg=F)
         self._wgrad(dY, D, ctx["Hc"], F, M, T, w2)
-        self._bias_grad(dY, D, M, D, prefix + "pos_ffn.2.conv.bias")
         del dY
         w1 = prefix + "pos_ffn.0.conv.weight"
         dX1 = self.empty(M, D)
@@ -258,13 +257,13 @@ class FS2Engine:
         ops.ln_bwd(dX1, D, ctx["s1"], D, ctx["mean1"], ctx["rstd1"], P[prefix + "norm1.norm.weight"],
                    P[prefix + "norm1.norm.bias"], ds1, D, M, D, dt=self.dt, ws=lnws, seed=seed,
                    dr=dAo, p_r=p_drop, salt_r=ctx["s_r1"], dgamma=G[prefix + "norm1.norm.weight"],
-                   dbeta=G[prefix + "norm1.norm.bias"])
+                   dbeta=G[prefix + "norm1.norm.bias"],
+                   dcol=G[prefix + "self_att.att.out_proj.bias"])
         del dX1
         wo = prefix + "self_att.att.out_proj.weight"
         dAtt = self.empty(M, D)
         self._dgrad(dAo, D, M, T, wo, dAtt, D)
         self._wgrad(dAo, D, ctx["Att"], D, M, T, wo)
-        self._bias_grad(dAo, D, M, D, prefix + "self_att.att.out_proj.bias")
         del dAo
         # ---- attention backward over the materialised probabilities
         QKV, Pm, Pd = ctx["QKV"], ctx["Pm"], ctx["Pd"]
@@ -342,24 +341,24 @@ class FS2Engine:
         ops.ln_bwd(dv2, D, c["a2"], D, c["m2"], c["r2"], P[name + ".ln2.norm.weight"],
                    P[name + ".ln2.norm.bias"], da2, D, M, D, dt=self.dt, ws=self.ws(ops.ln_ws(M, D)),
                    seed=seed, p_o=p_drop, salt_o=c["s2"], row_mask=keep, relu_gate_in=1,
-                   dgamma=G[name + ".ln2.norm.weight"], dbeta=G[name + ".ln2.norm.bias"])
+                   dgamma=G[name + ".ln2.norm.weight"], dbeta=G[name + ".ln2.norm.bias"],
+                   dcol=G[name + ".conv2.conv.bias"])
         w2 = name + ".conv2.conv.weight"
         dv1 = self.empty(M, D)
         self._dgrad(da2, D, M, T, w2, dv1, D)
         self._wgrad(da2, D, c["v1"], D, M, T, w2)
-        self._bias_grad(da2, D, M, D, name + ".conv2.conv.bias")
         da1 = self.empty(M, D)
         ops.ln_bwd(dv1, D, c["a1"], D, c["m1"], c["r1"], P[name + ".ln1.norm.weight"],
                    P[name + ".ln1.norm.bias"], da1, D, M, D, dt=self.dt, ws=self.ws(ops.ln_ws(M, D)),
                    seed=seed, p_o=p_drop, salt_o=c["s1"], row_mask=keep, relu_gate_in=1,
-                   dgamma=G[name + ".ln1.norm.weight"], dbeta=G[name + ".ln1.norm.bias"])
+                   dgamma=G[name + ".ln1.norm.weight"], dbeta=G[name + ".ln1.norm.bias"],
+                   dcol=G[name + ".conv1.conv.bias"])
         w1 = name + ".conv1.conv.weight"
         dZ = self.empty(M, D)
         self._dgrad(da1, D, M, T, w1, dZ, D, row_scale=keep, residual=residual,
                     ldr=D if residual is not None else 0,
                     row_scale_post=keep if post_mask else None)
         self._wgrad(da1, D, c["Zin"], D, M, T, w1)
-        self._bias_grad(da1, D, M, D, name + ".conv1.conv.bias")
         return dZ
 
     # ------------------------------------------------------------------ PostNet
@@ -417,17 +416,21 @@ class FS2Engine:
         dp4 = self.empty(M, NM)
         ops.ln_bwd(d_post, NM, p4, NM, mn3, rs3, P["postnet.ln3.weight"], P["postnet.ln3.bias"], dp4,
                    NM, M, NM, dt=self.dt, ws=self.ws(ops.ln_ws(M, NM)), seed=seed, p_o=p_drop,
-                   salt_o=s3, dgamma=G["postnet.ln3.weight"], dbeta=G["postnet.ln3.bias"])
+                   salt_o=s3, dgamma=G["postnet.ln3.weight"], dbeta=G["postnet.ln3.bias"],
+                   dcol=G["postnet.conv_post.conv.bias"])
         wname = "postnet.conv_post.conv.weight"
         dq3 = self.empty(M, E)
         self._dgrad(dp4, NM, M, T, wname, dq3, E)
         self._wgrad(dp4, NM, ctx["q3"], E, M, T, wname)
-        self._bias_grad(dp4, NM, M, NM, "postnet.conv_post.conv.bias")
         x, mn, rs, s = ctx["ln2"]
         dx = self.empty(M, E)
         ops.ln_bwd(dq3, E, x, E, mn, rs, P["postnet.ln2.weight"], P["postnet.ln2.bias"], dx, E, M, E,
                    dt=self.dt, ws=self.ws(ops.ln_ws(M, E)), seed=seed, do_tanh=1, p_o=p_drop,
-                   salt_o=s, dgamma=G["postnet.ln2.weight"], dbeta=G["postnet.ln2.bias"])
+                   salt_o=s, dgamma=G["postnet.ln2.weight"], dbeta=G["postnet.ln2.bias"],
+                   dcol=G[ctx["convs"][-1][0] + ".conv.bias"] if len(ctx["convs"]) > 1 else None)
+        # ln2's input is the last intermediate conv's output (if any): its bias gradient came
+        # with ln2's backward
+        bias_done = len(ctx["convs"]) - 1 if len(ctx["convs"]) > 1 else -1
         for i, (name, xin, ldx, p) in reversed(list(enumerate(ctx["convs"]))):
             if i == 0:
                 p0, mn1, rs1, s1 = ctx["ln1"]
@@ -435,18 +438,19 @@ class FS2Engine:
                 ops.ln_bwd(dx, E, p0, E, mn1, rs1, P["postnet.ln1.weight"], P["postnet.ln1.bias"], dp0,
                            E, M, E, dt=self.dt, ws=self.ws(ops.ln_ws(M, E)), seed=seed, do_tanh=1,
                            p_o=p_drop, salt_o=s1, dgamma=G["postnet.ln1.weight"],
-                           dbeta=G["postnet.ln1.bias"])
+                           dbeta=G["postnet.ln1.bias"],
+                           dcol=G[name + ".conv.bias"] if i != bias_done else None)
                 dx = dp0
                 dmel = self.empty(M, NM)
                 self._dgrad(dx, E, M, T, name + ".conv.weight", dmel, NM, residual=d_mel_total,
                             ldr=NM, row_scale_post=keep)
                 self._wgrad(dx, E, xin, ldx, M, T, name + ".conv.weight")
-                self._bias_grad(dx, E, M, E, name + ".conv.bias")
                 return dmel
             dprev = self.empty(M, E)
             self._dgrad(dx, E, M, T, name + ".conv.weight", dprev, E)
             self._wgrad(dx, E, xin, ldx, M, T, name + ".conv.weight")
-            self._bias_grad(dx, E, M, E, name + ".conv.bias")
+            if i != bias_done:
+                self._bias_grad(dx, E, M, E, name + ".conv.bias")
             dx = dprev
 
     # ------------------------------------------------------------------ full forward

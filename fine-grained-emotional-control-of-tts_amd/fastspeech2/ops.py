@@ -83,10 +83,11 @@ def ln_fwd(x, ldx, gamma, beta, eps, y, ldy, mean, rstd, M, D, *, dt, seed=0, r=
 
 def ln_bwd(dy, lddy, s, lds, mean, rstd, gamma, beta, ds, ldds, M, D, *, dt, ws, seed=0,
            do_tanh=0, p_o=0.0, salt_o=0, row_mask=None, relu_gate_in=0, dr=None, p_r=0.0,
-           salt_r=0, dgamma=None, dbeta=None):
+           salt_r=0, dgamma=None, dbeta=None, dcol=None):
     _chk(N.lib().fs2_ln_bwd(_p(dy), lddy, _p(s), lds, _p(mean), _p(rstd), _p(gamma), _p(beta),
                             do_tanh, p_o, salt_o, _p(row_mask), relu_gate_in, _p(ds), ldds, _p(dr),
-                            p_r, salt_r, _p(dgamma), _p(dbeta), M, D, dt, seed & 0xffffffff,
+                            p_r, salt_r, _p(dgamma), _p(dbeta), _p(dcol), M, D, dt,
+                            seed & 0xffffffff,
                             _p(ws), _s()), "fs2_ln_bwd")
 
 

@@ -99,11 +99,14 @@ int fs2_ln_fwd(const void* x, int64_t ldx, const void* r, int64_t ldr, float p_r
                int dtype, uint32_t seed, void* stream);
 
 /* backward of fs2_ln_fwd; dgamma/dbeta (+)= column sums (fp32).  ds = dL/ds (optionally
- * gated by (s > 0) for a ReLU that produced s), dr = ds * dropmask_r / (1 - p_r).        */
+ * gated by (s > 0) for a ReLU that produced s), dr = ds * dropmask_r / (1 - p_r).
+ * dcol (optional) (+)= column sums of dr (or of ds when dr is NULL): the bias gradient of
+ * the layer whose output fed r (resp. s), fused here instead of a separate fs2_colsum.    */
 int fs2_ln_bwd(const void* dy, int64_t lddy, const void* s, int64_t lds, const float* mean,
                const float* rstd, const float* gamma, const float* beta, int do_tanh, float p_o,
                uint32_t salt_o, const float* row_mask, int relu_gate_in, void* ds, int64_t ldds,
-               void* dr, float p_r, uint32_t salt_r, float* dgamma, float* dbeta, int M, int D,
+               void* dr, float p_r, uint32_t salt_r, float* dgamma, float* dbeta, float* dcol,
+               int M, int D,
                int dtype, uint32_t seed, float* workspace, void* stream);
 int64_t fs2_ln_workspace_floats(int M, int D);
 

@@ -104,10 +104,13 @@ def test_gemm_batched_attention_shapes(cuda, dt, code, tol):
 
 
 @pytest.mark.parametrize("dt,code,tol", DT)
-def test_layernorm_fwd_bwd(cuda, dt, code, tol):
+@pytest.mark.parametrize("D", [384, 90])
+def test_layernorm_fwd_bwd(cuda, dt, code, tol, D):
+    """D=384: 16-byte vector kernels; D=90: scalar kernels.  dcol = fused column sum of the
+    emitted gradient (the bias gradient of the layer that produced s)."""
     from fastspeech2 import ops
     torch.manual_seed(2)
-    M, D = 300, 384
+    M = 300
     x = torch.randn(M, D, device=cuda).to(dt)
     r = torch.randn(M, D, device=cuda).to(dt)
     g = torch.randn(D, device=cuda)
@@ -133,12 +136,18 @@ def test_layernorm_fwd_bwd(cuda, dt, code, tol):
         ds = torch.empty(M, D, device=cuda, dtype=dt)
         dg = torch.zeros(D, device=cuda)
         db = torch.zeros(D, device=cuda)
+        dc = torch.full((D,), 1.0, device=cuda)
         ws = torch.empty(int(ops.ln_ws(M, D)), device=cuda)
         ops.ln_bwd(dy, D, s, D, mean, rstd, g, b, ds, D, M, D, dt=code, ws=ws, do_tanh=tanh,
-                   row_mask=keep, dgamma=dg, dbeta=db)
+                   row_mask=keep, dgamma=dg, dbeta=db, dcol=dc)
         assert rel(ds, sr.grad) < tol * 3
         assert rel(dg, gr.grad) < tol * 3
         assert rel(db, br.grad) < tol * 3
+        assert rel(dc - 1.0, sr.grad.sum(0)) < tol * 3
+        dc2 = torch.zeros(D, device=cuda)          # column sum alone (no gamma/beta)
+        ops.ln_bwd(dy, D, s, D, mean, rstd, g, b, ds, D, M, D, dt=code, ws=ws, do_tanh=tanh,
+                   row_mask=keep, dcol=dc2)
+        assert rel(dc2, sr.grad.sum(0)) < tol * 3
 
 
 def test_attention_mask_quirk_against_torch_mha(cuda, golden_dir):
@@ -366,3 +375,17 @@ def test_gemm_big_tile_paths_bf16(cuda, Bn, T):
     ops.gemm(O, KW * Cin, ops.round_up(M, 8), G, O, X, Cin, dW, KW * Cin, dt=1, a_kmajor=0,
              b_kmajor=0, conv=(3, T, KW, Cin), c_fp32=1, kvalid=M, accumulate=1)
     assert rel(dW - 0.5, Wr.grad.permute(0, 2, 1)) < 2e-2
+
+
+@pytest.mark.parametrize("dt,code,tol", DT)
+@pytest.mark.parametrize("M,N,ldx", [(31264, 1536, 1536), (6400, 1152, 1152 * 3), (777, 90, 96)])
+def test_colsum_bias_gradient(cuda, dt, code, tol, M, N, ldx):
+    """fs2_colsum (bias gradients): out (+)= column sums over rows of a row-pitched matrix."""
+    from fastspeech2 import ops
+    torch.manual_seed(M)
+    X = torch.randn(M, ldx, device=cuda).to(dt)
+    out = torch.full((N,), 2.0, device=cuda)
+    ws = torch.empty(int(ops.colsum_ws(M, N)), device=cuda)
+    ops.colsum(X, ldx, M, N, out, dt=code, ws=ws, accumulate=1)
+    ref = X[:, :N].double().sum(0)
+    assert ((out.double() - 2.0 - ref).abs().max() / ref.abs().max()).item() < 1e-5
