@@ -1,0 +1,560 @@
+// Fused multi-head self-attention (bf16, MFMA) for the FFT blocks: forward and backward
+// without materialising the (B*H, T, T) score / probability tensors.
+//
+// Replaces, for the bf16 train path, the QK^T GEMM + masked softmax + dropout + PV GEMM of
+// torch nn.MultiheadAttention as SB calls it (model.py:338-346, 411-427),
+// with the reference's head-major mask tiling: for z = b*H + h the key k is
+// masked iff key_pad[b][k] | key_pad[(b*H + h) % B][k].  Dropout on the probabilities uses
+// the same counter hash and element index ((z*T + q)*T + k) as the materialised path
+// (attention.hip), so both paths draw identical masks.
+//
+// Layout: Q, K, V are column blocks of the packed projection QKV [B*T][ldq] (q | k | v, head
+// h at columns h*dh of each block); the context O is [B*T][ldo] with head h at h*dh.
+//
+// MFMA orientation (v_mfma_f32_16x16x32_bf16; C lane layout col = lane&15, rows 4*(lane>>4)+r):
+//   forward / dQ:  S^T = K Q^T  -> lanes own queries, so the row softmax statistics, the
+//                  log-sum-exp and D = rowsum(dO*O) are per-lane scalars;
+//                  O^T += V^T P^T, dQ^T += K^T dS^T take P^T / dS^T straight from registers:
+//                  the 32-wide reduction runs over keys {4g..4g+3, 16+4g..16+4g+3} for lane
+//                  group g, and the V^T / K^T fragments are read with ds_read_b64_tr_b16 over
+//                  the same key rows (the order of a reduction's terms is free).
+//   dK, dV:        S = Q K^T  -> lanes own keys; dV += P^T dO, dK += dS^T Q likewise.
+// LDS tiles [rows][dh] bf16 with 16-byte chunk c stored at c ^ (row & 7): conflict-free for
+// both the ds_read_b128 (row-major fragment) and the ds_read_b64_tr_b16 (transposed) reads.
+#include <cstdlib>
+
+#include "fs2_common.h"
+
+namespace {
+
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((ext_vector_type(8))) short s16x8;
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr int TMAX = 2048;
+
+struct AttnP {
+  const bf16* qkv; long ldq;
+  const uint8_t* kpad;
+  const bf16* o; long ldo;       // forward: written; backward: read
+  bf16* out; long ldout;         // forward: O
+  const bf16* dout; long lddo;   // backward: dO
+  bf16* dqkv; long lddq;         // backward: dQ | dK | dV
+  float* lse;                    // [B*H][T], log2 domain of the scaled scores
+  float* dsum;                   // [B*H][T], D = rowsum(dO * O)
+  int B, H, T, D;
+  float scale, scale_log2, p_drop, inv_keep;
+  uint32_t seed, salt;
+};
+
+__device__ __forceinline__ bf16x8 ld_frag(const bf16* g) { return *(const bf16x8*)g; }
+
+// row-major fragment: 8 consecutive features (chunk) of one row
+__device__ __forceinline__ bf16x8 lds_row_frag(const char* t, int rowbytes, int row, int chunk) {
+  return *(const bf16x8*)(t + row * rowbytes + ((chunk ^ (row & 7)) << 4));
+}
+
+// transposed fragment for an A operand A[m = feature][k = row] over the 32 rows
+// {4g..4g+3, 16+4g..16+4g+3} + rbase of lane group g, features m0..m0+15
+__device__ __forceinline__ bf16x8 lds_tr_frag(const char* t, int rowbytes, int rbase, int m0,
+                                              int lane) {
+  const int li = lane & 15, g = lane >> 4, q = li >> 2, p = li & 3;
+  const int m = m0 + 4 * p;
+  const int c = m >> 3, boff = (m & 7) * 2;
+  const int k1 = rbase + 4 * g + q, k2 = k1 + 16;
+  const char* a1 = t + k1 * rowbytes + ((c ^ (k1 & 7)) << 4) + boff;
+  const char* a2 = t + k2 * rowbytes + ((c ^ (k2 & 7)) << 4) + boff;
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a1);
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a2);
+  const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// rows [r0, r0 + NR) of a [rows][DH] column block starting at src (row pitch ld) -> LDS tile
+template <int DH, int NR>
+__device__ __forceinline__ void load_tile(char* t, const bf16* src, long ld, int r0, int nrows,
+                                          int tid, int nthreads) {
+  constexpr int CPR = DH / 8;
+  for (int i = tid; i < NR * CPR; i += nthreads) {
+    const int r = i / CPR, c = i - r * CPR;
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if (r0 + r < nrows) v = *(const u32x4*)(src + (long)(r0 + r) * ld + c * 8);
+    *(u32x4*)(t + r * DH * 2 + ((c ^ (r & 7)) << 4)) = v;
+  }
+}
+
+__device__ __forceinline__ bf16x8 pack8(const float* a, const float* b) {
+  bf16x8 r;
+  r[0] = (bf16)a[0]; r[1] = (bf16)a[1]; r[2] = (bf16)a[2]; r[3] = (bf16)a[3];
+  r[4] = (bf16)b[0]; r[5] = (bf16)b[1]; r[6] = (bf16)b[2]; r[7] = (bf16)b[3];
+  return r;
+}
+
+__device__ __forceinline__ float xg_max(float v) {
+  v = fmaxf(v, __shfl_xor(v, 16, 64));
+  return fmaxf(v, __shfl_xor(v, 32, 64));
+}
+__device__ __forceinline__ float xg_sum(float v) {
+  v += __shfl_xor(v, 16, 64);
+  return v + __shfl_xor(v, 32, 64);
+}
+
+// key-valid flags for (b, h) and the end of the last valid key
+__device__ __forceinline__ int build_kvalid(uint8_t* kval, int* kend_s, const AttnP& p, int b,
+                                            int h) {
+  const int b2 = (b * p.H + h) % p.B;
+  const uint8_t* k1 = p.kpad + (long)b * p.T;
+  const uint8_t* k2 = p.kpad + (long)b2 * p.T;
+  if (threadIdx.x == 0) *kend_s = 0;
+  __syncthreads();
+  int last = 0;
+  for (int j = threadIdx.x; j < p.T; j += blockDim.x) {
+    const uint8_t v = !(k1[j] | k2[j]);
+    kval[j] = v;
+    if (v) last = j + 1;
+  }
+  atomicMax(kend_s, last);
+  __syncthreads();
+  return *kend_s;
+}
+
+// ------------------------------------------------------------------------------ forward
+// block: 128 queries = (8 / QG) waves x QG 16-query groups; K/V tiles of 64 keys
+template <int DH, int QG>
+__global__ void __launch_bounds__(512 / QG, QG) attn_fwd_kernel(AttnP p) {
+  constexpr int NT = 512 / QG;
+  constexpr int NS = DH / 32, ND = DH / 16;
+  __shared__ __attribute__((aligned(16))) char Ks[64 * DH * 2];
+  __shared__ __attribute__((aligned(16))) char Vs[64 * DH * 2];
+  __shared__ uint8_t kval[TMAX];
+  __shared__ int kend_s;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
+  const int z = blockIdx.y, b = z / p.H, h = z - b * p.H;
+  const int kend = build_kvalid(kval, &kend_s, p, b, h);
+  const bf16* Qb = p.qkv + (long)b * p.T * p.ldq + h * DH;
+  const bf16* Kb = Qb + p.D;
+  const bf16* Vb = Qb + 2 * p.D;
+
+  int qi[QG];
+  bf16x8 qf[QG][NS];
+#pragma unroll
+  for (int qg = 0; qg < QG; ++qg) {
+    qi[qg] = blockIdx.x * 128 + wave * 16 * QG + qg * 16 + (lane & 15);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      if (qi[qg] < p.T) qf[qg][s] = ld_frag(Qb + (long)qi[qg] * p.ldq + 32 * s + 8 * g);
+      else qf[qg][s] = bf16x8{};
+    }
+  }
+  f32x4 oacc[ND][QG];
+#pragma unroll
+  for (int d = 0; d < ND; ++d)
+#pragma unroll
+    for (int qg = 0; qg < QG; ++qg) oacc[d][qg] = f32x4{0, 0, 0, 0};
+  float mrow[QG], lrow[QG];
+#pragma unroll
+  for (int qg = 0; qg < QG; ++qg) { mrow[qg] = -INFINITY; lrow[qg] = 0.f; }
+
+  for (int k0 = 0; k0 < kend; k0 += 64) {
+    __syncthreads();
+    load_tile<DH, 64>(Ks, Kb, p.ldq, k0, p.T, threadIdx.x, NT);
+    load_tile<DH, 64>(Vs, Vb, p.ldq, k0, p.T, threadIdx.x, NT);
+    __syncthreads();
+    f32x4 sacc[4][QG];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int qg = 0; qg < QG; ++qg) sacc[kt][qg] = f32x4{0, 0, 0, 0};
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+        const bf16x8 kf = lds_row_frag(Ks, DH * 2, kt * 16 + (lane & 15), 4 * s + g);
+#pragma unroll
+        for (int qg = 0; qg < QG; ++qg)
+          sacc[kt][qg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qg][s], sacc[kt][qg], 0, 0, 0);
+      }
+    bf16x8 pf[QG][2];
+#pragma unroll
+    for (int qg = 0; qg < QG; ++qg) {
+      float v[4][4];
+      float mt = -INFINITY;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = k0 + kt * 16 + 4 * g + r;
+          const bool ok = key < p.T && kval[key];
+          v[kt][r] = ok ? sacc[kt][qg][r] * p.scale_log2 : -INFINITY;
+          mt = fmaxf(mt, v[kt][r]);
+        }
+      mt = xg_max(mt);
+      const float mnew = fmaxf(mrow[qg], mt);
+      const float alpha = mnew == -INFINITY ? 1.f : exp2f(mrow[qg] - mnew);
+      mrow[qg] = mnew;
+      float ls = 0.f;
+      float pd[4][4];
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float e = v[kt][r] == -INFINITY ? 0.f : exp2f(v[kt][r] - mnew);
+          ls += e;
+          float q = e;
+          if (p.p_drop > 0.f) {
+            const int key = k0 + kt * 16 + 4 * g + r;
+            q = fs2_keep(p.seed, p.salt, ((uint64_t)z * p.T + qi[qg]) * p.T + key, p.p_drop)
+                    ? e * p.inv_keep : 0.f;
+          }
+          pd[kt][r] = q;
+        }
+      lrow[qg] = lrow[qg] * alpha + ls;
+#pragma unroll
+      for (int d = 0; d < ND; ++d) oacc[d][qg] *= alpha;
+      pf[qg][0] = pack8(pd[0], pd[1]);
+      pf[qg][1] = pack8(pd[2], pd[3]);
+    }
+#pragma unroll
+    for (int d = 0; d < ND; ++d)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const bf16x8 vf = lds_tr_frag(Vs, DH * 2, 32 * j, 16 * d, lane);
+#pragma unroll
+        for (int qg = 0; qg < QG; ++qg)
+          oacc[d][qg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[qg][j], oacc[d][qg], 0, 0, 0);
+      }
+  }
+#pragma unroll
+  for (int qg = 0; qg < QG; ++qg) {
+    const float l = xg_sum(lrow[qg]);
+    const float inv = 1.f / l;
+    if (qi[qg] >= p.T) continue;
+    if (g == 0) p.lse[(long)z * p.T + qi[qg]] = mrow[qg] + log2f(l);
+    bf16* orow = p.out + ((long)b * p.T + qi[qg]) * p.ldout + h * DH;
+#pragma unroll
+    for (int d = 0; d < ND; ++d) {
+      const f32x4 a = oacc[d][qg] * inv;
+      u32x2 w;
+      w[0] = (unsigned)__builtin_bit_cast(unsigned short, (bf16)a[0]) |
+             ((unsigned)__builtin_bit_cast(unsigned short, (bf16)a[1]) << 16);
+      w[1] = (unsigned)__builtin_bit_cast(unsigned short, (bf16)a[2]) |
+             ((unsigned)__builtin_bit_cast(unsigned short, (bf16)a[3]) << 16);
+      *(u32x2*)(orow + 16 * d + 4 * g) = w;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------ backward dQ
+// block: 128 queries = (8 / QG) waves x QG 16-query groups; also writes D = rowsum(dO * O)
+// for the dK/dV kernel
+template <int DH, int QG>
+__global__ void __launch_bounds__(512 / QG, QG) attn_bwd_dq_kernel(AttnP p) {
+  constexpr int NT = 512 / QG;
+  constexpr int NS = DH / 32, ND = DH / 16;
+  __shared__ __attribute__((aligned(16))) char Ks[64 * DH * 2];
+  __shared__ __attribute__((aligned(16))) char Vs[64 * DH * 2];
+  __shared__ uint8_t kval[TMAX];
+  __shared__ int kend_s;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
+  const int z = blockIdx.y, b = z / p.H, h = z - b * p.H;
+  const int kend = build_kvalid(kval, &kend_s, p, b, h);
+  const bf16* Qb = p.qkv + (long)b * p.T * p.ldq + h * DH;
+  const bf16* Kb = Qb + p.D;
+  const bf16* Vb = Qb + 2 * p.D;
+
+  int qi[QG];
+  bf16x8 qf[QG][NS], dof[QG][NS];
+  float lse[QG], dsum[QG];
+#pragma unroll
+  for (int qg = 0; qg < QG; ++qg) {
+    qi[qg] = blockIdx.x * 128 + wave * 16 * QG + qg * 16 + (lane & 15);
+    const bool in = qi[qg] < p.T;
+    float dot = 0.f;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      if (in) {
+        qf[qg][s] = ld_frag(Qb + (long)qi[qg] * p.ldq + 32 * s + 8 * g);
+        const long ro = (long)b * p.T + qi[qg];
+        dof[qg][s] = ld_frag(p.dout + ro * p.lddo + h * DH + 32 * s + 8 * g);
+        const bf16x8 of = ld_frag(p.o + ro * p.ldo + h * DH + 32 * s + 8 * g);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dot += (float)dof[qg][s][e] * (float)of[e];
+      } else {
+        qf[qg][s] = bf16x8{};
+        dof[qg][s] = bf16x8{};
+      }
+    }
+    dsum[qg] = xg_sum(dot);
+    lse[qg] = in ? p.lse[(long)z * p.T + qi[qg]] : 0.f;
+    if (in && g == 0) p.dsum[(long)z * p.T + qi[qg]] = dsum[qg];
+  }
+  f32x4 qacc[ND][QG];
+#pragma unroll
+  for (int d = 0; d < ND; ++d)
+#pragma unroll
+    for (int qg = 0; qg < QG; ++qg) qacc[d][qg] = f32x4{0, 0, 0, 0};
+
+  for (int k0 = 0; k0 < kend; k0 += 64) {
+    __syncthreads();
+    load_tile<DH, 64>(Ks, Kb, p.ldq, k0, p.T, threadIdx.x, NT);
+    load_tile<DH, 64>(Vs, Vb, p.ldq, k0, p.T, threadIdx.x, NT);
+    __syncthreads();
+    f32x4 sacc[4][QG], pacc[4][QG];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int qg = 0; qg < QG; ++qg) { sacc[kt][qg] = f32x4{0, 0, 0, 0}; pacc[kt][qg] = f32x4{0, 0, 0, 0}; }
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+        const bf16x8 kf = lds_row_frag(Ks, DH * 2, kt * 16 + (lane & 15), 4 * s + g);
+        const bf16x8 vf = lds_row_frag(Vs, DH * 2, kt * 16 + (lane & 15), 4 * s + g);
+#pragma unroll
+        for (int qg = 0; qg < QG; ++qg) {
+          sacc[kt][qg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qg][s], sacc[kt][qg], 0, 0, 0);
+          pacc[kt][qg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, dof[qg][s], pacc[kt][qg], 0, 0, 0);
+        }
+      }
+    bf16x8 sf[QG][2];
+#pragma unroll
+    for (int qg = 0; qg < QG; ++qg) {
+      float ds[4][4];
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = k0 + kt * 16 + 4 * g + r;
+          const bool ok = key < p.T && kval[key];
+          const float pr = ok ? exp2f(sacc[kt][qg][r] * p.scale_log2 - lse[qg]) : 0.f;
+          float dp = pacc[kt][qg][r];
+          if (p.p_drop > 0.f)
+            dp = fs2_keep(p.seed, p.salt, ((uint64_t)z * p.T + qi[qg]) * p.T + key, p.p_drop)
+                     ? dp * p.inv_keep : 0.f;
+          ds[kt][r] = pr * (dp - dsum[qg]);
+        }
+      sf[qg][0] = pack8(ds[0], ds[1]);
+      sf[qg][1] = pack8(ds[2], ds[3]);
+    }
+#pragma unroll
+    for (int d = 0; d < ND; ++d)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const bf16x8 kf = lds_tr_frag(Ks, DH * 2, 32 * j, 16 * d, lane);
+#pragma unroll
+        for (int qg = 0; qg < QG; ++qg)
+          qacc[d][qg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, sf[qg][j], qacc[d][qg], 0, 0, 0);
+      }
+  }
+#pragma unroll
+  for (int qg = 0; qg < QG; ++qg) {
+    if (qi[qg] >= p.T) continue;
+    bf16* row = p.dqkv + ((long)b * p.T + qi[qg]) * p.lddq + h * DH;
+#pragma unroll
+    for (int d = 0; d < ND; ++d) {
+      const f32x4 a = qacc[d][qg] * p.scale;
+      u32x2 w;
+      w[0] = (unsigned)__builtin_bit_cast(unsigned short, (bf16)a[0]) |
+             ((unsigned)__builtin_bit_cast(unsigned short, (bf16)a[1]) << 16);
+      w[1] = (unsigned)__builtin_bit_cast(unsigned short, (bf16)a[2]) |
+             ((unsigned)__builtin_bit_cast(unsigned short, (bf16)a[3]) << 16);
+      *(u32x2*)(row + 16 * d + 4 * g) = w;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------ backward dK dV
+// block: 8 waves x 16 keys; query tiles of 64 (Q, dO, lse, D staged in LDS)
+template <int DH>
+__global__ void __launch_bounds__(512, 1) attn_bwd_dkv_kernel(AttnP p) {
+  constexpr int NS = DH / 32, ND = DH / 16;
+  __shared__ __attribute__((aligned(16))) char Qs[64 * DH * 2];
+  __shared__ __attribute__((aligned(16))) char Os[64 * DH * 2];  // dO tile
+  __shared__ float ls_s[64], ds_s[64];
+  __shared__ uint8_t kval[TMAX];
+  __shared__ int kend_s;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
+  const int z = blockIdx.y, b = z / p.H, h = z - b * p.H;
+  build_kvalid(kval, &kend_s, p, b, h);
+  const bf16* Qb = p.qkv + (long)b * p.T * p.ldq + h * DH;
+  const bf16* Kb = Qb + p.D;
+  const bf16* Vb = Qb + 2 * p.D;
+  const bf16* dOb = p.dout + (long)b * p.T * p.lddo + h * DH;
+
+  const int key = blockIdx.x * 128 + wave * 16 + (lane & 15);   // this lane's key (B col)
+  const bool kin = key < p.T;
+  const bool kok = kin && kval[key];
+  bf16x8 kf[NS], vf[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    kf[s] = kin ? ld_frag(Kb + (long)key * p.ldq + 32 * s + 8 * g) : bf16x8{};
+    vf[s] = kin ? ld_frag(Vb + (long)key * p.ldq + 32 * s + 8 * g) : bf16x8{};
+  }
+  f32x4 dk[ND], dv[ND];
+#pragma unroll
+  for (int d = 0; d < ND; ++d) { dk[d] = f32x4{0, 0, 0, 0}; dv[d] = f32x4{0, 0, 0, 0}; }
+  // a block whose 128 keys are all masked contributes nothing: skip the query loop
+  const int anyk = __syncthreads_or(kok);
+
+  for (int q0 = 0; anyk && q0 < p.T; q0 += 64) {
+    __syncthreads();
+    load_tile<DH, 64>(Qs, Qb, p.ldq, q0, p.T, threadIdx.x, 512);
+    load_tile<DH, 64>(Os, dOb, p.lddo, q0, p.T, threadIdx.x, 512);
+    if (threadIdx.x < 64) {
+      const int q = q0 + threadIdx.x;
+      ls_s[threadIdx.x] = q < p.T ? p.lse[(long)z * p.T + q] : 0.f;
+      ds_s[threadIdx.x] = q < p.T ? p.dsum[(long)z * p.T + q] : 0.f;
+    }
+    __syncthreads();
+    // S = Q K^T, dP = dO V^T for 64 queries x this wave's 16 keys (C: col key, rows queries)
+    f32x4 sacc[4], pacc[4];
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt) { sacc[qt] = f32x4{0, 0, 0, 0}; pacc[qt] = f32x4{0, 0, 0, 0}; }
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+      for (int qt = 0; qt < 4; ++qt) {
+        const bf16x8 qa = lds_row_frag(Qs, DH * 2, qt * 16 + (lane & 15), 4 * s + g);
+        const bf16x8 oa = lds_row_frag(Os, DH * 2, qt * 16 + (lane & 15), 4 * s + g);
+        sacc[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, kf[s], sacc[qt], 0, 0, 0);
+        pacc[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(oa, vf[s], pacc[qt], 0, 0, 0);
+      }
+    float pdv[4][4], dsv[4][4];
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ql = qt * 16 + 4 * g + r, q = q0 + ql;
+        const bool ok = kok && q < p.T;
+        const float pr = ok ? exp2f(sacc[qt][r] * p.scale_log2 - ls_s[ql]) : 0.f;
+        float dp = pacc[qt][r];
+        float pd = pr;
+        if (p.p_drop > 0.f) {
+          const bool keep = fs2_keep(p.seed, p.salt, ((uint64_t)z * p.T + q) * p.T + key, p.p_drop);
+          dp = keep ? dp * p.inv_keep : 0.f;
+          pd = keep ? pr * p.inv_keep : 0.f;
+        }
+        pdv[qt][r] = pd;
+        dsv[qt][r] = pr * (dp - ds_s[ql]);
+      }
+    // dV += Pd^T dO, dK += dS^T Q : A = (key x query) from registers, B = tile^T via tr reads
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const bf16x8 pa = pack8(pdv[2 * j], pdv[2 * j + 1]);
+      const bf16x8 sa = pack8(dsv[2 * j], dsv[2 * j + 1]);
+#pragma unroll
+      for (int d = 0; d < ND; ++d) {
+        const bf16x8 ob = lds_tr_frag(Os, DH * 2, 32 * j, 16 * d, lane);
+        const bf16x8 qb = lds_tr_frag(Qs, DH * 2, 32 * j, 16 * d, lane);
+        dv[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, ob, dv[d], 0, 0, 0);
+        dk[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sa, qb, dk[d], 0, 0, 0);
+      }
+    }
+  }
+  // C layout: col = feature (lane & 15), rows = keys 4g + r of this wave's 16
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int kr = blockIdx.x * 128 + wave * 16 + 4 * g + r;
+    if (kr >= p.T) continue;
+    bf16* krow = p.dqkv + ((long)b * p.T + kr) * p.lddq + p.D + h * DH;
+    bf16* vrow = krow + p.D;
+#pragma unroll
+    for (int d = 0; d < ND; ++d) {
+      krow[16 * d + (lane & 15)] = (bf16)(dk[d][r] * p.scale);
+      vrow[16 * d + (lane & 15)] = (bf16)dv[d][r];
+    }
+  }
+}
+
+int attn_qg_fwd(int dh) {
+  static const int env = [] { const char* v = std::getenv("FS2_ATTN_QG"); return v ? std::atoi(v) : 0; }();
+  if (env == 1 || env == 2) return env;
+  return dh <= 128 ? 2 : 1;
+}
+
+template <int DH>
+void launch_fwd(const AttnP& p, hipStream_t s) {
+  dim3 grid((p.T + 127) / 128, p.B * p.H);
+  if (attn_qg_fwd(DH) == 2) hipLaunchKernelGGL((attn_fwd_kernel<DH, 2>), grid, dim3(256), 0, s, p);
+  else hipLaunchKernelGGL((attn_fwd_kernel<DH, 1>), grid, dim3(512), 0, s, p);
+}
+template <int DH>
+void launch_bwd(const AttnP& p, hipStream_t s) {
+  dim3 g1((p.T + 127) / 128, p.B * p.H);
+  if (DH <= 64) hipLaunchKernelGGL((attn_bwd_dq_kernel<DH, 2>), g1, dim3(256), 0, s, p);
+  else hipLaunchKernelGGL((attn_bwd_dq_kernel<DH, 1>), g1, dim3(512), 0, s, p);
+  hipLaunchKernelGGL(attn_bwd_dkv_kernel<DH>, g1, dim3(512), 0, s, p);
+}
+
+bool a16(const void* q) { return ((uintptr_t)q & 15) == 0; }
+
+int check(int B, int H, int T, int dh, long ldq, const void* qkv, int dtype) {
+  if (dtype != FS2_BF16) return FS2_EINVAL;
+  if (B <= 0 || H <= 0 || T <= 0 || T > TMAX) return FS2_EINVAL;
+  if (dh != 64 && dh != 128 && dh != 192 && dh != 256) return FS2_EINVAL;
+  if (!qkv || !a16(qkv) || (ldq % 8) || ldq < 3L * H * dh) return FS2_EALIGN;
+  return 0;
+}
+
+}  // namespace
+
+extern "C" int fs2_attn_supported(int T, int dh, int dtype) {
+  return dtype == FS2_BF16 && T > 0 && T <= TMAX &&
+         (dh == 64 || dh == 128 || dh == 192 || dh == 256);
+}
+
+extern "C" int fs2_attn_fwd(const void* qkv, int64_t ldq, const uint8_t* key_pad, int B, int H,
+                            int T, int dh, float scale, float p_drop, uint32_t seed,
+                            uint32_t salt, void* out, int64_t ldo, float* lse, int dtype,
+                            void* stream) {
+  if (int rc = check(B, H, T, dh, ldq, qkv, dtype)) return rc;
+  if (!key_pad || !out || !lse || !a16(out) || (ldo % 8)) return FS2_EINVAL;
+  AttnP p{};
+  p.qkv = (const bf16*)qkv; p.ldq = ldq; p.kpad = key_pad;
+  p.out = (bf16*)out; p.ldout = ldo; p.lse = lse;
+  p.B = B; p.H = H; p.T = T; p.D = H * dh;
+  p.scale = scale; p.scale_log2 = scale * LOG2E; p.p_drop = p_drop;
+  p.inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+  p.seed = seed; p.salt = salt;
+  hipStream_t s = (hipStream_t)stream;
+  switch (dh) {
+    case 64: launch_fwd<64>(p, s); break;
+    case 128: launch_fwd<128>(p, s); break;
+    case 192: launch_fwd<192>(p, s); break;
+    default: launch_fwd<256>(p, s); break;
+  }
+  FS2_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int fs2_attn_bwd(const void* qkv, int64_t ldq, const uint8_t* key_pad,
+                            const void* out, int64_t ldo, const void* dout, int64_t lddo,
+                            const float* lse, int B, int H, int T, int dh, float scale,
+                            float p_drop, uint32_t seed, uint32_t salt, void* dqkv,
+                            int64_t lddq, float* workspace, int dtype, void* stream) {
+  if (int rc = check(B, H, T, dh, ldq, qkv, dtype)) return rc;
+  if (!key_pad || !out || !dout || !lse || !dqkv || !workspace) return FS2_EINVAL;
+  if (!a16(out) || !a16(dout) || !a16(dqkv) || (ldo % 8) || (lddo % 8) || (lddq % 8))
+    return FS2_EALIGN;
+  AttnP p{};
+  p.qkv = (const bf16*)qkv; p.ldq = ldq; p.kpad = key_pad;
+  p.o = (const bf16*)out; p.ldo = ldo;
+  p.dout = (const bf16*)dout; p.lddo = lddo;
+  p.dqkv = (bf16*)dqkv; p.lddq = lddq;
+  p.lse = (float*)lse; p.dsum = workspace;
+  p.B = B; p.H = H; p.T = T; p.D = H * dh;
+  p.scale = scale; p.scale_log2 = scale * LOG2E; p.p_drop = p_drop;
+  p.inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+  p.seed = seed; p.salt = salt;
+  hipStream_t s = (hipStream_t)stream;
+  switch (dh) {
+    case 64: launch_bwd<64>(p, s); break;
+    case 128: launch_bwd<128>(p, s); break;
+    case 192: launch_bwd<192>(p, s); break;
+    default: launch_bwd<256>(p, s); break;
+  }
+  FS2_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int64_t fs2_attn_workspace_floats(int B, int H, int T) { return (int64_t)B * H * T; }

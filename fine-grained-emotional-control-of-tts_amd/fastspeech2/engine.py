@@ -14,6 +14,7 @@ gradients, LayerNorm statistics and losses are fp32 in both.
 """
 
 import math
+import os
 
 import torch
 
@@ -31,6 +32,9 @@ class _Salt:
     def __call__(self):
         self.n += 1
         return self.n
+
+
+_NO_FLASH = os.environ.get("FS2_NO_FLASH", "0") not in ("", "0")
 
 
 def dgrad_split(Mp, C, K, dt):
@@ -74,6 +78,11 @@ class FS2Engine:
             self.timer.stop(tag)
 
     # ------------------------------------------------------------------ helpers
+    def use_flash(self, T, dh):
+        """fused attention kernels on the bf16 path (fp32 parity mode keeps the materialised
+        softmax); FS2_NO_FLASH=1 forces the materialised path for A/B runs."""
+        return self.dt == 1 and not _NO_FLASH and ops.attn_supported(T, dh, self.dt)
+
     def ws(self, n):
         n = int(n)
         if self._ws.numel() < n:
@@ -182,20 +191,29 @@ class FS2Engine:
         self._fwd(X, D, M, T, prefix + "self_att.att.in_proj_weight", QKV, 3 * D,
                   bias=P[prefix + "self_att.att.in_proj_bias"])
         ldt = round_up(T, 8)
-        S = torch.empty(B * H, T, ldt, dtype=torch.float32, device=self.dev)
-        ops.gemm(T, T, dh, QKV, 3 * D, QKV[:, D:], 3 * D, S, ldt, dt=self.dt, c_fp32=1,
-                 batch=B * H, batch_div=H,
-                 strides=(T * 3 * D, dh, T * 3 * D, dh, H * T * ldt, T * ldt, 0, 0))
-        Pm = self.empty(B * H, T, ldt)
-        Pd = self.empty(B * H, T, ldt) if p_drop > 0 else Pm
-        s_att = salt()
-        ops.softmax_fwd(S, key_pad, B, H, T, T, ldt, 1.0 / math.sqrt(dh), p_drop, seed, s_att, Pm,
-                        Pd if p_drop > 0 else None, dt=self.dt)
-        del S
         Att = self.empty(M, D)
-        ops.gemm(T, dh, ldt, Pd, ldt, QKV[:, 2 * D:], 3 * D, Att, D, dt=self.dt, b_kmajor=0,
-                 kvalid=T, batch=B * H, batch_div=H,
-                 strides=(H * T * ldt, T * ldt, T * 3 * D, dh, T * D, dh, 0, 0))
+        if self.use_flash(T, dh):
+            # fused attention: no (B*H, T, T) tensors; lse kept for the backward
+            lse = torch.empty(B * H, T, dtype=torch.float32, device=self.dev)
+            s_att = salt()
+            ops.attn_fwd(QKV, 3 * D, key_pad, B, H, T, dh, 1.0 / math.sqrt(dh), p_drop, seed,
+                         s_att, Att, D, lse, dt=self.dt)
+            Pm = Pd = None
+            ctx.update(lse=lse, key_pad=key_pad)
+        else:
+            S = torch.empty(B * H, T, ldt, dtype=torch.float32, device=self.dev)
+            ops.gemm(T, T, dh, QKV, 3 * D, QKV[:, D:], 3 * D, S, ldt, dt=self.dt, c_fp32=1,
+                     batch=B * H, batch_div=H,
+                     strides=(T * 3 * D, dh, T * 3 * D, dh, H * T * ldt, T * ldt, 0, 0))
+            Pm = self.empty(B * H, T, ldt)
+            Pd = self.empty(B * H, T, ldt) if p_drop > 0 else Pm
+            s_att = salt()
+            ops.softmax_fwd(S, key_pad, B, H, T, T, ldt, 1.0 / math.sqrt(dh), p_drop, seed, s_att,
+                            Pm, Pd if p_drop > 0 else None, dt=self.dt)
+            del S
+            ops.gemm(T, dh, ldt, Pd, ldt, QKV[:, 2 * D:], 3 * D, Att, D, dt=self.dt, b_kmajor=0,
+                     kvalid=T, batch=B * H, batch_div=H,
+                     strides=(H * T * ldt, T * ldt, T * 3 * D, dh, T * D, dh, 0, 0))
         Ao = self.empty(M, D)
         self._fwd(Att, D, M, T, prefix + "self_att.att.out_proj.weight", Ao, D,
                   bias=P[prefix + "self_att.att.out_proj.bias"])
@@ -265,8 +283,14 @@ class FS2Engine:
         self._dgrad(dAo, D, M, T, wo, dAtt, D)
         self._wgrad(dAo, D, ctx["Att"], D, M, T, wo)
         del dAo
-        # ---- attention backward over the materialised probabilities
         QKV, Pm, Pd = ctx["QKV"], ctx["Pm"], ctx["Pd"]
+        if "lse" in ctx:     # fused attention backward (dQ, dK, dV in one pass each)
+            dQKV = self.empty(M, 3 * D)
+            ops.attn_bwd(QKV, 3 * D, ctx["key_pad"], ctx["Att"], D, dAtt, D, ctx["lse"], B, H, T,
+                         dh, 1.0 / math.sqrt(dh), p_drop, seed, ctx["s_att"], dQKV, 3 * D,
+                         dt=self.dt, ws=self.ws(ops.attn_ws(B, H, T)))
+            return self._qkv_bwd(dQKV, ctx, M, T, D, prefix, ds1)
+        # ---- attention backward over the materialised probabilities
         dPd = torch.empty(B * H, T, ldt, dtype=torch.float32, device=self.dev)
         ops.gemm(T, T, dh, dAtt, D, QKV[:, 2 * D:], 3 * D, dPd, ldt, dt=self.dt, c_fp32=1,
                  batch=B * H, batch_div=H,
@@ -289,6 +313,9 @@ class FS2Engine:
                  b_kmajor=0, kvalid=T, mvalid=T, batch=B * H, batch_div=H,
                  strides=(H * T * ldt, T * ldt, T * 3 * D, dh, T * 3 * D, dh, 0, 0))
         del dS
+        return self._qkv_bwd(dQKV, ctx, M, T, D, prefix, ds1)
+
+    def _qkv_bwd(self, dQKV, ctx, M, T, D, prefix, ds1):
         wi = prefix + "self_att.att.in_proj_weight"
         dX = self.empty(M, D)
         self._dgrad(dQKV, 3 * D, M, T, wi, dX, D, residual=ds1, ldr=D)

@@ -95,6 +95,27 @@ def ln_ws(M, D):
     return N.lib().fs2_ln_workspace_floats(M, D)
 
 
+def attn_supported(T, dh, dt):
+    return bool(N.lib().fs2_attn_supported(T, dh, dt))
+
+
+def attn_fwd(qkv, ldq, key_pad, B, H, T, dh, scale, p_drop, seed, salt, out, ldo, lse, *, dt):
+    _chk(N.lib().fs2_attn_fwd(_p(qkv), ldq, _p(key_pad), B, H, T, dh, scale, p_drop,
+                              seed & 0xffffffff, salt, _p(out), ldo, _p(lse), dt, _s()),
+         "fs2_attn_fwd")
+
+
+def attn_bwd(qkv, ldq, key_pad, out, ldo, dout, lddo, lse, B, H, T, dh, scale, p_drop, seed, salt,
+             dqkv, lddq, *, dt, ws):
+    _chk(N.lib().fs2_attn_bwd(_p(qkv), ldq, _p(key_pad), _p(out), ldo, _p(dout), lddo, _p(lse), B,
+                              H, T, dh, scale, p_drop, seed & 0xffffffff, salt, _p(dqkv), lddq,
+                              _p(ws), dt, _s()), "fs2_attn_bwd")
+
+
+def attn_ws(B, H, T):
+    return N.lib().fs2_attn_workspace_floats(B, H, T)
+
+
 def softmax_fwd(S, key_pad, B, H, Tq, Tk, ldt, scale, p_drop, seed, salt, P, Pd, *, dt):
     _chk(N.lib().fs2_softmax_fwd(_p(S), _p(key_pad), B, H, Tq, Tk, ldt, scale, p_drop,
                                  seed & 0xffffffff, salt, _p(P), _p(Pd), dt, _s()), "fs2_softmax_fwd")

@@ -126,6 +126,25 @@ int fs2_softmax_bwd(const float* dPd, const void* P, int B, int H, int Tq, int T
                     void* stream);
 
 /* ------------------------------------------------------------------------------------------
+ * Fused attention (bf16; K4/K16): softmax(scale * Q K^T with the tiling mask) -> dropout -> PV
+ * without materialising the (B*H, T, T) scores.  Q | K | V are column blocks of the packed
+ * projection qkv [B*T][ldq] (head h at columns h*dh of each block); out [B*T][ldo] gets head h
+ * at h*dh; lse [B*H][T] keeps the log2-domain log-sum-exp for the backward, which writes
+ * dQ | dK | dV into dqkv with the same layout as qkv.  Same mask rule and dropout indices as
+ * fs2_softmax_fwd/bwd.  Requires dtype bf16, dh in {64,128,192,256}, T <= 2048
+ * (fs2_attn_supported); workspace: fs2_attn_workspace_floats.
+ * ------------------------------------------------------------------------------------------ */
+int fs2_attn_supported(int T, int dh, int dtype);
+int fs2_attn_fwd(const void* qkv, int64_t ldq, const uint8_t* key_pad, int B, int H, int T,
+                 int dh, float scale, float p_drop, uint32_t seed, uint32_t salt, void* out,
+                 int64_t ldo, float* lse, int dtype, void* stream);
+int fs2_attn_bwd(const void* qkv, int64_t ldq, const uint8_t* key_pad, const void* out,
+                 int64_t ldo, const void* dout, int64_t lddo, const float* lse, int B, int H,
+                 int T, int dh, float scale, float p_drop, uint32_t seed, uint32_t salt,
+                 void* dqkv, int64_t lddq, float* workspace, int dtype, void* stream);
+int64_t fs2_attn_workspace_floats(int B, int H, int T);
+
+/* ------------------------------------------------------------------------------------------
  * Token embedding + positional encoding + pad mask (K1, K2; model.py:331-337)
  *   X[m] = (E[tok[m]] + pe[t]) * (tok[m] != pad);  keep[m] = (tok[m] != pad)
  * ------------------------------------------------------------------------------------------ */

@@ -389,3 +389,71 @@ def test_colsum_bias_gradient(cuda, dt, code, tol, M, N, ldx):
     ops.colsum(X, ldx, M, N, out, dt=code, ws=ws, accumulate=1)
     ref = X[:, :N].double().sum(0)
     assert ((out.double() - 2.0 - ref).abs().max() / ref.abs().max()).item() < 1e-5
+
+
+def _keep_np(seed, salt, idx, p):
+    """numpy restatement of fs2_keep (fs2_common.h) for the dropout masks of the HIP kernels."""
+    M32 = np.uint64(0xffffffff)
+
+    def mix(h):
+        h = h & M32
+        h ^= h >> np.uint64(16)
+        h = (h * np.uint64(0x85ebca6b)) & M32
+        h ^= h >> np.uint64(13)
+        h = (h * np.uint64(0xc2b2ae35)) & M32
+        h ^= h >> np.uint64(16)
+        return h
+
+    idx = idx.astype(np.uint64)
+    s0 = mix(np.uint64((seed ^ ((salt * 0x9E3779B9) & 0xffffffff)) & 0xffffffff))
+    h = mix((idx & M32) ^ s0)
+    h = mix(h ^ (idx >> np.uint64(32)) ^ np.uint64(0x68bc21eb))
+    return ((h >> np.uint64(8)).astype(np.float64) / 16777216.0) >= p
+
+
+@pytest.mark.parametrize("dh,T,p_drop", [(192, 150, 0.0), (192, 150, 0.1), (64, 70, 0.1),
+                                          (256, 130, 0.0)])
+def test_fused_attention_vs_torch(cuda, dh, T, p_drop):
+    """fs2_attn_fwd/bwd (bf16) against torch fp32 on the same bf16 Q/K/V: the head-major mask
+    tiling rule, ragged lengths, and (p > 0) the counter-hash dropout masks restated in numpy.
+    Tolerance rel 2e-2 (O) / 3e-2 (dQ, dK, dV): bf16 operands and probabilities."""
+    from fastspeech2 import ops
+    torch.manual_seed(dh + T)
+    B, H = 3, 2
+    D = H * dh
+    lens = [T, T - 37, T - 90]
+    qkv = (torch.randn(B * T, 3 * D, device=cuda) * 0.5).to(torch.bfloat16)
+    kp = torch.zeros(B, T, dtype=torch.uint8, device=cuda)
+    for b, L in enumerate(lens):
+        kp[b, L:] = 1
+    scale = 1.0 / math.sqrt(dh)
+    seed, salt = 77, 5
+    out = torch.empty(B * T, D, device=cuda, dtype=torch.bfloat16)
+    lse = torch.empty(B * H, T, device=cuda)
+    ops.attn_fwd(qkv, 3 * D, kp, B, H, T, dh, scale, p_drop, seed, salt, out, D, lse, dt=1)
+    # torch reference
+    x = qkv.float().view(B, T, 3, H, dh)
+    q = x[:, :, 0].permute(0, 2, 1, 3).clone().requires_grad_(True)
+    k = x[:, :, 1].permute(0, 2, 1, 3).clone().requires_grad_(True)
+    v = x[:, :, 2].permute(0, 2, 1, 3).clone().requires_grad_(True)
+    pad = kp.bool()
+    b2 = [(b * H + h) % B for b in range(B) for h in range(H)]
+    mask = (pad.repeat_interleave(H, 0) | pad[b2]).view(B, H, 1, T)
+    s = (q @ k.transpose(-1, -2)) * scale
+    P = torch.softmax(s.masked_fill(mask, float("-inf")), -1)
+    if p_drop > 0:
+        idx = np.arange(B * H * T * T, dtype=np.uint64)
+        keep = torch.from_numpy(_keep_np(seed, salt, idx, p_drop).reshape(B, H, T, T)).to(cuda)
+        P = P * keep / (1 - p_drop)
+    o = P @ v
+    ref = o.permute(0, 2, 1, 3).reshape(B * T, D)
+    assert rel(out, ref) < 2e-2
+    dout = torch.randn(B * T, D, device=cuda).to(torch.bfloat16)
+    ref.backward(dout.float())
+    dqkv = torch.full((B * T, 3 * D), float("nan"), device=cuda, dtype=torch.bfloat16)
+    ws = torch.empty(int(ops.attn_ws(B, H, T)), device=cuda)
+    ops.attn_bwd(qkv, 3 * D, kp, out, D, dout, D, lse, B, H, T, dh, scale, p_drop, seed, salt,
+                 dqkv, 3 * D, dt=1, ws=ws)
+    for i, t in enumerate((q, k, v)):
+        r = t.grad.permute(0, 2, 1, 3).reshape(B * T, D)
+        assert rel(dqkv[:, i * D:(i + 1) * D], r) < 3e-2, i
