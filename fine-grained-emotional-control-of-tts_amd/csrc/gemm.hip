@@ -45,6 +45,7 @@ struct GemmP {
   const float* row_scale_post;
   int accumulate; int split_k; int k_per_split;
   long split_stride;  // >0: split z stores its partial to C + z*split_stride (no atomics)
+  int g4_flags;       // gemm256 A/B switches (FS2_G4_FLAGS): 1 no stagger, 2 no setprio
   int batch_div;
   long sA1, sA2, sB1, sB2, sC1, sC2, sR1, sR2;
   int tiles_m, tiles_n;
@@ -650,6 +651,81 @@ __device__ __forceinline__ void glds_k_piece(char* lds, const char* base, long l
   glds16(src, lds + piece * 1024);
 }
 
+// Epilogue of a 256-row x 128-column fp32 tile staged in LDS (cs[row][col ^ swz], 512 threads):
+// vector pass (bias, ReLU, gate, row scales, residual, 16-byte stores), or the scalar pass for
+// weight gradients (column remap, split-K atomics).
+__device__ __forceinline__ void epilogue_256x128(const GemmP& p, const float* cs, int m0, int n0,
+                                                 char* Cb, const char* Rb, int tid) {
+  if (!p.vec_ok) {  // weight gradients: fp32, conv column remap n=(j,c) -> c*KW + j, atomics
+    const int cc = p.c_conv_kw > 0 ? p.N / p.c_conv_kw : 0;
+    const bool atomic = p.split_k > 1 && p.split_stride == 0;
+    float* Cf = (float*)Cb;
+    for (int idx = tid; idx < BBM * 128; idx += BNT) {
+      const int row = idx >> 7, col = idx & 127;
+      const int m = m0 + row, n = n0 + col;
+      if (m >= p.mvalid || n >= p.nvalid) continue;
+      float v = cs[row * 128 + (col ^ (((row >> 2) & 1) << 4))];
+      long c2 = n;
+      if (cc > 0) { const int jj = n / cc; c2 = (long)(n - jj * cc) * p.c_conv_kw + jj; }
+      const long off = (long)m * p.ldc + c2;
+      if (atomic) atomicAdd(Cf + off, v);
+      else if (p.accumulate) Cf[off] += v;
+      else Cf[off] = v;
+    }
+    return;
+  }
+  const int c8 = (tid & 15) * 8;
+  const int n = n0 + c8;
+#pragma unroll 2
+  for (int pass = 0; pass < 8; ++pass) {
+    const int row = (tid >> 4) + 32 * pass;
+    const int m = m0 + row;
+    if (m >= p.mvalid || n >= p.nvalid) continue;
+    const int sw = ((row >> 2) & 1) << 4;
+    const f32x4 lo = *(const f32x4*)&cs[row * 128 + (c8 ^ sw)];
+    const f32x4 hi = *(const f32x4*)&cs[row * 128 + ((c8 + 4) ^ sw)];
+    float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    const int nn = min(8, p.nvalid - n);
+    const float rs = p.row_scale ? p.row_scale[m] : 1.f;
+    const float rs2 = p.row_scale_post ? p.row_scale_post[m] : 1.f;
+    if (p.bias) {
+      if (nn == 8) {
+        const f32x4 b0 = *(const f32x4*)(p.bias + n), b1 = *(const f32x4*)(p.bias + n + 4);
+        v[0] += b0[0]; v[1] += b0[1]; v[2] += b0[2]; v[3] += b0[3];
+        v[4] += b1[0]; v[5] += b1[1]; v[6] += b1[2]; v[7] += b1[3];
+      } else {
+        for (int e = 0; e < nn; ++e) v[e] += p.bias[n + e];
+      }
+    }
+    float g[8], rr[8];
+    if (p.gate) load8<bf16>(g, (const bf16*)p.gate + (long)m * p.ldg + n, nn);
+    if (Rb) load8<bf16>(rr, (const bf16*)Rb + (long)m * p.ldr + n, nn);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float x = v[e];
+      if (p.relu) x = fmaxf(x, 0.f);
+      if (p.gate) x = (g[e] > 0.f) ? x : 0.f;
+      x *= rs;
+      if (Rb) x += rr[e];
+      v[e] = x * rs2;
+    }
+    const long off = (long)m * p.ldc + n;
+    if (p.c_fp32) {
+      float* Cf = (float*)Cb + off;
+      if (nn == 8) {
+        f32x4 o0 = {v[0], v[1], v[2], v[3]}, o1 = {v[4], v[5], v[6], v[7]};
+        if (p.accumulate) { o0 += *(const f32x4*)Cf; o1 += *(const f32x4*)(Cf + 4); }
+        *(f32x4*)Cf = o0;
+        *(f32x4*)(Cf + 4) = o1;
+      } else {
+        for (int e = 0; e < nn; ++e) Cf[e] = p.accumulate ? Cf[e] + v[e] : v[e];
+      }
+    } else {
+      store8<bf16>((bf16*)Cb + off, v, nn);
+    }
+  }
+}
+
 template <bool AK, bool BKM>
 __global__ void __launch_bounds__(BNT) gemm_big_kernel(GemmP p) {
   __shared__ __attribute__((aligned(16))) char smem[BIG_LDS];
@@ -854,73 +930,271 @@ __global__ void __launch_bounds__(BNT) gemm_big_kernel(GemmP p) {
         cs[row * 128 + (col ^ (((row >> 2) & 1) << 4))] = acc[i][j][r];
       }
   __syncthreads();
-  if (!p.vec_ok) {  // weight gradients: fp32, conv column remap n=(j,c) -> c*KW + j, atomics
-    const int cc = p.c_conv_kw > 0 ? p.N / p.c_conv_kw : 0;
-    const bool atomic = p.split_k > 1 && p.split_stride == 0;
-    float* Cf = (float*)Cb;
-    for (int idx = tid; idx < BBM * 128; idx += BNT) {
-      const int row = idx >> 7, col = idx & 127;
-      const int m = m0 + row, n = n0 + col;
-      if (m >= p.mvalid || n >= p.nvalid) continue;
-      float v = cs[row * 128 + (col ^ (((row >> 2) & 1) << 4))];
-      long c2 = n;
-      if (cc > 0) { const int jj = n / cc; c2 = (long)(n - jj * cc) * p.c_conv_kw + jj; }
-      const long off = (long)m * p.ldc + c2;
-      if (atomic) atomicAdd(Cf + off, v);
-      else if (p.accumulate) Cf[off] += v;
-      else Cf[off] = v;
-    }
-    return;
+  epilogue_256x128(p, cs, m0, n0, Cb, Rb, tid);
+}
+
+// ---------------------------------------------------------------------------------------------
+// 256x256 tile, BK = 64, 8 waves as 2 (M) x 4 (N), 128x64 outputs per wave (acc 8x4 fragments).
+// Phased main loop after the CDNA4 256^2 template (cdna_hip_programming.md section 5): a K-tile
+// is 4 phases; phase p = (k-half s = p>>1, m-half mq = p&1) runs one 64x64 quadrant x K=32
+// = 16 MFMAs per wave.  LDS holds two K-tile slots of four 16 KiB regions
+// [A k0 | B k0 | A k1 | B k1] (K-major: 256 rows x 64 B; MN-major: 32 k-rows x 512 B).
+// Each phase: ds_read its fragments, issue ONE region of the next K-tile (2 LDS-DMA pieces per
+// wave, region p), barrier, MFMAs at raised priority, barrier.  Region p of tile t+1 is written
+// >= 3 phases after that slot region's last read of tile t-1 and waited for (counted vmcnt(4),
+// never 0 in the loop) >= 3 phases after issue.  Waves 4-7 run half a phase behind (one extra
+// barrier) so each SIMD pairs one wave's MFMA cluster with its partner's reads and DMA issue;
+// they retire their DMA at the end of their memory section, the first group at the end of its
+// MFMA section -- both before the barrier instance that precedes the first read of the data.
+constexpr int G4_NT = 512;
+constexpr int G4_REG = 16384;
+constexpr int G4_SLOT = 4 * G4_REG;
+constexpr int G4_LDS = 2 * G4_SLOT;   // 128 KiB; also holds the 256x128 fp32 epilogue half-tile
+
+// 16-byte chunk swizzle of the 64-byte-row K-major region: conflict-free ds_read_b128 for
+// 16 consecutive rows x chunk (lane >> 4)
+__device__ __forceinline__ int g4_fsw(int row) { return (0x78 >> (2 * ((row >> 2) & 3))) & 3; }
+
+__device__ __forceinline__ bf16x8 g4_frag_k(const char* rg, int row, int g) {
+  return *(const bf16x8*)(rg + row * 64 + ((g ^ g4_fsw(row)) << 4));
+}
+
+template <bool AK, bool BKM>
+__global__ void __launch_bounds__(G4_NT, 1) gemm256_kernel(GemmP p) {
+  __shared__ __attribute__((aligned(16))) char smem[G4_LDS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int nwg = p.tiles_m * p.tiles_n;
+  const int orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int tm = bid / p.tiles_n, tn = bid - tm * p.tiles_n;
+  const int m0 = tm * 256, n0 = tn * 256;
+  const int z = p.split_k > 1 ? 0 : blockIdx.z;
+  const long zb = z / p.batch_div, zh = z - zb * p.batch_div;
+  const char* Ab = p.A + (zb * p.sA1 + zh * p.sA2) * 2;
+  const char* Bb = p.B + (zb * p.sB1 + zh * p.sB2) * 2;
+  const int K = p.K;
+  const int kva = min(K, p.kvalid);
+  const int amode = (p.conv_mode == 1 || p.conv_mode == 4) ? p.conv_mode : 0;
+  const int nk_all = (K + 63) / 64;
+  int kt0 = 0, kt1 = nk_all;
+  if (p.split_k > 1) {
+    const int kps = (nk_all + p.split_k - 1) / p.split_k;
+    kt0 = blockIdx.z * kps;
+    kt1 = min(nk_all, kt0 + kps);
   }
-  const int c8 = (tid & 15) * 8;
-  const int n = n0 + c8;
-#pragma unroll 2
-  for (int pass = 0; pass < 8; ++pass) {
-    const int row = (tid >> 4) + 32 * pass;
-    const int m = m0 + row;
-    if (m >= p.mvalid || n >= p.nvalid) continue;
-    const int sw = ((row >> 2) & 1) << 4;
-    const f32x4 lo = *(const f32x4*)&cs[row * 128 + (c8 ^ sw)];
-    const f32x4 hi = *(const f32x4*)&cs[row * 128 + ((c8 + 4) ^ sw)];
-    float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    const int nn = min(8, p.nvalid - n);
-    const float rs = p.row_scale ? p.row_scale[m] : 1.f;
-    const float rs2 = p.row_scale_post ? p.row_scale_post[m] : 1.f;
-    if (p.bias) {
-      if (nn == 8) {
-        const f32x4 b0 = *(const f32x4*)(p.bias + n), b1 = *(const f32x4*)(p.bias + n + 4);
-        v[0] += b0[0]; v[1] += b0[1]; v[2] += b0[2]; v[3] += b0[3];
-        v[4] += b1[0]; v[5] += b1[1]; v[6] += b1[2]; v[7] += b1[3];
-      } else {
-        for (int e = 0; e < nn; ++e) v[e] += p.bias[n + e];
-      }
-    }
-    float g[8], rr[8];
-    if (p.gate) load8<bf16>(g, (const bf16*)p.gate + (long)m * p.ldg + n, nn);
-    if (Rb) load8<bf16>(rr, (const bf16*)Rb + (long)m * p.ldr + n, nn);
+  const bool bconv3 = p.conv_mode == 3;
+  const bool tap_uniform = amode && (p.conv_c % 32) == 0;  // a 32-wide region sits in one tap
+  const int rpu = amode == 4 ? p.conv_t + 2 * p.conv_p : p.conv_t;
+  const char* zero = g_fs2_zero;
+  const bool zsrc = p.g4_flags & 16;    // timing: every DMA reads the zero line
+
+  // ---- per-lane source state of this wave's two pieces of an A region and of a B region ----
+  const char* arow[2];
+  int abt[2], at[2], ac[2];
+  bool aval[2];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      float x = v[e];
-      if (p.relu) x = fmaxf(x, 0.f);
-      if (p.gate) x = (g[e] > 0.f) ? x : 0.f;
-      x *= rs;
-      if (Rb) x += rr[e];
-      v[e] = x * rs2;
+  for (int i = 0; i < 2; ++i) {
+    const int piece = wave * 2 + i;
+    if constexpr (AK) {  // 16 rows x 64 B per piece
+      const int r = piece * 16 + (lane >> 2);
+      ac[i] = (lane & 3) ^ g4_fsw(r);
+      const int row = m0 + r;
+      aval[i] = row < p.M;
+      const int rr = aval[i] ? row : 0;
+      const int b = amode ? rr / rpu : 0;
+      abt[i] = b * p.conv_t;
+      at[i] = rr - b * rpu;
+      arow[i] = Ab + (long)rr * p.lda * 2;
+    } else {             // 2 k-rows x 512 B per piece
+      const int kr = piece * 2 + (lane >> 5);
+      ac[i] = (lane & 31) ^ mn_swz<bf16>(kr);
+      at[i] = kr;
+      const int mn = m0 + ac[i] * 8;
+      aval[i] = mn < p.M;
+      arow[i] = Ab + (long)(aval[i] ? mn : 0) * 2;
+      abt[i] = 0;
     }
-    const long off = (long)m * p.ldc + n;
-    if (p.c_fp32) {
-      float* Cf = (float*)Cb + off;
-      if (nn == 8) {
-        f32x4 o0 = {v[0], v[1], v[2], v[3]}, o1 = {v[4], v[5], v[6], v[7]};
-        if (p.accumulate) { o0 += *(const f32x4*)Cf; o1 += *(const f32x4*)(Cf + 4); }
-        *(f32x4*)Cf = o0;
-        *(f32x4*)(Cf + 4) = o1;
-      } else {
-        for (int e = 0; e < nn; ++e) Cf[e] = p.accumulate ? Cf[e] + v[e] : v[e];
+  }
+  const char* brow[2];
+  int bc[2], bkr[2];
+  bool bval[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int piece = wave * 2 + i;
+    if constexpr (BKM) {
+      const int r = piece * 16 + (lane >> 2);
+      bc[i] = (lane & 3) ^ g4_fsw(r);
+      const int row = n0 + r;
+      bval[i] = row < p.N;
+      brow[i] = Bb + (long)(bval[i] ? row : 0) * p.ldb * 2;
+      bkr[i] = 0;
+    } else {
+      const int kr = piece * 2 + (lane >> 5);
+      const int lc = (lane & 31) ^ mn_swz<bf16>(kr);
+      bkr[i] = kr;
+      const int mn = n0 + lc * 8;
+      bval[i] = mn < p.N;
+      int col = mn;
+      bc[i] = 0;
+      if (bconv3 && bval[i]) { const int j = mn / p.conv_c; col = mn - j * p.conv_c; bc[i] = j; }
+      brow[i] = Bb + (long)(bval[i] ? col : 0) * 2;
+    }
+  }
+
+  // region reg (0: A k0, 1: B k0, 2: A k1, 3: B k1) of relative K-tile it -> slot it & 1
+  auto issue = [&](int it, int reg) {
+    const int kh = reg >> 1;
+    const int k0 = (kt0 + it) * 64 + kh * 32;
+    char* dst = smem + (it & 1) * G4_SLOT + reg * G4_REG;
+    if ((reg & 1) == 0) {
+      int jt = 0, c0 = 0;
+      if (tap_uniform) { jt = k0 / p.conv_c; c0 = k0 - jt * p.conv_c; }
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const char* src;
+        if constexpr (AK) {
+          const int k = k0 + ac[i] * 8;
+          bool ok = aval[i] && k < K;
+          if (!amode) {
+            src = arow[i] + (long)k * 2;
+          } else {
+            int j, c;
+            if (tap_uniform) { j = jt; c = c0 + ac[i] * 8; }
+            else { j = k / p.conv_c; c = k - j * p.conv_c; }
+            int ts;
+            if (amode == 1) {
+              ts = reflect_idx(at[i] + j - p.conv_p, p.conv_t);
+            } else {
+              ts = at[i] - j;
+              ok = ok && ts >= 0 && ts < p.conv_t;
+              ts = ok ? ts : 0;
+            }
+            src = Ab + ((long)(abt[i] + ts) * p.lda + c) * 2;
+          }
+          src = ok ? src : zero;
+        } else {
+          const int k = k0 + at[i];
+          const bool ok = aval[i] && k < kva;
+          src = ok ? arow[i] + (long)k * p.lda * 2 : zero;
+        }
+        glds16(zsrc ? zero : src, dst + (wave * 2 + i) * 1024);
       }
     } else {
-      store8<bf16>((bf16*)Cb + off, v, nn);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const char* src;
+        if constexpr (BKM) {
+          const int k = k0 + bc[i] * 8;
+          src = (bval[i] && k < K) ? brow[i] + (long)k * 2 : zero;
+        } else {
+          const int k = k0 + bkr[i];
+          const bool ok = bval[i] && k < kva;
+          long srow = k;
+          if (bconv3) {
+            const int b = k / p.conv_t, t = k - b * p.conv_t;
+            srow = (long)b * p.conv_t + reflect_idx(t + bc[i] - p.conv_p, p.conv_t);
+          }
+          src = ok ? brow[i] + srow * p.ldb * 2 : zero;
+        }
+        glds16(zsrc ? zero : src, dst + (wave * 2 + i) * 1024);
+      }
     }
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = kt1 - kt0;
+  if (nk > 0) {
+    issue(0, 0); issue(0, 1); issue(0, 2); issue(0, 3);
+  }
+  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // k0 regions of the first tile
+  __builtin_amdgcn_s_barrier();
+  const bool stag = !(p.g4_flags & 1);
+  const bool prio = !(p.g4_flags & 2);
+  const bool nowait = p.g4_flags & 4;   // timing experiments only (wrong results)
+  const bool noissue = p.g4_flags & 8;
+  // stagger: waves 4-7 half a phase behind; without it both groups retire DMA like group 1
+  const int grp = stag ? wr : 1;
+  if (stag && wr == 1) __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+
+  bf16x8 af[4], bfr[4];
+  for (int it = 0; it < nk; ++it) {
+    const bool more = it + 1 < nk;
+#pragma unroll
+    for (int ph = 0; ph < 4; ++ph) {
+      const int s = ph >> 1, mq = ph & 1;
+      const char* rA = smem + (it & 1) * G4_SLOT + (2 * s) * G4_REG;
+      const char* rB = rA + G4_REG;
+      // ---- memory section: fragments of this phase, then one region of the next tile ----
+      if (mq == 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          bfr[j] = BKM ? g4_frag_k(rB, wc * 64 + j * 16 + (lane & 15), lane >> 4)
+                       : frag_bf16_mnmajor512(rB, wc * 64 + j * 16, 0, lane);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        af[i] = AK ? g4_frag_k(rA, wr * 128 + mq * 64 + i * 16 + (lane & 15), lane >> 4)
+                   : frag_bf16_mnmajor512(rA, wr * 128 + mq * 64 + i * 16, 0, lane);
+      if (more && !noissue) issue(it + 1, ph);
+      if (grp == 1 && (ph & 1) && !nowait && !noissue) {
+        if (more) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      // ---- matrix section: one 64x64 quadrant x K=32 ----
+      if (prio) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[mq * 4 + i][j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[mq * 4 + i][j], 0, 0, 0);
+      if (prio) __builtin_amdgcn_s_setprio(0);
+      if (grp == 0 && (ph & 1) && !nowait && !noissue) {
+        if (more) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  if (stag && wr == 0) __builtin_amdgcn_s_barrier();  // balance the stagger
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // ---- epilogue: two 256x128 column halves through LDS ----
+  char* Cb = p.C + (zb * p.sC1 + zh * p.sC2) * (p.c_fp32 ? 4 : 2);
+  if (p.split_stride > 0 && p.split_k > 1) Cb += (long)blockIdx.z * p.split_stride * 4;
+  const char* Rb = p.residual ? p.residual + (zb * p.sR1 + zh * p.sR2) * 2 : nullptr;
+  float* cs = (float*)smem;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if ((wc >> 1) == h) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = wr * 128 + i * 16 + (lane >> 4) * 4 + r;
+            const int col = (wc & 1) * 64 + j * 16 + (lane & 15);
+            cs[row * 128 + (col ^ (((row >> 2) & 1) << 4))] = acc[i][j][r];
+          }
+    }
+    __syncthreads();
+    if (n0 + h * 128 < p.nvalid) epilogue_256x128(p, cs, m0, n0 + h * 128, Cb, Rb, tid);
+    __syncthreads();
   }
 }
 
@@ -952,6 +1226,42 @@ int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
       split_big = max(1, min((480 + tiles_big - 1) / tiles_big, nk / 8));
     }
     const bool slices = p.split_stride > 0 && p.split_k > 1;  // caller-chosen split, plain stores
+    // 256x256 phased kernel: wide outputs (<= 15 % column padding)
+    static const bool no256 = getenv_flag("FS2_GEMM_NO256");
+    const int tm256 = (p.M + 255) / 256, tn256 = (p.N + 255) / 256;
+    const int tiles256 = tm256 * tn256;
+    const bool wide = p.N >= 512 && tn256 * 256 * 100 <= p.N * 115;
+    int split256 = 1;
+    if (wgrad) {
+      const int nk = (p.K + 63) / 64;
+      split256 = max(1, min((240 + tiles256 - 1) / tiles256, nk / 8));
+    }
+    const bool use256 = !no256 && wide && p.conv_mode != 2 &&
+                        ((p.vec_ok && p.split_k <= 1 && tiles256 * batch >= 200) ||
+                         (slices && p.vec_ok && tiles256 * p.split_k >= 160) ||
+                         (wgrad && tiles256 * split256 >= 160));
+    if (use256) {
+      GemmP q = p;
+      static const int g4f = [] { const char* v = std::getenv("FS2_G4_FLAGS"); return v ? std::atoi(v) : 0; }();
+      q.g4_flags = g4f;
+      q.tiles_m = tm256;
+      q.tiles_n = tn256;
+      int gz2 = slices ? p.split_k : gz;
+      if (wgrad) {
+        q.k_per_split = ((p.K + split256 - 1) / split256 + 63) / 64 * 64;
+        q.split_k = (p.K + q.k_per_split - 1) / q.k_per_split;
+        q.vec_ok = q.split_k == 1;
+        q.accumulate = 1;
+        gz2 = q.split_k;
+      }
+      dim3 g2(tiles256, 1, gz2);
+      if (ak && bk) hipLaunchKernelGGL((gemm256_kernel<true, true>), g2, dim3(G4_NT), 0, s, q);
+      else if (ak && !bk) hipLaunchKernelGGL((gemm256_kernel<true, false>), g2, dim3(G4_NT), 0, s, q);
+      else if (!ak && bk) hipLaunchKernelGGL((gemm256_kernel<false, true>), g2, dim3(G4_NT), 0, s, q);
+      else hipLaunchKernelGGL((gemm256_kernel<false, false>), g2, dim3(G4_NT), 0, s, q);
+      FS2_CHECK_LAUNCH();
+      return 0;
+    }
     const bool use_big = !no_big && p.conv_mode != 2 &&
                          ((p.vec_ok && p.split_k <= 1 && tiles_big * batch >= 240) ||
                           (slices && p.vec_ok && tiles_big * p.split_k >= 160) ||

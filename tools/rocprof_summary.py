@@ -2,6 +2,8 @@
 
     python tools/rocprof_summary.py stats  <dir> <steps> [out.txt]
         per-kernel time per train step from <dir>/**/*kernel_stats.csv
+    python tools/rocprof_summary.py shapes <dir> <steps> [top]
+        per (kernel, grid) time per step from the kernel trace (which GEMM shape costs what)
     python tools/rocprof_summary.py kernel <dir> <kernel-substr> <grid> <min_us>
         average duration of the matching dispatches in <dir>/**/*kernel_trace.csv (cross-check
         of bench.py's live HIP-event timing of the roofline kernel)
@@ -44,6 +46,18 @@ def stats(d, steps, out=None):
     if out:
         open(out, "w").write(txt + "\n")
     print(txt)
+
+
+def shapes(d, steps, top=40):
+    import collections
+    g = collections.defaultdict(list)
+    for f in _find(d, "kernel_trace.csv"):
+        for r in csv.DictReader(open(f)):
+            key = (r["Kernel_Name"][:70], r["Grid_Size_X"], r["Grid_Size_Z"], r["Workgroup_Size_X"])
+            g[key].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    for k, v in sorted(g.items(), key=lambda kv: -sum(kv[1]))[:top]:
+        print(f"{sum(v) / steps / 1e3:7.3f} ms/step {len(v) / steps:5.1f}/step "
+              f"avg {sum(v) / len(v):8.1f} us  grid {k[1]}x{k[2]} wg {k[3]}  {k[0]}")
 
 
 def kernel(d, name_sub, grid, min_us):
@@ -96,6 +110,8 @@ def traffic(fdir, wdir, name_sub, grid, min_us, out=None):
 if __name__ == "__main__":
     if sys.argv[1] == "stats":
         stats(sys.argv[2], int(sys.argv[3]), sys.argv[4] if len(sys.argv) > 4 else None)
+    elif sys.argv[1] == "shapes":
+        shapes(sys.argv[2], int(sys.argv[3]), int(sys.argv[4]) if len(sys.argv) > 4 else 40)
     elif sys.argv[1] == "kernel":
         kernel(sys.argv[2], sys.argv[3], int(sys.argv[4]), float(sys.argv[5]))
     elif sys.argv[1] == "traffic":
