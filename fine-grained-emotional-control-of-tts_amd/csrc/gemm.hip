@@ -759,9 +759,12 @@ __global__ void __launch_bounds__(BNT) gemm_big_kernel(GemmP p) {
   const int rpu = amode == 4 ? p.conv_t + 2 * p.conv_p : p.conv_t;  // rows per utterance
   const char* zero = g_fs2_zero;
 
-  // ---- per-lane, per-piece source state, hoisted out of the K loop ----
-  // A K-major: pieces 4w+i (8 rows each), lane row r = piece*8 + (lane>>3), chunk lc
-  const char* arow[4];
+  // ---- per-lane, per-piece DMA source state, hoisted out of the K loop.  Tiles are issued in
+  // increasing k: pointers advance by wave-uniform offsets and the implicit-conv rows are
+  // re-pointed only when the tap changes.
+  // A K-major: pieces 4w+i (8 rows each), lane row r = piece*8 + (lane>>3), chunk alc
+  const char* ap[4];
+  bool aok[4];
   int abt[4], at[4], alc[4];
   bool aval[4];
 #pragma unroll
@@ -775,19 +778,21 @@ __global__ void __launch_bounds__(BNT) gemm_big_kernel(GemmP p) {
       const int b = amode ? rr / rpu : 0;
       abt[i] = b * p.conv_t;       // source row base (unpadded utterance)
       at[i] = rr - b * rpu;        // position inside the (padded) utterance
-      arow[i] = Ab + (long)rr * p.lda * 2;
+      ap[i] = Ab + ((long)rr * p.lda + alc[i] * 8) * 2;
     } else {  // MN-major (512-byte k-rows): piece = 2 k-rows
       const int kr = (wave * 4 + i) * 2 + (lane >> 5);
       alc[i] = (lane & 31) ^ mn_swz<bf16>(kr);
       at[i] = kr;
       const int mn = m0 + alc[i] * 8;
       aval[i] = mn < p.M;
-      arow[i] = Ab + (long)(aval[i] ? mn : 0) * 2;
+      ap[i] = Ab + ((long)(aval[i] ? mn : 0) + (long)kr * p.lda) * 2;
       abt[i] = 0;
     }
+    aok[i] = aval[i];
   }
-  const char* brow[2];
-  int blc[2], bkr[2];
+  int a_tap = -1;
+  const char* bp[2];
+  int blc[2], bkr[2], bb[2], bt[2];
   bool bval[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
@@ -796,8 +801,8 @@ __global__ void __launch_bounds__(BNT) gemm_big_kernel(GemmP p) {
       blc[i] = (lane & 7) ^ (r & 7);
       const int row = n0 + r;
       bval[i] = row < p.N;
-      brow[i] = Bb + (long)(bval[i] ? row : 0) * p.ldb * 2;
-      bkr[i] = 0;
+      bp[i] = Bb + ((long)(bval[i] ? row : 0) * p.ldb + blc[i] * 8) * 2;
+      bkr[i] = 0; bb[i] = 0; bt[i] = 0;
     } else {  // MN-major (256-byte k-rows): piece = 4 k-rows
       const int kr = (wave * 2 + i) * 4 + (lane >> 4);
       blc[i] = (lane & 15) ^ mn_swz<bf16>(kr);
@@ -807,28 +812,57 @@ __global__ void __launch_bounds__(BNT) gemm_big_kernel(GemmP p) {
       int col = mn;
       if (bconv3 && bval[i]) { const int j = mn / p.conv_c; col = mn - j * p.conv_c; blc[i] = j; }
       else if (bconv3) blc[i] = 0;
-      brow[i] = Bb + (long)(bval[i] ? col : 0) * 2;
+      bp[i] = Bb + ((long)(bval[i] ? col : 0) + (bconv3 ? 0L : (long)kr * p.ldb)) * 2;
+      const int k = kt0 * 64 + kr;
+      bb[i] = bconv3 ? k / p.conv_t : 0;
+      bt[i] = bconv3 ? k - bb[i] * p.conv_t : 0;
     }
   }
+  int b_k = kt0 * 64;
 
-  auto issue = [&](int kt, int stage) {   // 6 LDS-DMA pieces per wave, branch-free sources
+  auto issue = [&](int kt, int stage) {   // 6 LDS-DMA pieces per wave
     const int k0 = kt * 64;
     char* la = smem + stage * BIG_STAGE;
     char* lb = la + BIG_A;
-    int jt = 0, c0 = 0;
-    if (tap_uniform) { jt = k0 / p.conv_c; c0 = k0 - jt * p.conv_c; }
+    if constexpr (AK) {
+      if (amode && tap_uniform) {
+        const int j = k0 / p.conv_c, c0 = k0 - j * p.conv_c;   // wave-uniform
+        if (j != a_tap) {
+          a_tap = j;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const char* src;
-      if constexpr (AK) {
-        const int k = k0 + alc[i] * 8;
-        bool ok = aval[i] && k < K;
-        if (!amode) {
-          src = arow[i] + (long)k * 2;
-        } else {
-          int j, c;
-          if (tap_uniform) { j = jt; c = c0 + alc[i] * 8; }
-          else { j = k / p.conv_c; c = k - j * p.conv_c; }
+          for (int i = 0; i < 4; ++i) {
+            int ts;
+            bool ok = aval[i];
+            if (amode == 1) {
+              ts = reflect_idx(at[i] + j - p.conv_p, p.conv_t);
+            } else {
+              ts = at[i] - j;
+              ok = ok && ts >= 0 && ts < p.conv_t;
+              ts = ok ? ts : 0;
+            }
+            ap[i] = Ab + ((long)(abt[i] + ts) * p.lda + alc[i] * 8) * 2;
+            aok[i] = ok;
+          }
+        }
+        const bool kin = k0 + 64 <= K;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const bool ok = aok[i] && (kin || k0 + alc[i] * 8 < K);
+          glds16(ok ? ap[i] + (long)c0 * 2 : zero, la + (wave * 4 + i) * 1024);
+        }
+      } else if (!amode) {
+        const bool kin = k0 + 64 <= K;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const bool ok = aok[i] && (kin || k0 + alc[i] * 8 < K);
+          glds16(ok ? ap[i] + (long)k0 * 2 : zero, la + (wave * 4 + i) * 1024);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int k = k0 + alc[i] * 8;
+          bool ok = aval[i] && k < K;
+          const int j = k / p.conv_c, c = k - j * p.conv_c;
           int ts;
           if (amode == 1) {
             ts = reflect_idx(at[i] + j - p.conv_p, p.conv_t);
@@ -837,33 +871,46 @@ __global__ void __launch_bounds__(BNT) gemm_big_kernel(GemmP p) {
             ok = ok && ts >= 0 && ts < p.conv_t;
             ts = ok ? ts : 0;
           }
-          src = Ab + ((long)(abt[i] + ts) * p.lda + c) * 2;
+          const char* src = Ab + ((long)(abt[i] + ts) * p.lda + c) * 2;
+          glds16(ok ? src : zero, la + (wave * 4 + i) * 1024);
         }
-        src = ok ? src : zero;
-      } else {
-        const int k = k0 + at[i];
-        const bool ok = aval[i] && k < kva;
-        src = ok ? arow[i] + (long)k * p.lda * 2 : zero;
       }
-      glds16(src, la + (wave * 4 + i) * 1024);
-    }
+    } else {
+      const bool kin = k0 + 64 <= kva;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const char* src;
-      if constexpr (BKM) {
-        const int k = k0 + blc[i] * 8;
-        src = (bval[i] && k < K) ? brow[i] + (long)k * 2 : zero;
-      } else {
-        const int k = k0 + bkr[i];
-        const bool ok = bval[i] && k < kva;
-        long srow = k;
-        if (bconv3) {
-          const int b = k / p.conv_t, t = k - b * p.conv_t;
-          srow = (long)b * p.conv_t + reflect_idx(t + blc[i] - p.conv_p, p.conv_t);
-        }
-        src = ok ? brow[i] + srow * p.ldb * 2 : zero;
+      for (int i = 0; i < 4; ++i) {
+        const bool ok = aok[i] && (kin || k0 + at[i] < kva);
+        glds16(ok ? ap[i] + (long)k0 * p.lda * 2 : zero, la + (wave * 4 + i) * 1024);
       }
-      glds16(src, lb + (wave * 2 + i) * 1024);
+    }
+    if constexpr (BKM) {
+      const bool kin = k0 + 64 <= K;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const bool ok = bval[i] && (kin || k0 + blc[i] * 8 < K);
+        glds16(ok ? bp[i] + (long)k0 * 2 : zero, lb + (wave * 2 + i) * 1024);
+      }
+    } else if (!bconv3) {
+      const bool kin = k0 + 64 <= kva;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const bool ok = bval[i] && (kin || k0 + bkr[i] < kva);
+        glds16(ok ? bp[i] + (long)k0 * p.ldb * 2 : zero, lb + (wave * 2 + i) * 1024);
+      }
+    } else {
+      const int dk = k0 - b_k;
+      b_k = k0;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        int t = bt[i] + dk, b = bb[i];
+        while (t >= p.conv_t) { t -= p.conv_t; ++b; }
+        bt[i] = t; bb[i] = b;
+        int ts = t + blc[i] - p.conv_p;
+        ts = ts < 0 ? -ts : (ts >= p.conv_t ? 2 * (p.conv_t - 1) - ts : ts);
+        const bool ok = bval[i] && k0 + bkr[i] < kva;
+        glds16(ok ? bp[i] + ((long)b * p.conv_t + ts) * p.ldb * 2 : zero,
+               lb + (wave * 2 + i) * 1024);
+      }
     }
   };
 
@@ -989,11 +1036,13 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256_kernel(GemmP p) {
   const bool tap_uniform = amode && (p.conv_c % 32) == 0;  // a 32-wide region sits in one tap
   const int rpu = amode == 4 ? p.conv_t + 2 * p.conv_p : p.conv_t;
   const char* zero = g_fs2_zero;
-  const bool zsrc = p.g4_flags & 16;    // timing: every DMA reads the zero line
 
-  // ---- per-lane source state of this wave's two pieces of an A region and of a B region ----
-  const char* arow[2];
-  int abt[2], at[2], ac[2];
+  // ---- per-lane DMA source state of this wave's two pieces of an A region and of a B region.
+  // Regions are issued in increasing k, so pointers advance by wave-uniform offsets; the
+  // implicit-conv row (reflect / shift by the tap) is recomputed only when the tap changes.
+  const char* ap[2];   // A: element pointer at k = 0 of the current tap (conv) or of the row
+  bool aok[2];
+  int ar[2], abt[2], at[2], ac[2];
   bool aval[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
@@ -1004,23 +1053,28 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256_kernel(GemmP p) {
       const int row = m0 + r;
       aval[i] = row < p.M;
       const int rr = aval[i] ? row : 0;
+      ar[i] = rr;
       const int b = amode ? rr / rpu : 0;
       abt[i] = b * p.conv_t;
       at[i] = rr - b * rpu;
-      arow[i] = Ab + (long)rr * p.lda * 2;
+      ap[i] = Ab + ((long)rr * p.lda + ac[i] * 8) * 2;
+      aok[i] = aval[i];
     } else {             // 2 k-rows x 512 B per piece
       const int kr = piece * 2 + (lane >> 5);
       ac[i] = (lane & 31) ^ mn_swz<bf16>(kr);
       at[i] = kr;
       const int mn = m0 + ac[i] * 8;
       aval[i] = mn < p.M;
-      arow[i] = Ab + (long)(aval[i] ? mn : 0) * 2;
-      abt[i] = 0;
+      ap[i] = Ab + ((long)(aval[i] ? mn : 0) + (long)kr * p.lda) * 2;
+      aok[i] = aval[i];
+      ar[i] = 0; abt[i] = 0;
     }
   }
-  const char* brow[2];
-  int bc[2], bkr[2];
+  int a_tap = -1;      // tap whose rows ap[] point at (implicit conv)
+  const char* bp[2];
+  int bc[2], bkr[2], bb[2], bt[2];
   bool bval[2];
+  int b_k = 0;         // k of the last B region issued (conv3 incremental (b, t))
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int piece = wave * 2 + i;
@@ -1029,8 +1083,8 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256_kernel(GemmP p) {
       bc[i] = (lane & 3) ^ g4_fsw(r);
       const int row = n0 + r;
       bval[i] = row < p.N;
-      brow[i] = Bb + (long)(bval[i] ? row : 0) * p.ldb * 2;
-      bkr[i] = 0;
+      bp[i] = Bb + ((long)(bval[i] ? row : 0) * p.ldb + bc[i] * 8) * 2;
+      bkr[i] = 0; bb[i] = 0; bt[i] = 0;
     } else {
       const int kr = piece * 2 + (lane >> 5);
       const int lc = (lane & 31) ^ mn_swz<bf16>(kr);
@@ -1040,31 +1094,23 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256_kernel(GemmP p) {
       int col = mn;
       bc[i] = 0;
       if (bconv3 && bval[i]) { const int j = mn / p.conv_c; col = mn - j * p.conv_c; bc[i] = j; }
-      brow[i] = Bb + (long)(bval[i] ? col : 0) * 2;
+      bp[i] = Bb + ((long)(bval[i] ? col : 0) + (bconv3 ? 0L : (long)kr * p.ldb)) * 2;
+      bb[i] = bconv3 ? kr / p.conv_t : 0;
+      bt[i] = bconv3 ? kr - bb[i] * p.conv_t : 0;
     }
   }
 
-  // region reg (0: A k0, 1: B k0, 2: A k1, 3: B k1) of relative K-tile it -> slot it & 1
-  auto issue = [&](int it, int reg) {
-    const int kh = reg >> 1;
-    const int k0 = (kt0 + it) * 64 + kh * 32;
-    char* dst = smem + (it & 1) * G4_SLOT + reg * G4_REG;
-    if ((reg & 1) == 0) {
-      int jt = 0, c0 = 0;
-      if (tap_uniform) { jt = k0 / p.conv_c; c0 = k0 - jt * p.conv_c; }
+  auto issueA = [&](char* dst, int k0) {
+    if constexpr (AK) {
+      if (amode && tap_uniform) {
+        const int j = k0 / p.conv_c;            // wave-uniform
+        const int c0 = k0 - j * p.conv_c;
+        if (j != a_tap) {                       // new tap: re-point the rows
+          a_tap = j;
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const char* src;
-        if constexpr (AK) {
-          const int k = k0 + ac[i] * 8;
-          bool ok = aval[i] && k < K;
-          if (!amode) {
-            src = arow[i] + (long)k * 2;
-          } else {
-            int j, c;
-            if (tap_uniform) { j = jt; c = c0 + ac[i] * 8; }
-            else { j = k / p.conv_c; c = k - j * p.conv_c; }
+          for (int i = 0; i < 2; ++i) {
             int ts;
+            bool ok = aval[i];
             if (amode == 1) {
               ts = reflect_idx(at[i] + j - p.conv_p, p.conv_t);
             } else {
@@ -1072,37 +1118,100 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256_kernel(GemmP p) {
               ok = ok && ts >= 0 && ts < p.conv_t;
               ts = ok ? ts : 0;
             }
-            src = Ab + ((long)(abt[i] + ts) * p.lda + c) * 2;
+            ap[i] = Ab + ((long)(abt[i] + ts) * p.lda + ac[i] * 8) * 2;
+            aok[i] = ok;
           }
-          src = ok ? src : zero;
-        } else {
-          const int k = k0 + at[i];
-          const bool ok = aval[i] && k < kva;
-          src = ok ? arow[i] + (long)k * p.lda * 2 : zero;
         }
-        glds16(zsrc ? zero : src, dst + (wave * 2 + i) * 1024);
+        const bool kin = k0 + 32 <= K;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const bool ok = aok[i] && (kin || k0 + ac[i] * 8 < K);
+          glds16(ok ? ap[i] + (long)c0 * 2 : zero, dst + (wave * 2 + i) * 1024);
+        }
+      } else if (!amode) {
+        const bool kin = k0 + 32 <= K;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const bool ok = aok[i] && (kin || k0 + ac[i] * 8 < K);
+          glds16(ok ? ap[i] + (long)k0 * 2 : zero, dst + (wave * 2 + i) * 1024);
+        }
+      } else {                                  // conv with taps straddling 8-chunks' regions
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int k = k0 + ac[i] * 8;
+          bool ok = aval[i] && k < K;
+          const int j = k / p.conv_c, c = k - j * p.conv_c;
+          int ts;
+          if (amode == 1) {
+            ts = reflect_idx(at[i] + j - p.conv_p, p.conv_t);
+          } else {
+            ts = at[i] - j;
+            ok = ok && ts >= 0 && ts < p.conv_t;
+            ts = ok ? ts : 0;
+          }
+          const char* src = Ab + ((long)(abt[i] + ts) * p.lda + c) * 2;
+          glds16(ok ? src : zero, dst + (wave * 2 + i) * 1024);
+        }
       }
     } else {
+      const bool kin = k0 + 32 <= kva;
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const char* src;
-        if constexpr (BKM) {
-          const int k = k0 + bc[i] * 8;
-          src = (bval[i] && k < K) ? brow[i] + (long)k * 2 : zero;
-        } else {
-          const int k = k0 + bkr[i];
-          const bool ok = bval[i] && k < kva;
-          long srow = k;
-          if (bconv3) {
-            const int b = k / p.conv_t, t = k - b * p.conv_t;
-            srow = (long)b * p.conv_t + reflect_idx(t + bc[i] - p.conv_p, p.conv_t);
-          }
-          src = ok ? brow[i] + srow * p.ldb * 2 : zero;
-        }
-        glds16(zsrc ? zero : src, dst + (wave * 2 + i) * 1024);
+        const bool ok = aok[i] && (kin || k0 + at[i] < kva);
+        glds16(ok ? ap[i] + (long)k0 * p.lda * 2 : zero, dst + (wave * 2 + i) * 1024);
       }
     }
   };
+  auto issueB = [&](char* dst, int k0) {
+    if constexpr (BKM) {
+      const bool kin = k0 + 32 <= K;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const bool ok = bval[i] && (kin || k0 + bc[i] * 8 < K);
+        glds16(ok ? bp[i] + (long)k0 * 2 : zero, dst + (wave * 2 + i) * 1024);
+      }
+    } else if (!bconv3) {
+      const bool kin = k0 + 32 <= kva;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const bool ok = bval[i] && (kin || k0 + bkr[i] < kva);
+        glds16(ok ? bp[i] + (long)k0 * p.ldb * 2 : zero, dst + (wave * 2 + i) * 1024);
+      }
+    } else {
+      // k-row k = k0 + bkr = b*T + t, advanced incrementally from the previous region
+      const int dk = k0 - b_k;
+      b_k = k0;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        int t = bt[i] + dk, b = bb[i];
+        while (t >= p.conv_t) { t -= p.conv_t; ++b; }
+        bt[i] = t; bb[i] = b;
+        int ts = t + bc[i] - p.conv_p;
+        ts = ts < 0 ? -ts : (ts >= p.conv_t ? 2 * (p.conv_t - 1) - ts : ts);
+        const bool ok = bval[i] && k0 + bkr[i] < kva;
+        glds16(ok ? bp[i] + ((long)b * p.conv_t + ts) * p.ldb * 2 : zero,
+               dst + (wave * 2 + i) * 1024);
+      }
+    }
+  };
+  // region reg (0: A k0, 1: B k0, 2: A k1, 3: B k1) of relative K-tile it -> slot it & 1
+  auto issue = [&](int it, int reg) {
+    const int k0 = (kt0 + it) * 64 + (reg >> 1) * 32;
+    char* dst = smem + (it & 1) * G4_SLOT + reg * G4_REG;
+    if ((reg & 1) == 0) issueA(dst, k0);
+    else issueB(dst, k0);
+  };
+  if constexpr (!BKM) {
+    if (bconv3) {   // start the incremental (b, t) at the first region of this split
+      b_k = kt0 * 64;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int k = b_k + bkr[i];
+        bb[i] = k / p.conv_t;
+        bt[i] = k - bb[i] * p.conv_t;
+      }
+    }
+  }
 
   f32x4 acc[8][4];
 #pragma unroll
