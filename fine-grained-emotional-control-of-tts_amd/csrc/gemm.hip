@@ -22,6 +22,11 @@
 #include <cstdlib>
 #include <cstring>
 
+typedef __attribute__((ext_vector_type(4))) int i32x4;
+__device__ void llvm_raw_buffer_load_lds(i32x4 rsrc, __attribute__((address_space(3))) uint32_t* lds,
+                                         int size, int voffset, int soffset, int offset,
+                                         int aux) __asm("llvm.amdgcn.raw.buffer.load.lds");
+
 namespace {
 
 // host-side A/B switch for kernel variants (read once)
@@ -203,6 +208,24 @@ typedef __attribute__((address_space(3))) void lptr_t;
 
 __device__ __forceinline__ void glds16(const char* src, char* lds_wave_base) {
   __builtin_amdgcn_global_load_lds((const gptr_t*)src, (lptr_t*)lds_wave_base, 16, 0, 0);
+}
+
+// Buffer-resource form of the LDS-DMA (buffer_load_dwordx4 ... lds): a wave-uniform base in
+// SGPRs, a 32-bit per-lane byte offset and a uniform SGPR offset.  Lanes with the offset
+// BUF_OOB fall outside num_records and load zeros -- no per-lane pointer selects.
+constexpr int BUF_OOB = (int)0x80000000u;
+__device__ __forceinline__ i32x4 make_rsrc(const void* base) {
+  const uint64_t a = (uint64_t)base;
+  i32x4 r;
+  r[0] = __builtin_amdgcn_readfirstlane((int)(a & 0xffffffffu));
+  r[1] = __builtin_amdgcn_readfirstlane((int)(a >> 32));
+  r[2] = 0x7fffffff;
+  r[3] = 0x00020000;
+  return r;
+}
+__device__ __forceinline__ void blds16(i32x4 rsrc, int voff, int soff, char* lds_wave_base) {
+  llvm_raw_buffer_load_lds(rsrc, (__attribute__((address_space(3))) uint32_t*)lds_wave_base, 16,
+                           voff, soff, 0, 0);
 }
 
 // K-major tile (128 rows x 128 B): 16 x 1 KiB pieces, wave w issues pieces 4w..4w+3 (8 rows each)
@@ -1035,14 +1058,14 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256_kernel(GemmP p) {
   const bool bconv3 = p.conv_mode == 3;
   const bool tap_uniform = amode && (p.conv_c % 32) == 0;  // a 32-wide region sits in one tap
   const int rpu = amode == 4 ? p.conv_t + 2 * p.conv_p : p.conv_t;
-  const char* zero = g_fs2_zero;
 
-  // ---- per-lane DMA source state of this wave's two pieces of an A region and of a B region.
-  // Regions are issued in increasing k, so pointers advance by wave-uniform offsets; the
-  // implicit-conv row (reflect / shift by the tap) is recomputed only when the tap changes.
-  const char* ap[2];   // A: element pointer at k = 0 of the current tap (conv) or of the row
-  bool aok[2];
-  int ar[2], abt[2], at[2], ac[2];
+  // ---- per-lane DMA source state of this wave's two pieces of an A region and of a B region:
+  // 32-bit byte offsets from the operand base (BUF_OOB: zero fill), advanced by wave-uniform
+  // offsets as regions are issued in increasing k; the implicit-conv rows are re-pointed only
+  // when the tap changes.
+  const i32x4 rsA = make_rsrc(Ab), rsB = make_rsrc(Bb);
+  int avo[2];          // A: offset at k = 0 of the current tap (conv) or of the row/column
+  int abt[2], at[2], ac[2];
   bool aval[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
@@ -1053,28 +1076,25 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256_kernel(GemmP p) {
       const int row = m0 + r;
       aval[i] = row < p.M;
       const int rr = aval[i] ? row : 0;
-      ar[i] = rr;
       const int b = amode ? rr / rpu : 0;
       abt[i] = b * p.conv_t;
       at[i] = rr - b * rpu;
-      ap[i] = Ab + ((long)rr * p.lda + ac[i] * 8) * 2;
-      aok[i] = aval[i];
+      avo[i] = aval[i] ? (int)(((long)rr * p.lda + ac[i] * 8) * 2) : BUF_OOB;
     } else {             // 2 k-rows x 512 B per piece
       const int kr = piece * 2 + (lane >> 5);
       ac[i] = (lane & 31) ^ mn_swz<bf16>(kr);
       at[i] = kr;
       const int mn = m0 + ac[i] * 8;
       aval[i] = mn < p.M;
-      ap[i] = Ab + ((long)(aval[i] ? mn : 0) + (long)kr * p.lda) * 2;
-      aok[i] = aval[i];
-      ar[i] = 0; abt[i] = 0;
+      avo[i] = aval[i] ? (int)(((long)mn + (long)kr * p.lda) * 2) : BUF_OOB;
+      abt[i] = 0;
     }
   }
-  int a_tap = -1;      // tap whose rows ap[] point at (implicit conv)
-  const char* bp[2];
+  int a_tap = -1;      // tap whose rows avo[] point at (implicit conv)
+  int bvo[2];
   int bc[2], bkr[2], bb[2], bt[2];
   bool bval[2];
-  int b_k = 0;         // k of the last B region issued (conv3 incremental (b, t))
+  int b_k = kt0 * 64;  // k of the last B region issued (conv3 incremental (b, t))
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int piece = wave * 2 + i;
@@ -1083,7 +1103,7 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256_kernel(GemmP p) {
       bc[i] = (lane & 3) ^ g4_fsw(r);
       const int row = n0 + r;
       bval[i] = row < p.N;
-      bp[i] = Bb + ((long)(bval[i] ? row : 0) * p.ldb + bc[i] * 8) * 2;
+      bvo[i] = bval[i] ? (int)(((long)row * p.ldb + bc[i] * 8) * 2) : BUF_OOB;
       bkr[i] = 0; bb[i] = 0; bt[i] = 0;
     } else {
       const int kr = piece * 2 + (lane >> 5);
@@ -1094,9 +1114,10 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256_kernel(GemmP p) {
       int col = mn;
       bc[i] = 0;
       if (bconv3 && bval[i]) { const int j = mn / p.conv_c; col = mn - j * p.conv_c; bc[i] = j; }
-      bp[i] = Bb + ((long)(bval[i] ? col : 0) + (bconv3 ? 0L : (long)kr * p.ldb)) * 2;
-      bb[i] = bconv3 ? kr / p.conv_t : 0;
-      bt[i] = bconv3 ? kr - bb[i] * p.conv_t : 0;
+      bvo[i] = bval[i] ? (int)(((long)col + (bconv3 ? 0L : (long)kr * p.ldb)) * 2) : BUF_OOB;
+      const int k = b_k + kr;
+      bb[i] = bconv3 ? k / p.conv_t : 0;
+      bt[i] = bconv3 ? k - bb[i] * p.conv_t : 0;
     }
   }
 
@@ -1116,26 +1137,24 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256_kernel(GemmP p) {
             } else {
               ts = at[i] - j;
               ok = ok && ts >= 0 && ts < p.conv_t;
-              ts = ok ? ts : 0;
             }
-            ap[i] = Ab + ((long)(abt[i] + ts) * p.lda + ac[i] * 8) * 2;
-            aok[i] = ok;
+            avo[i] = ok ? (int)(((long)(abt[i] + ts) * p.lda + ac[i] * 8) * 2) : BUF_OOB;
           }
         }
         const bool kin = k0 + 32 <= K;
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-          const bool ok = aok[i] && (kin || k0 + ac[i] * 8 < K);
-          glds16(ok ? ap[i] + (long)c0 * 2 : zero, dst + (wave * 2 + i) * 1024);
+          const int vo = (kin || k0 + ac[i] * 8 < K) ? avo[i] : BUF_OOB;
+          blds16(rsA, vo, c0 * 2, dst + (wave * 2 + i) * 1024);
         }
       } else if (!amode) {
         const bool kin = k0 + 32 <= K;
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-          const bool ok = aok[i] && (kin || k0 + ac[i] * 8 < K);
-          glds16(ok ? ap[i] + (long)k0 * 2 : zero, dst + (wave * 2 + i) * 1024);
+          const int vo = (kin || k0 + ac[i] * 8 < K) ? avo[i] : BUF_OOB;
+          blds16(rsA, vo, k0 * 2, dst + (wave * 2 + i) * 1024);
         }
-      } else {                                  // conv with taps straddling 8-chunks' regions
+      } else {                                  // taps not aligned to 32-wide regions
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
           const int k = k0 + ac[i] * 8;
@@ -1147,18 +1166,17 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256_kernel(GemmP p) {
           } else {
             ts = at[i] - j;
             ok = ok && ts >= 0 && ts < p.conv_t;
-            ts = ok ? ts : 0;
           }
-          const char* src = Ab + ((long)(abt[i] + ts) * p.lda + c) * 2;
-          glds16(ok ? src : zero, dst + (wave * 2 + i) * 1024);
+          const int vo = ok ? (int)(((long)(abt[i] + ts) * p.lda + c) * 2) : BUF_OOB;
+          blds16(rsA, vo, 0, dst + (wave * 2 + i) * 1024);
         }
       }
     } else {
       const bool kin = k0 + 32 <= kva;
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const bool ok = aok[i] && (kin || k0 + at[i] < kva);
-        glds16(ok ? ap[i] + (long)k0 * p.lda * 2 : zero, dst + (wave * 2 + i) * 1024);
+        const int vo = (kin || k0 + at[i] < kva) ? avo[i] : BUF_OOB;
+        blds16(rsA, vo, (int)((long)k0 * p.lda * 2), dst + (wave * 2 + i) * 1024);
       }
     }
   };
@@ -1167,15 +1185,15 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256_kernel(GemmP p) {
       const bool kin = k0 + 32 <= K;
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const bool ok = bval[i] && (kin || k0 + bc[i] * 8 < K);
-        glds16(ok ? bp[i] + (long)k0 * 2 : zero, dst + (wave * 2 + i) * 1024);
+        const int vo = (kin || k0 + bc[i] * 8 < K) ? bvo[i] : BUF_OOB;
+        blds16(rsB, vo, k0 * 2, dst + (wave * 2 + i) * 1024);
       }
     } else if (!bconv3) {
       const bool kin = k0 + 32 <= kva;
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const bool ok = bval[i] && (kin || k0 + bkr[i] < kva);
-        glds16(ok ? bp[i] + (long)k0 * p.ldb * 2 : zero, dst + (wave * 2 + i) * 1024);
+        const int vo = (kin || k0 + bkr[i] < kva) ? bvo[i] : BUF_OOB;
+        blds16(rsB, vo, (int)((long)k0 * p.ldb * 2), dst + (wave * 2 + i) * 1024);
       }
     } else {
       // k-row k = k0 + bkr = b*T + t, advanced incrementally from the previous region
@@ -1189,8 +1207,8 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256_kernel(GemmP p) {
         int ts = t + bc[i] - p.conv_p;
         ts = ts < 0 ? -ts : (ts >= p.conv_t ? 2 * (p.conv_t - 1) - ts : ts);
         const bool ok = bval[i] && k0 + bkr[i] < kva;
-        glds16(ok ? bp[i] + ((long)b * p.conv_t + ts) * p.ldb * 2 : zero,
-               dst + (wave * 2 + i) * 1024);
+        const int vo = ok ? bvo[i] + (int)(((long)b * p.conv_t + ts) * p.ldb * 2) : BUF_OOB;
+        blds16(rsB, vo, 0, dst + (wave * 2 + i) * 1024);
       }
     }
   };
@@ -1201,17 +1219,6 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256_kernel(GemmP p) {
     if ((reg & 1) == 0) issueA(dst, k0);
     else issueB(dst, k0);
   };
-  if constexpr (!BKM) {
-    if (bconv3) {   // start the incremental (b, t) at the first region of this split
-      b_k = kt0 * 64;
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int k = b_k + bkr[i];
-        bb[i] = k / p.conv_t;
-        bt[i] = k - bb[i] * p.conv_t;
-      }
-    }
-  }
 
   f32x4 acc[8][4];
 #pragma unroll
