@@ -780,14 +780,13 @@ __global__ void __launch_bounds__(BNT) gemm_big_kernel(GemmP p) {
   const bool bconv3 = p.conv_mode == 3;
   const bool tap_uniform = amode && (p.conv_c % 64) == 0;  // a 64-wide k-tile sits in one tap
   const int rpu = amode == 4 ? p.conv_t + 2 * p.conv_p : p.conv_t;  // rows per utterance
-  const char* zero = g_fs2_zero;
 
-  // ---- per-lane, per-piece DMA source state, hoisted out of the K loop.  Tiles are issued in
-  // increasing k: pointers advance by wave-uniform offsets and the implicit-conv rows are
-  // re-pointed only when the tap changes.
+  // ---- per-lane, per-piece DMA source state (32-bit byte offsets from the operand base,
+  // BUF_OOB = zero fill), advanced by wave-uniform offsets; implicit-conv rows re-pointed only
+  // when the tap changes.
   // A K-major: pieces 4w+i (8 rows each), lane row r = piece*8 + (lane>>3), chunk alc
-  const char* ap[4];
-  bool aok[4];
+  const i32x4 rsA = make_rsrc(Ab), rsB = make_rsrc(Bb);
+  int avo[4];
   int abt[4], at[4], alc[4];
   bool aval[4];
 #pragma unroll
@@ -801,22 +800,22 @@ __global__ void __launch_bounds__(BNT) gemm_big_kernel(GemmP p) {
       const int b = amode ? rr / rpu : 0;
       abt[i] = b * p.conv_t;       // source row base (unpadded utterance)
       at[i] = rr - b * rpu;        // position inside the (padded) utterance
-      ap[i] = Ab + ((long)rr * p.lda + alc[i] * 8) * 2;
+      avo[i] = aval[i] ? (int)(((long)rr * p.lda + alc[i] * 8) * 2) : BUF_OOB;
     } else {  // MN-major (512-byte k-rows): piece = 2 k-rows
       const int kr = (wave * 4 + i) * 2 + (lane >> 5);
       alc[i] = (lane & 31) ^ mn_swz<bf16>(kr);
       at[i] = kr;
       const int mn = m0 + alc[i] * 8;
       aval[i] = mn < p.M;
-      ap[i] = Ab + ((long)(aval[i] ? mn : 0) + (long)kr * p.lda) * 2;
+      avo[i] = aval[i] ? (int)(((long)mn + (long)kr * p.lda) * 2) : BUF_OOB;
       abt[i] = 0;
     }
-    aok[i] = aval[i];
   }
   int a_tap = -1;
-  const char* bp[2];
+  int bvo[2];
   int blc[2], bkr[2], bb[2], bt[2];
   bool bval[2];
+  int b_k = kt0 * 64;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     if constexpr (BKM) {
@@ -824,7 +823,7 @@ __global__ void __launch_bounds__(BNT) gemm_big_kernel(GemmP p) {
       blc[i] = (lane & 7) ^ (r & 7);
       const int row = n0 + r;
       bval[i] = row < p.N;
-      bp[i] = Bb + ((long)(bval[i] ? row : 0) * p.ldb + blc[i] * 8) * 2;
+      bvo[i] = bval[i] ? (int)(((long)row * p.ldb + blc[i] * 8) * 2) : BUF_OOB;
       bkr[i] = 0; bb[i] = 0; bt[i] = 0;
     } else {  // MN-major (256-byte k-rows): piece = 4 k-rows
       const int kr = (wave * 2 + i) * 4 + (lane >> 4);
@@ -835,13 +834,12 @@ __global__ void __launch_bounds__(BNT) gemm_big_kernel(GemmP p) {
       int col = mn;
       if (bconv3 && bval[i]) { const int j = mn / p.conv_c; col = mn - j * p.conv_c; blc[i] = j; }
       else if (bconv3) blc[i] = 0;
-      bp[i] = Bb + ((long)(bval[i] ? col : 0) + (bconv3 ? 0L : (long)kr * p.ldb)) * 2;
-      const int k = kt0 * 64 + kr;
+      bvo[i] = bval[i] ? (int)(((long)col + (bconv3 ? 0L : (long)kr * p.ldb)) * 2) : BUF_OOB;
+      const int k = b_k + kr;
       bb[i] = bconv3 ? k / p.conv_t : 0;
       bt[i] = bconv3 ? k - bb[i] * p.conv_t : 0;
     }
   }
-  int b_k = kt0 * 64;
 
   auto issue = [&](int kt, int stage) {   // 6 LDS-DMA pieces per wave
     const int k0 = kt * 64;
@@ -861,24 +859,22 @@ __global__ void __launch_bounds__(BNT) gemm_big_kernel(GemmP p) {
             } else {
               ts = at[i] - j;
               ok = ok && ts >= 0 && ts < p.conv_t;
-              ts = ok ? ts : 0;
             }
-            ap[i] = Ab + ((long)(abt[i] + ts) * p.lda + alc[i] * 8) * 2;
-            aok[i] = ok;
+            avo[i] = ok ? (int)(((long)(abt[i] + ts) * p.lda + alc[i] * 8) * 2) : BUF_OOB;
           }
         }
         const bool kin = k0 + 64 <= K;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const bool ok = aok[i] && (kin || k0 + alc[i] * 8 < K);
-          glds16(ok ? ap[i] + (long)c0 * 2 : zero, la + (wave * 4 + i) * 1024);
+          const int vo = (kin || k0 + alc[i] * 8 < K) ? avo[i] : BUF_OOB;
+          blds16(rsA, vo, c0 * 2, la + (wave * 4 + i) * 1024);
         }
       } else if (!amode) {
         const bool kin = k0 + 64 <= K;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const bool ok = aok[i] && (kin || k0 + alc[i] * 8 < K);
-          glds16(ok ? ap[i] + (long)k0 * 2 : zero, la + (wave * 4 + i) * 1024);
+          const int vo = (kin || k0 + alc[i] * 8 < K) ? avo[i] : BUF_OOB;
+          blds16(rsA, vo, k0 * 2, la + (wave * 4 + i) * 1024);
         }
       } else {
 #pragma unroll
@@ -892,33 +888,32 @@ __global__ void __launch_bounds__(BNT) gemm_big_kernel(GemmP p) {
           } else {
             ts = at[i] - j;
             ok = ok && ts >= 0 && ts < p.conv_t;
-            ts = ok ? ts : 0;
           }
-          const char* src = Ab + ((long)(abt[i] + ts) * p.lda + c) * 2;
-          glds16(ok ? src : zero, la + (wave * 4 + i) * 1024);
+          const int vo = ok ? (int)(((long)(abt[i] + ts) * p.lda + c) * 2) : BUF_OOB;
+          blds16(rsA, vo, 0, la + (wave * 4 + i) * 1024);
         }
       }
     } else {
       const bool kin = k0 + 64 <= kva;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const bool ok = aok[i] && (kin || k0 + at[i] < kva);
-        glds16(ok ? ap[i] + (long)k0 * p.lda * 2 : zero, la + (wave * 4 + i) * 1024);
+        const int vo = (kin || k0 + at[i] < kva) ? avo[i] : BUF_OOB;
+        blds16(rsA, vo, (int)((long)k0 * p.lda * 2), la + (wave * 4 + i) * 1024);
       }
     }
     if constexpr (BKM) {
       const bool kin = k0 + 64 <= K;
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const bool ok = bval[i] && (kin || k0 + blc[i] * 8 < K);
-        glds16(ok ? bp[i] + (long)k0 * 2 : zero, lb + (wave * 2 + i) * 1024);
+        const int vo = (kin || k0 + blc[i] * 8 < K) ? bvo[i] : BUF_OOB;
+        blds16(rsB, vo, k0 * 2, lb + (wave * 2 + i) * 1024);
       }
     } else if (!bconv3) {
       const bool kin = k0 + 64 <= kva;
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const bool ok = bval[i] && (kin || k0 + bkr[i] < kva);
-        glds16(ok ? bp[i] + (long)k0 * p.ldb * 2 : zero, lb + (wave * 2 + i) * 1024);
+        const int vo = (kin || k0 + bkr[i] < kva) ? bvo[i] : BUF_OOB;
+        blds16(rsB, vo, (int)((long)k0 * p.ldb * 2), lb + (wave * 2 + i) * 1024);
       }
     } else {
       const int dk = k0 - b_k;
@@ -931,8 +926,8 @@ __global__ void __launch_bounds__(BNT) gemm_big_kernel(GemmP p) {
         int ts = t + blc[i] - p.conv_p;
         ts = ts < 0 ? -ts : (ts >= p.conv_t ? 2 * (p.conv_t - 1) - ts : ts);
         const bool ok = bval[i] && k0 + bkr[i] < kva;
-        glds16(ok ? bp[i] + ((long)b * p.conv_t + ts) * p.ldb * 2 : zero,
-               lb + (wave * 2 + i) * 1024);
+        const int vo = ok ? bvo[i] + (int)(((long)b * p.conv_t + ts) * p.ldb * 2) : BUF_OOB;
+        blds16(rsB, vo, 0, lb + (wave * 2 + i) * 1024);
       }
     }
   };
