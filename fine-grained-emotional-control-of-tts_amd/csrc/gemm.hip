@@ -749,7 +749,9 @@ __device__ __forceinline__ void epilogue_256x128(const GemmP& p, const float* cs
   }
 }
 
-template <bool AK, bool BKM>
+// CM: A-operand conv mode fixed at compile time (0 plain, 1 reflect conv, 4 shift conv, both
+// with 64-aligned taps) or -1 = decided at run time; B3: B-operand conv3 (0/1) or -1 = run time.
+template <bool AK, bool BKM, int CM, int B3>
 __global__ void __launch_bounds__(BNT) gemm_big_kernel(GemmP p) {
   __shared__ __attribute__((aligned(16))) char smem[BIG_LDS];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -768,7 +770,7 @@ __global__ void __launch_bounds__(BNT) gemm_big_kernel(GemmP p) {
   const char* Bb = p.B + (zb * p.sB1 + zh * p.sB2) * 2;
   const int K = p.K;
   const int kva = min(K, p.kvalid);
-  const int amode = (p.conv_mode == 1 || p.conv_mode == 4) ? p.conv_mode : 0;
+  const int amode = CM >= 0 ? CM : ((p.conv_mode == 1 || p.conv_mode == 4) ? p.conv_mode : 0);
   // split-K: this block reduces k-tiles [kt0, kt1) and accumulates with fp32 atomics
   const int nk_all = (K + 63) / 64;
   int kt0 = 0, kt1 = nk_all;
@@ -777,8 +779,9 @@ __global__ void __launch_bounds__(BNT) gemm_big_kernel(GemmP p) {
     kt0 = blockIdx.z * kps;
     kt1 = min(nk_all, kt0 + kps);
   }
-  const bool bconv3 = p.conv_mode == 3;
-  const bool tap_uniform = amode && (p.conv_c % 64) == 0;  // a 64-wide k-tile sits in one tap
+  const bool bconv3 = B3 >= 0 ? B3 == 1 : p.conv_mode == 3;
+  // a 64-wide k-tile sits in one tap
+  const bool tap_uniform = CM > 0 ? true : (CM == 0 ? false : amode && (p.conv_c % 64) == 0);
   const int rpu = amode == 4 ? p.conv_t + 2 * p.conv_p : p.conv_t;  // rows per utterance
 
   // ---- per-lane, per-piece DMA source state (32-bit byte offsets from the operand base,
@@ -1024,7 +1027,7 @@ __device__ __forceinline__ bf16x8 g4_frag_k(const char* rg, int row, int g) {
   return *(const bf16x8*)(rg + row * 64 + ((g ^ g4_fsw(row)) << 4));
 }
 
-template <bool AK, bool BKM>
+template <bool AK, bool BKM, int CM, int B3>   // CM, B3: as gemm_big_kernel (32-aligned taps)
 __global__ void __launch_bounds__(G4_NT, 1) gemm256_kernel(GemmP p) {
   __shared__ __attribute__((aligned(16))) char smem[G4_LDS];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1042,7 +1045,7 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256_kernel(GemmP p) {
   const char* Bb = p.B + (zb * p.sB1 + zh * p.sB2) * 2;
   const int K = p.K;
   const int kva = min(K, p.kvalid);
-  const int amode = (p.conv_mode == 1 || p.conv_mode == 4) ? p.conv_mode : 0;
+  const int amode = CM >= 0 ? CM : ((p.conv_mode == 1 || p.conv_mode == 4) ? p.conv_mode : 0);
   const int nk_all = (K + 63) / 64;
   int kt0 = 0, kt1 = nk_all;
   if (p.split_k > 1) {
@@ -1050,8 +1053,9 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256_kernel(GemmP p) {
     kt0 = blockIdx.z * kps;
     kt1 = min(nk_all, kt0 + kps);
   }
-  const bool bconv3 = p.conv_mode == 3;
-  const bool tap_uniform = amode && (p.conv_c % 32) == 0;  // a 32-wide region sits in one tap
+  const bool bconv3 = B3 >= 0 ? B3 == 1 : p.conv_mode == 3;
+  // a 32-wide region sits in one tap
+  const bool tap_uniform = CM > 0 ? true : (CM == 0 ? false : amode && (p.conv_c % 32) == 0);
   const int rpu = amode == 4 ? p.conv_t + 2 * p.conv_p : p.conv_t;
 
   // ---- per-lane DMA source state of this wave's two pieces of an A region and of a B region:
@@ -1309,6 +1313,14 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256_kernel(GemmP p) {
   }
 }
 
+// compile-time A-operand conv variant for the large-tile kernels: 0 plain, 1 / 4 conv with
+// taps aligned to the k-granule, -1 anything else (run-time generic path)
+int conv_variant(const GemmP& q, int granule) {
+  if (q.conv_mode == 0 || q.conv_mode == 3) return 0;
+  if ((q.conv_mode == 1 || q.conv_mode == 4) && q.conv_c % granule == 0) return q.conv_mode;
+  return -1;
+}
+
 template <typename T, bool GA, bool GB>
 void launch4(const GemmP& p, dim3 grid, hipStream_t s, int ak, int bk) {
   if (ak && bk) hipLaunchKernelGGL((gemm_kernel<T, true, true, GA, GB>), grid, dim3(NT), 0, s, p);
@@ -1366,10 +1378,21 @@ int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
         gz2 = q.split_k;
       }
       dim3 g2(tiles256, 1, gz2);
-      if (ak && bk) hipLaunchKernelGGL((gemm256_kernel<true, true>), g2, dim3(G4_NT), 0, s, q);
-      else if (ak && !bk) hipLaunchKernelGGL((gemm256_kernel<true, false>), g2, dim3(G4_NT), 0, s, q);
-      else if (!ak && bk) hipLaunchKernelGGL((gemm256_kernel<false, true>), g2, dim3(G4_NT), 0, s, q);
-      else hipLaunchKernelGGL((gemm256_kernel<false, false>), g2, dim3(G4_NT), 0, s, q);
+      const int cm = conv_variant(q, 32);
+      if (ak && bk) {
+        if (cm == 0) hipLaunchKernelGGL((gemm256_kernel<true, true, 0, 0>), g2, dim3(G4_NT), 0, s, q);
+        else if (cm == 1) hipLaunchKernelGGL((gemm256_kernel<true, true, 1, 0>), g2, dim3(G4_NT), 0, s, q);
+        else if (cm == 4) hipLaunchKernelGGL((gemm256_kernel<true, true, 4, 0>), g2, dim3(G4_NT), 0, s, q);
+        else hipLaunchKernelGGL((gemm256_kernel<true, true, -1, -1>), g2, dim3(G4_NT), 0, s, q);
+      } else if (!ak && !bk) {
+        if (q.conv_mode == 3) hipLaunchKernelGGL((gemm256_kernel<false, false, 0, 1>), g2, dim3(G4_NT), 0, s, q);
+        else if (q.conv_mode == 0) hipLaunchKernelGGL((gemm256_kernel<false, false, 0, 0>), g2, dim3(G4_NT), 0, s, q);
+        else hipLaunchKernelGGL((gemm256_kernel<false, false, -1, -1>), g2, dim3(G4_NT), 0, s, q);
+      } else if (ak) {
+        hipLaunchKernelGGL((gemm256_kernel<true, false, -1, -1>), g2, dim3(G4_NT), 0, s, q);
+      } else {
+        hipLaunchKernelGGL((gemm256_kernel<false, true, -1, -1>), g2, dim3(G4_NT), 0, s, q);
+      }
       FS2_CHECK_LAUNCH();
       return 0;
     }
@@ -1389,10 +1412,21 @@ int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
         q.accumulate = 1;
       }
       dim3 g2(q.tiles_m * q.tiles_n, 1, wgrad ? split_big : (slices ? p.split_k : gz));
-      if (ak && bk) hipLaunchKernelGGL((gemm_big_kernel<true, true>), g2, dim3(BNT), 0, s, q);
-      else if (ak && !bk) hipLaunchKernelGGL((gemm_big_kernel<true, false>), g2, dim3(BNT), 0, s, q);
-      else if (!ak && bk) hipLaunchKernelGGL((gemm_big_kernel<false, true>), g2, dim3(BNT), 0, s, q);
-      else hipLaunchKernelGGL((gemm_big_kernel<false, false>), g2, dim3(BNT), 0, s, q);
+      const int cm = conv_variant(q, 64);
+      if (ak && bk) {
+        if (cm == 0) hipLaunchKernelGGL((gemm_big_kernel<true, true, 0, 0>), g2, dim3(BNT), 0, s, q);
+        else if (cm == 1) hipLaunchKernelGGL((gemm_big_kernel<true, true, 1, 0>), g2, dim3(BNT), 0, s, q);
+        else if (cm == 4) hipLaunchKernelGGL((gemm_big_kernel<true, true, 4, 0>), g2, dim3(BNT), 0, s, q);
+        else hipLaunchKernelGGL((gemm_big_kernel<true, true, -1, -1>), g2, dim3(BNT), 0, s, q);
+      } else if (!ak && !bk) {
+        if (q.conv_mode == 3) hipLaunchKernelGGL((gemm_big_kernel<false, false, 0, 1>), g2, dim3(BNT), 0, s, q);
+        else if (q.conv_mode == 0) hipLaunchKernelGGL((gemm_big_kernel<false, false, 0, 0>), g2, dim3(BNT), 0, s, q);
+        else hipLaunchKernelGGL((gemm_big_kernel<false, false, -1, -1>), g2, dim3(BNT), 0, s, q);
+      } else if (ak) {
+        hipLaunchKernelGGL((gemm_big_kernel<true, false, -1, -1>), g2, dim3(BNT), 0, s, q);
+      } else {
+        hipLaunchKernelGGL((gemm_big_kernel<false, true, -1, -1>), g2, dim3(BNT), 0, s, q);
+      }
     } else if (p.conv_mode == 2) launch4<T, false, true>(p, grid, s, ak, bk);
     else launch4<T, true, true>(p, grid, s, ak, bk);
   } else {
