@@ -10,6 +10,7 @@
 // torch in this container).  A fully masked row yields NaN, as torch's softmax does.
 //
 // One wave per (z, query) row; scores fp32, probabilities stored in the activation dtype.
+// Dropout: fs2_keep_fast over element index row * round_up(Tk, 2) + k (same draw as flash.hip).
 #include "fs2_common.h"
 
 namespace {
@@ -39,6 +40,7 @@ __global__ void __launch_bounds__(256) softmax_fwd_kernel(const float* S, const 
   l = wave_sum(l);
   const float inv = 1.f / l;  // l == 0 (all keys masked) -> inf * 0 = NaN below, like torch
   const float inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+  const uint32_t dkey = fs2_drop_key(seed, salt), thr = fs2_thr16(p_drop);
   T* prow = P + row * ldt;
   T* pdrow = Pd ? Pd + row * ldt : nullptr;
   for (int k = lane; k < ldt; k += 64) {
@@ -48,7 +50,7 @@ __global__ void __launch_bounds__(256) softmax_fwd_kernel(const float* S, const 
     if (pdrow) {
       float q = pv;
       if (p_drop > 0.f && k < Tk)
-        q = fs2_keep(seed, salt, (uint64_t)row * Tk + k, p_drop) ? pv * inv_keep : 0.f;
+        q = fs2_keep_fast(dkey, (uint64_t)row * ((Tk + 1) & ~1) + k, thr) ? pv * inv_keep : 0.f;
       pdrow[k] = from_f<T>(q);
     }
   }
@@ -65,10 +67,11 @@ __global__ void __launch_bounds__(256) softmax_bwd_kernel(const float* dPd, cons
   const float* g = dPd + row * ldt;
   const T* prow = P + row * ldt;
   const float inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+  const uint32_t dkey = fs2_drop_key(seed, salt), thr = fs2_thr16(p_drop);
   float dot = 0.f;
   for (int k = lane; k < Tk; k += 64) {
     float gv = g[k];
-    if (p_drop > 0.f) gv = fs2_keep(seed, salt, (uint64_t)row * Tk + k, p_drop) ? gv * inv_keep : 0.f;
+    if (p_drop > 0.f) gv = fs2_keep_fast(dkey, (uint64_t)row * ((Tk + 1) & ~1) + k, thr) ? gv * inv_keep : 0.f;
     dot += gv * to_f(prow[k]);
   }
   dot = wave_sum(dot);
@@ -77,7 +80,7 @@ __global__ void __launch_bounds__(256) softmax_bwd_kernel(const float* dPd, cons
     float v = 0.f;
     if (k < Tk) {
       float gv = g[k];
-      if (p_drop > 0.f) gv = fs2_keep(seed, salt, (uint64_t)row * Tk + k, p_drop) ? gv * inv_keep : 0.f;
+      if (p_drop > 0.f) gv = fs2_keep_fast(dkey, (uint64_t)row * ((Tk + 1) & ~1) + k, thr) ? gv * inv_keep : 0.f;
       v = scale * to_f(prow[k]) * (gv - dot);
     }
     drow[k] = from_f<T>(v);

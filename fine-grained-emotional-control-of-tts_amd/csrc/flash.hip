@@ -5,8 +5,8 @@
 // torch nn.MultiheadAttention as SB calls it (model.py:338-346, 411-427),
 // with the reference's head-major mask tiling: for z = b*H + h the key k is
 // masked iff key_pad[b][k] | key_pad[(b*H + h) % B][k].  Dropout on the probabilities uses
-// the same counter hash and element index ((z*T + q)*T + k) as the materialised path
-// (attention.hip), so both paths draw identical masks.
+// the same pair hash (fs2_keep_fast) and element index ((z*T + q)*round_up(T, 2) + k) as the
+// materialised path (attention.hip), so both paths draw identical masks.
 //
 // Layout: Q, K, V are column blocks of the packed projection QKV [B*T][ldq] (q | k | v, head
 // h at columns h*dh of each block); the context O is [B*T][ldo] with head h at h*dh.
@@ -45,6 +45,7 @@ struct AttnP {
   int B, H, T, D;
   float scale, scale_log2, p_drop, inv_keep;
   uint32_t seed, salt;
+  uint32_t thr16;                // dropout threshold (fs2_thr16)
 };
 
 __device__ __forceinline__ bf16x8 ld_frag(const bf16* g) { return *(const bf16x8*)g; }
@@ -130,6 +131,8 @@ __global__ void __launch_bounds__(512 / QG, QG) attn_fwd_kernel(AttnP p) {
   __shared__ int kend_s;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
   const int z = blockIdx.y, b = z / p.H, h = z - b * p.H;
+  const uint32_t dkey = fs2_drop_key(p.seed, p.salt);
+  const uint64_t T2 = (uint64_t)((p.T + 1) & ~1);   // dropout rows padded to even length
   const int kend = build_kvalid(kval, &kend_s, p, b, h);
   const bf16* Qb = p.qkv + (long)b * p.T * p.ldq + h * DH;
   const bf16* Kb = Qb + p.D;
@@ -194,20 +197,26 @@ __global__ void __launch_bounds__(512 / QG, QG) attn_fwd_kernel(AttnP p) {
       mrow[qg] = mnew;
       float ls = 0.f;
       float pd[4][4];
+      const uint64_t rowi = ((uint64_t)z * p.T + qi[qg]) * T2;
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float e = v[kt][r] == -INFINITY ? 0.f : exp2f(v[kt][r] - mnew);
           ls += e;
-          float q = e;
-          if (p.p_drop > 0.f) {
-            const int key = k0 + kt * 16 + 4 * g + r;
-            q = fs2_keep(p.seed, p.salt, ((uint64_t)z * p.T + qi[qg]) * p.T + key, p.p_drop)
-                    ? e * p.inv_keep : 0.f;
-          }
-          pd[kt][r] = q;
+          pd[kt][r] = e;
         }
+      if (p.p_drop > 0.f) {
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+          for (int r = 0; r < 4; r += 2) {
+            const uint64_t idx = rowi + k0 + kt * 16 + 4 * g + r;   // even
+            const uint32_t h = fs2_hash_pair(dkey, idx >> 1);
+            pd[kt][r] = fs2_keep_pair_bit(h, idx, p.thr16) ? pd[kt][r] * p.inv_keep : 0.f;
+            pd[kt][r + 1] = fs2_keep_pair_bit(h, idx + 1, p.thr16) ? pd[kt][r + 1] * p.inv_keep : 0.f;
+          }
+      }
       lrow[qg] = lrow[qg] * alpha + ls;
 #pragma unroll
       for (int d = 0; d < ND; ++d) oacc[d][qg] *= alpha;
@@ -257,6 +266,8 @@ __global__ void __launch_bounds__(512 / QG, QG) attn_bwd_dq_kernel(AttnP p) {
   __shared__ int kend_s;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
   const int z = blockIdx.y, b = z / p.H, h = z - b * p.H;
+  const uint32_t dkey = fs2_drop_key(p.seed, p.salt);
+  const uint64_t T2 = (uint64_t)((p.T + 1) & ~1);   // dropout rows padded to even length
   const int kend = build_kvalid(kval, &kend_s, p, b, h);
   const bf16* Qb = p.qkv + (long)b * p.T * p.ldq + h * DH;
   const bf16* Kb = Qb + p.D;
@@ -320,18 +331,22 @@ __global__ void __launch_bounds__(512 / QG, QG) attn_bwd_dq_kernel(AttnP p) {
 #pragma unroll
     for (int qg = 0; qg < QG; ++qg) {
       float ds[4][4];
+      const uint64_t rowi = ((uint64_t)z * p.T + qi[qg]) * T2;
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
+        for (int r = 0; r < 4; r += 2) {
           const int key = k0 + kt * 16 + 4 * g + r;
-          const bool ok = key < p.T && kval[key];
-          const float pr = ok ? exp2f(sacc[kt][qg][r] * p.scale_log2 - lse[qg]) : 0.f;
-          float dp = pacc[kt][qg][r];
-          if (p.p_drop > 0.f)
-            dp = fs2_keep(p.seed, p.salt, ((uint64_t)z * p.T + qi[qg]) * p.T + key, p.p_drop)
-                     ? dp * p.inv_keep : 0.f;
-          ds[kt][r] = pr * (dp - dsum[qg]);
+          const uint32_t h = p.p_drop > 0.f ? fs2_hash_pair(dkey, (rowi + key) >> 1) : 0u;
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const bool ok = key + e < p.T && kval[key + e];
+            const float pr = ok ? exp2f(sacc[kt][qg][r + e] * p.scale_log2 - lse[qg]) : 0.f;
+            float dp = pacc[kt][qg][r + e];
+            if (p.p_drop > 0.f)
+              dp = fs2_keep_pair_bit(h, rowi + key + e, p.thr16) ? dp * p.inv_keep : 0.f;
+            ds[kt][r + e] = pr * (dp - dsum[qg]);
+          }
         }
       sf[qg][0] = pack8(ds[0], ds[1]);
       sf[qg][1] = pack8(ds[2], ds[3]);
@@ -375,6 +390,8 @@ __global__ void __launch_bounds__(512, 1) attn_bwd_dkv_kernel(AttnP p) {
   __shared__ int kend_s;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
   const int z = blockIdx.y, b = z / p.H, h = z - b * p.H;
+  const uint32_t dkey = fs2_drop_key(p.seed, p.salt);
+  const uint64_t T2 = (uint64_t)((p.T + 1) & ~1);   // dropout rows padded to even length
   build_kvalid(kval, &kend_s, p, b, h);
   const bf16* Qb = p.qkv + (long)b * p.T * p.ldq + h * DH;
   const bf16* Kb = Qb + p.D;
@@ -430,7 +447,7 @@ __global__ void __launch_bounds__(512, 1) attn_bwd_dkv_kernel(AttnP p) {
         float dp = pacc[qt][r];
         float pd = pr;
         if (p.p_drop > 0.f) {
-          const bool keep = fs2_keep(p.seed, p.salt, ((uint64_t)z * p.T + q) * p.T + key, p.p_drop);
+          const bool keep = fs2_keep_fast(dkey, ((uint64_t)z * p.T + q) * T2 + key, p.thr16);
           dp = keep ? dp * p.inv_keep : 0.f;
           pd = keep ? pr * p.inv_keep : 0.f;
         }
@@ -516,6 +533,7 @@ extern "C" int fs2_attn_fwd(const void* qkv, int64_t ldq, const uint8_t* key_pad
   p.scale = scale; p.scale_log2 = scale * LOG2E; p.p_drop = p_drop;
   p.inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
   p.seed = seed; p.salt = salt;
+  p.thr16 = (uint32_t)(p_drop * 65536.f + 0.5f);
   hipStream_t s = (hipStream_t)stream;
   switch (dh) {
     case 64: launch_fwd<64>(p, s); break;
@@ -546,6 +564,7 @@ extern "C" int fs2_attn_bwd(const void* qkv, int64_t ldq, const uint8_t* key_pad
   p.scale = scale; p.scale_log2 = scale * LOG2E; p.p_drop = p_drop;
   p.inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
   p.seed = seed; p.salt = salt;
+  p.thr16 = (uint32_t)(p_drop * 65536.f + 0.5f);
   hipStream_t s = (hipStream_t)stream;
   switch (dh) {
     case 64: launch_bwd<64>(p, s); break;

@@ -95,6 +95,26 @@ __device__ __forceinline__ bool fs2_keep(uint32_t seed, uint32_t salt, uint64_t 
   return u >= p;
 }
 
+// Attention-probability dropout draws B*H*T^2 masks per layer, so it uses a cheaper form:
+// one murmur-finaliser round per PAIR of elements (idx >> 1) keyed by a per-call key, 16 bits
+// per element compared with thr16 = round(p * 65536).  Element indices are row-major over
+// rows padded to an even length, so a lane's consecutive keys share one hash.
+__device__ __forceinline__ uint32_t fs2_drop_key(uint32_t seed, uint32_t salt) {
+  return fs2_mix32(seed ^ (salt * 0x9E3779B9u)) | 1u;
+}
+__device__ __forceinline__ uint32_t fs2_hash_pair(uint32_t key, uint64_t pair) {
+  uint32_t h = ((uint32_t)pair * 0x9E3779B1u) ^ ((uint32_t)(pair >> 32) * 0x85EBCA77u) ^ key;
+  h ^= h >> 15; h *= 0x2C1B3C6Du; h ^= h >> 12; h *= 0x297A2D39u; h ^= h >> 15;
+  return h;
+}
+__device__ __forceinline__ bool fs2_keep_pair_bit(uint32_t h, uint64_t idx, uint32_t thr16) {
+  return ((h >> ((uint32_t)(idx & 1) * 16)) & 0xffffu) >= thr16;
+}
+__device__ __forceinline__ bool fs2_keep_fast(uint32_t key, uint64_t idx, uint32_t thr16) {
+  return fs2_keep_pair_bit(fs2_hash_pair(key, idx >> 1), idx, thr16);
+}
+__device__ __forceinline__ uint32_t fs2_thr16(float p) { return (uint32_t)(p * 65536.f + 0.5f); }
+
 // reflect index into [0, T) (torch F.pad(mode="reflect") semantics, single bounce)
 __device__ __forceinline__ int reflect_idx(int i, int T) {
   if (i < 0) i = -i;

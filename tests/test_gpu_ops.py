@@ -392,7 +392,7 @@ def test_colsum_bias_gradient(cuda, dt, code, tol, M, N, ldx):
 
 
 def _keep_np(seed, salt, idx, p):
-    """numpy restatement of fs2_keep (fs2_common.h) for the dropout masks of the HIP kernels."""
+    """numpy restatement of fs2_keep_fast (fs2_common.h): the attention-dropout mask."""
     M32 = np.uint64(0xffffffff)
 
     def mix(h):
@@ -404,11 +404,19 @@ def _keep_np(seed, salt, idx, p):
         h ^= h >> np.uint64(16)
         return h
 
+    key = int(mix(np.uint64((seed ^ ((salt * 0x9E3779B9) & 0xffffffff)) & 0xffffffff))) | 1
     idx = idx.astype(np.uint64)
-    s0 = mix(np.uint64((seed ^ ((salt * 0x9E3779B9) & 0xffffffff)) & 0xffffffff))
-    h = mix((idx & M32) ^ s0)
-    h = mix(h ^ (idx >> np.uint64(32)) ^ np.uint64(0x68bc21eb))
-    return ((h >> np.uint64(8)).astype(np.float64) / 16777216.0) >= p
+    pair = idx >> np.uint64(1)
+    h = ((pair & M32) * np.uint64(0x9E3779B1)) & M32
+    h ^= ((pair >> np.uint64(32)) * np.uint64(0x85EBCA77)) & M32
+    h ^= np.uint64(key)
+    h ^= h >> np.uint64(15)
+    h = (h * np.uint64(0x2C1B3C6D)) & M32
+    h ^= h >> np.uint64(12)
+    h = (h * np.uint64(0x297A2D39)) & M32
+    h ^= h >> np.uint64(15)
+    bits = (h >> ((idx & np.uint64(1)) * np.uint64(16))) & np.uint64(0xffff)
+    return bits >= np.uint64(int(p * 65536 + 0.5))
 
 
 @pytest.mark.parametrize("dh,T,p_drop", [(192, 150, 0.0), (192, 150, 0.1), (64, 70, 0.1),
@@ -442,7 +450,9 @@ def test_fused_attention_vs_torch(cuda, dh, T, p_drop):
     s = (q @ k.transpose(-1, -2)) * scale
     P = torch.softmax(s.masked_fill(mask, float("-inf")), -1)
     if p_drop > 0:
-        idx = np.arange(B * H * T * T, dtype=np.uint64)
+        T2 = (T + 1) & ~1                          # dropout rows padded to even length
+        idx = (np.arange(B * H * T, dtype=np.uint64)[:, None] * np.uint64(T2)
+               + np.arange(T, dtype=np.uint64)[None, :])
         keep = torch.from_numpy(_keep_np(seed, salt, idx, p_drop).reshape(B, H, T, T)).to(cuda)
         P = P * keep / (1 - p_drop)
     o = P @ v
