@@ -25,6 +25,11 @@
 
 #include "fs2_common.h"
 
+typedef __attribute__((ext_vector_type(4))) int i32x4;
+__device__ void llvm_raw_buffer_load_lds(i32x4 rsrc, __attribute__((address_space(3))) uint32_t* lds,
+                                         int size, int voffset, int soffset, int offset,
+                                         int aux) __asm("llvm.amdgcn.raw.buffer.load.lds");
+
 namespace {
 
 typedef __attribute__((ext_vector_type(4))) short s16x4;
@@ -84,6 +89,51 @@ __device__ __forceinline__ void load_tile(char* t, const bf16* src, long ld, int
   }
 }
 
+// Buffer-resource LDS-DMA (buffer_load_dwordx4 ... lds): wave-uniform base, 32-bit lane
+// offset, lanes at BUF_OOB load zeros.
+constexpr int BUF_OOB = (int)0x80000000u;
+__device__ __forceinline__ i32x4 make_rsrc(const void* base) {
+  const uint64_t a = (uint64_t)base;
+  i32x4 r;
+  r[0] = __builtin_amdgcn_readfirstlane((int)(a & 0xffffffffu));
+  r[1] = __builtin_amdgcn_readfirstlane((int)(a >> 32));
+  r[2] = 0x7fffffff;
+  r[3] = 0x00020000;
+  return r;
+}
+__device__ __forceinline__ void blds16(i32x4 rsrc, int voff, int soff, char* lds_wave_base) {
+  llvm_raw_buffer_load_lds(rsrc, (__attribute__((address_space(3))) uint32_t*)lds_wave_base, 16,
+                           voff, soff, 0, 0);
+}
+
+// A 64-row x DH tile image (16-byte chunk c of row r stored at c ^ (r & 7)) filled by LDS-DMA:
+// 1 KiB instruction i covers image bytes [1024 i, 1024 i + 1024) and each lane fetches the
+// logical chunk that lands at its slot.  NW waves issue NI / NW instructions each.
+template <int DH, int NW>
+struct TileDma {
+  static constexpr int NI = 64 * DH * 2 / 1024;
+  static constexpr int PER = NI / NW;
+  static_assert(NI % NW == 0, "tile instructions must split evenly over the waves");
+  int lane16;   // lane * 16: the per-lane byte offset inside each 1 KiB instruction
+  __device__ __forceinline__ void init(int, int lane, long) { lane16 = lane * 16; }
+  // rows r0 .. r0+63 of the column block (rows >= nrows read zeros); slots are recomputed per
+  // call (a few VALU per instruction) to keep the register budget for the MFMA work
+  __device__ __forceinline__ void issue(char* tile, i32x4 rs, long ld, int r0, int nrows,
+                                        int wave) const {
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int o = (wave + j * NW) * 1024 + lane16;
+      const int r = o / (DH * 2), cp = (o - r * DH * 2) >> 4;
+      const int vo = (r * (int)ld + (cp ^ (r & 7)) * 8) * 2;
+      blds16(rs, r0 + r < nrows ? vo : BUF_OOB, (int)((long)r0 * ld * 2),
+             tile + (wave + j * NW) * 1024);
+    }
+  }
+};
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
 __device__ __forceinline__ bf16x8 pack8(const float* a, const float* b) {
   bf16x8 r;
   r[0] = (bf16)a[0]; r[1] = (bf16)a[1]; r[2] = (bf16)a[2]; r[3] = (bf16)a[3];
@@ -122,13 +172,15 @@ __device__ __forceinline__ int build_kvalid(uint8_t* kval, int* kend_s, const At
 // ------------------------------------------------------------------------------ forward
 // block: 128 queries = (8 / QG) waves x QG 16-query groups; K/V tiles of 64 keys
 template <int DH, int QG>
-__global__ void __launch_bounds__(512 / QG, QG) attn_fwd_kernel(AttnP p) {
+__global__ void __launch_bounds__(512 / QG, 1) attn_fwd_kernel(AttnP p) {
   constexpr int NT = 512 / QG;
   constexpr int NS = DH / 32, ND = DH / 16;
-  __shared__ __attribute__((aligned(16))) char Ks[64 * DH * 2];
-  __shared__ __attribute__((aligned(16))) char Vs[64 * DH * 2];
-  __shared__ uint8_t kval[TMAX];
-  __shared__ int kend_s;
+  constexpr int TB = 64 * DH * 2;
+  // one LDS array (a second __shared__ object can make hipcc drain the DMA ring early):
+  // [tile buffer 0: 2 tensors | tile buffer 1: 2 tensors | kval | kend]
+  __shared__ __attribute__((aligned(16))) char smem[4 * TB + TMAX + 16];
+  uint8_t* kval = (uint8_t*)(smem + 4 * TB);
+  int& kend_s = *(int*)(smem + 4 * TB + TMAX);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
   const int z = blockIdx.y, b = z / p.H, h = z - b * p.H;
   const uint32_t dkey = fs2_drop_key(p.seed, p.salt);
@@ -158,11 +210,30 @@ __global__ void __launch_bounds__(512 / QG, QG) attn_fwd_kernel(AttnP p) {
 #pragma unroll
   for (int qg = 0; qg < QG; ++qg) { mrow[qg] = -INFINITY; lrow[qg] = 0.f; }
 
-  for (int k0 = 0; k0 < kend; k0 += 64) {
-    __syncthreads();
-    load_tile<DH, 64>(Ks, Kb, p.ldq, k0, p.T, threadIdx.x, NT);
-    load_tile<DH, 64>(Vs, Vb, p.ldq, k0, p.T, threadIdx.x, NT);
-    __syncthreads();
+  // K/V tiles double-buffered through LDS-DMA: tile t+1 streams in while tile t computes
+  TileDma<DH, NT / 64> dma;
+  dma.init(wave, lane, p.ldq);
+  const i32x4 rsK = make_rsrc(Kb), rsV = make_rsrc(Vb);
+  const int ntile = (kend + 63) / 64;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // Q fragments resident before the ring
+  if (ntile > 0) {
+    dma.issue(smem, rsK, p.ldq, 0, p.T, wave);
+    dma.issue(smem + TB, rsV, p.ldq, 0, p.T, wave);
+  }
+  for (int t = 0; t < ntile; ++t) {
+    const int k0 = t * 64;
+    const char* Ks = smem + (t & 1) * 2 * TB;
+    const char* Vs = Ks + TB;
+    if (t + 1 < ntile) {
+      char* nx = smem + ((t + 1) & 1) * 2 * TB;
+      dma.issue(nx, rsK, p.ldq, k0 + 64, p.T, wave);
+      dma.issue(nx + TB, rsV, p.ldq, k0 + 64, p.T, wave);
+      wait_vmcnt<2 * TileDma<DH, NT / 64>::PER>();
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
     f32x4 sacc[4][QG];
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt)
@@ -232,6 +303,7 @@ __global__ void __launch_bounds__(512 / QG, QG) attn_fwd_kernel(AttnP p) {
         for (int qg = 0; qg < QG; ++qg)
           oacc[d][qg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[qg][j], oacc[d][qg], 0, 0, 0);
       }
+    __builtin_amdgcn_s_barrier();   // every wave is done with buffer t & 1 before t+2 lands
   }
 #pragma unroll
   for (int qg = 0; qg < QG; ++qg) {
@@ -257,13 +329,15 @@ __global__ void __launch_bounds__(512 / QG, QG) attn_fwd_kernel(AttnP p) {
 // block: 128 queries = (8 / QG) waves x QG 16-query groups; also writes D = rowsum(dO * O)
 // for the dK/dV kernel
 template <int DH, int QG>
-__global__ void __launch_bounds__(512 / QG, QG) attn_bwd_dq_kernel(AttnP p) {
+__global__ void __launch_bounds__(512 / QG, 1) attn_bwd_dq_kernel(AttnP p) {
   constexpr int NT = 512 / QG;
   constexpr int NS = DH / 32, ND = DH / 16;
-  __shared__ __attribute__((aligned(16))) char Ks[64 * DH * 2];
-  __shared__ __attribute__((aligned(16))) char Vs[64 * DH * 2];
-  __shared__ uint8_t kval[TMAX];
-  __shared__ int kend_s;
+  constexpr int TB = 64 * DH * 2;
+  // one LDS array (a second __shared__ object can make hipcc drain the DMA ring early):
+  // [tile buffer 0: 2 tensors | tile buffer 1: 2 tensors | kval | kend]
+  __shared__ __attribute__((aligned(16))) char smem[4 * TB + TMAX + 16];
+  uint8_t* kval = (uint8_t*)(smem + 4 * TB);
+  int& kend_s = *(int*)(smem + 4 * TB + TMAX);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
   const int z = blockIdx.y, b = z / p.H, h = z - b * p.H;
   const uint32_t dkey = fs2_drop_key(p.seed, p.salt);
@@ -305,11 +379,30 @@ __global__ void __launch_bounds__(512 / QG, QG) attn_bwd_dq_kernel(AttnP p) {
 #pragma unroll
     for (int qg = 0; qg < QG; ++qg) qacc[d][qg] = f32x4{0, 0, 0, 0};
 
-  for (int k0 = 0; k0 < kend; k0 += 64) {
-    __syncthreads();
-    load_tile<DH, 64>(Ks, Kb, p.ldq, k0, p.T, threadIdx.x, NT);
-    load_tile<DH, 64>(Vs, Vb, p.ldq, k0, p.T, threadIdx.x, NT);
-    __syncthreads();
+  // K/V tiles double-buffered through LDS-DMA: tile t+1 streams in while tile t computes
+  TileDma<DH, NT / 64> dma;
+  dma.init(wave, lane, p.ldq);
+  const i32x4 rsK = make_rsrc(Kb), rsV = make_rsrc(Vb);
+  const int ntile = (kend + 63) / 64;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // Q fragments resident before the ring
+  if (ntile > 0) {
+    dma.issue(smem, rsK, p.ldq, 0, p.T, wave);
+    dma.issue(smem + TB, rsV, p.ldq, 0, p.T, wave);
+  }
+  for (int t = 0; t < ntile; ++t) {
+    const int k0 = t * 64;
+    const char* Ks = smem + (t & 1) * 2 * TB;
+    const char* Vs = Ks + TB;
+    if (t + 1 < ntile) {
+      char* nx = smem + ((t + 1) & 1) * 2 * TB;
+      dma.issue(nx, rsK, p.ldq, k0 + 64, p.T, wave);
+      dma.issue(nx + TB, rsV, p.ldq, k0 + 64, p.T, wave);
+      wait_vmcnt<2 * TileDma<DH, NT / 64>::PER>();
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
     f32x4 sacc[4][QG], pacc[4][QG];
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt)
@@ -360,6 +453,7 @@ __global__ void __launch_bounds__(512 / QG, QG) attn_bwd_dq_kernel(AttnP p) {
         for (int qg = 0; qg < QG; ++qg)
           qacc[d][qg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, sf[qg][j], qacc[d][qg], 0, 0, 0);
       }
+    __builtin_amdgcn_s_barrier();   // every wave is done with buffer t & 1 before t+2 lands
   }
 #pragma unroll
   for (int qg = 0; qg < QG; ++qg) {
