@@ -34,6 +34,8 @@ def parse():
     ap.add_argument("--max-shape", action="store_true", help="all T_phon=200, d=5 (T_mel=1000)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-utts", type=int, default=2)
+    ap.add_argument("--no-extractor", action="store_true",
+                    help="skip the second timed loop that adds the frozen IntensityExtractor")
     return ap.parse_args()
 
 
@@ -76,6 +78,53 @@ def pmc_traffic():
     return d["hbm_bytes_per_launch"], os.path.relpath(hits[-1], ROOT)
 
 
+def extractor_leg(cfg_all, args, trainer, b, bt, Tm, dt, world, frames_local):
+    """The reference train loop body INCLUDING the frozen IntensityExtractor forward + phoneme
+    averaging (train.py:69-81), timed the same way over ``steps`` steps.  Reported
+    beside ``value`` (whose definition, SURVEY 8d, excludes the extractor)."""
+    from fastspeech2.intensity import IntensityExtractor, get_intensity_representation
+    from fastspeech2.flops import extractor_flops
+    rc = cfg_all["model"]["rank_model"]
+    torch.manual_seed(1)
+    ext = IntensityExtractor(cfg_all["audio"]["n_mels"], rc["n_heads"], 5, rc["n_encoder_layers"],
+                             rc["hidden_dim"], rc["kernel_size"], rc["dropout"],
+                             act_dtype=dt).cuda()
+    coll = as_collate(b)
+    for _ in range(2):
+        rep = get_intensity_representation(ext, coll)
+        trainer.step(bt, rep, mel_len_max=Tm)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        get_intensity_representation(ext, coll)
+    torch.cuda.synchronize()
+    t_ext = (time.perf_counter() - t0) / args.steps
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        rep = get_intensity_representation(ext, coll)
+        trainer.step(bt, rep, mel_len_max=Tm)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = torch.tensor([time.perf_counter() - t0], device="cuda")
+    fr = torch.tensor([frames_local], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        dist.all_reduce(fr, op=dist.ReduceOp.SUM)
+    el = float(el.item())
+    fl = extractor_flops(args.batch, Tm, rc["hidden_dim"], rc["n_encoder_layers"],
+                         rc["kernel_size"])
+    return {"value": float(fr.item()) * args.steps / el, "unit": "mel-frames/s",
+            "ms_per_step": el / args.steps * 1e3,
+            "extractor_ms": t_ext * 1e3, "extractor_flop": fl,
+            "extractor_tflops": fl / t_ext / 1e12,
+            "note": "train step + frozen IntensityExtractor fwd + phoneme averaging "
+                    "(train.py:69-81); extractor weights random-init, rank_X from the batch"}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -87,9 +136,9 @@ def main():
     from fastspeech2 import load_config
     from fastspeech2.model import FastSpeech2
     from fastspeech2.train import FusedTrainer
-    from fastspeech2.synthetic import make_batch, as_tuple
+    from fastspeech2.synthetic import make_batch, as_tuple, as_collate
     from fastspeech2.timing import KernelTimer
-    from fastspeech2.flops import train_flops
+    from fastspeech2.flops import train_flops, extractor_flops
     cfg_all = load_config()
     dt = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     torch.manual_seed(0)
@@ -125,6 +174,9 @@ def main():
     elapsed = float(tmax.item())
     frames_all = float(ftot.item())
     loss_v = loss.float().cpu().tolist()
+    ext_info = None
+    if not args.no_extractor:
+        ext_info = extractor_leg(cfg_all, args, trainer, b, bt, Tm, dt, world, frames_local)
     if rank == 0:
         c = model.cfg
         D, F, KW = c.dec_d_model, c.dec_ffn_dim, c.ffn_cnn_kernel_size_list[0]
@@ -158,6 +210,8 @@ def main():
             "kernel_ms": {k: v[1] for k, v in ks.items()},
             "loss_total_last": loss_v[0],
         }
+        if ext_info is not None:
+            line["with_intensity_extractor"] = ext_info
         if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(cfg_all, args)
         print(json.dumps(line), flush=True)

@@ -7,7 +7,8 @@
 //   key_padding_mask = srcmask
 // torch reads the (B*nhead) attn_mask batch-major, so for batch z = b*H + h the key k is
 // masked iff key_pad[b][k] OR key_pad[(b*H + h) % B][k]  (verified with
-// torch in this container).  A fully masked row yields NaN, as torch's softmax does.
+// torch in this container) -- mask_mode 1.  mask_mode 0 is plain key padding (key_pad[b][k]),
+// the IntensityExtractor's src_key_padding_mask (rank_model/model.py:35,101).  A fully masked row yields NaN, as torch's softmax does.
 //
 // One wave per (z, query) row; scores fp32, probabilities stored in the activation dtype.
 // Dropout: fs2_keep_fast over element index row * round_up(Tk, 2) + k (same draw as flash.hip).
@@ -17,7 +18,7 @@ namespace {
 
 template <typename T>
 __global__ void __launch_bounds__(256) softmax_fwd_kernel(const float* S, const uint8_t* kp,
-                                                          int B, int H, int Tq, int Tk, int ldt,
+                                                          int tiled, int B, int H, int Tq, int Tk, int ldt,
                                                           float scale, float p_drop,
                                                           uint32_t seed, uint32_t salt, T* P,
                                                           T* Pd, long nrows) {
@@ -26,7 +27,7 @@ __global__ void __launch_bounds__(256) softmax_fwd_kernel(const float* S, const 
   if (row >= nrows) return;
   const int z = (int)(row / Tq);
   const int b = z / H, h = z - b * H;
-  const int b2 = (b * H + h) % B;
+  const int b2 = tiled ? (b * H + h) % B : b;
   const uint8_t* k1 = kp + (long)b * Tk;
   const uint8_t* k2 = kp + (long)b2 * Tk;
   const float* s = S + row * ldt;
@@ -89,7 +90,8 @@ __global__ void __launch_bounds__(256) softmax_bwd_kernel(const float* dPd, cons
 
 }  // namespace
 
-extern "C" int fs2_softmax_fwd(const float* S, const uint8_t* key_pad, int B, int H, int Tq,
+extern "C" int fs2_softmax_fwd(const float* S, const uint8_t* key_pad, int mask_mode, int B,
+                               int H, int Tq,
                                int Tk, int ldt, float scale, float p_drop, uint32_t seed,
                                uint32_t salt, void* P, void* Pd, int dtype, void* stream) {
   if (B <= 0 || Tq <= 0) return 0;
@@ -98,10 +100,10 @@ extern "C" int fs2_softmax_fwd(const float* S, const uint8_t* key_pad, int B, in
   dim3 grid((unsigned)((nrows + 3) / 4));
   hipStream_t s = (hipStream_t)stream;
   if (dtype == FS2_BF16)
-    hipLaunchKernelGGL(softmax_fwd_kernel<bf16>, grid, dim3(256), 0, s, S, key_pad, B, H, Tq, Tk,
+    hipLaunchKernelGGL(softmax_fwd_kernel<bf16>, grid, dim3(256), 0, s, S, key_pad, mask_mode != 0, B, H, Tq, Tk,
                        ldt, scale, p_drop, seed, salt, (bf16*)P, (bf16*)Pd, nrows);
   else if (dtype == FS2_F32)
-    hipLaunchKernelGGL(softmax_fwd_kernel<float>, grid, dim3(256), 0, s, S, key_pad, B, H, Tq, Tk,
+    hipLaunchKernelGGL(softmax_fwd_kernel<float>, grid, dim3(256), 0, s, S, key_pad, mask_mode != 0, B, H, Tq, Tk,
                        ldt, scale, p_drop, seed, salt, (float*)P, (float*)Pd, nrows);
   else return FS2_EINVAL;
   FS2_CHECK_LAUNCH();

@@ -4,7 +4,8 @@
 // Replaces, for the bf16 train path, the QK^T GEMM + masked softmax + dropout + PV GEMM of
 // torch nn.MultiheadAttention as SB calls it (model.py:338-346, 411-427),
 // with the reference's head-major mask tiling: for z = b*H + h the key k is
-// masked iff key_pad[b][k] | key_pad[(b*H + h) % B][k].  Dropout on the probabilities uses
+// masked iff key_pad[b][k] | key_pad[(b*H + h) % B][k] (mask_mode 1), or with plain key padding
+// key_pad[b][k] (mask_mode 0: the IntensityExtractor's MHA, rank_model/model.py:35).  Dropout on the probabilities uses
 // the same pair hash (fs2_keep_fast) and element index ((z*T + q)*round_up(T, 2) + k) as the
 // materialised path (attention.hip), so both paths draw identical masks.
 //
@@ -41,6 +42,7 @@ constexpr int TMAX = 2048;
 struct AttnP {
   const bf16* qkv; long ldq;
   const uint8_t* kpad;
+  int tiled;                     // mask_mode: 1 head-major tiling quirk, 0 plain padding
   const bf16* o; long ldo;       // forward: written; backward: read
   bf16* out; long ldout;         // forward: O
   const bf16* dout; long lddo;   // backward: dO
@@ -153,7 +155,7 @@ __device__ __forceinline__ float xg_sum(float v) {
 // key-valid flags for (b, h) and the end of the last valid key
 __device__ __forceinline__ int build_kvalid(uint8_t* kval, int* kend_s, const AttnP& p, int b,
                                             int h) {
-  const int b2 = (b * p.H + h) % p.B;
+  const int b2 = p.tiled ? (b * p.H + h) % p.B : b;
   const uint8_t* k1 = p.kpad + (long)b * p.T;
   const uint8_t* k2 = p.kpad + (long)b2 * p.T;
   if (threadIdx.x == 0) *kend_s = 0;
@@ -614,14 +616,14 @@ extern "C" int fs2_attn_supported(int T, int dh, int dtype) {
          (dh == 64 || dh == 128 || dh == 192 || dh == 256);
 }
 
-extern "C" int fs2_attn_fwd(const void* qkv, int64_t ldq, const uint8_t* key_pad, int B, int H,
-                            int T, int dh, float scale, float p_drop, uint32_t seed,
+extern "C" int fs2_attn_fwd(const void* qkv, int64_t ldq, const uint8_t* key_pad, int mask_mode,
+                            int B, int H, int T, int dh, float scale, float p_drop, uint32_t seed,
                             uint32_t salt, void* out, int64_t ldo, float* lse, int dtype,
                             void* stream) {
   if (int rc = check(B, H, T, dh, ldq, qkv, dtype)) return rc;
   if (!key_pad || !out || !lse || !a16(out) || (ldo % 8)) return FS2_EINVAL;
   AttnP p{};
-  p.qkv = (const bf16*)qkv; p.ldq = ldq; p.kpad = key_pad;
+  p.qkv = (const bf16*)qkv; p.ldq = ldq; p.kpad = key_pad; p.tiled = mask_mode != 0;
   p.out = (bf16*)out; p.ldout = ldo; p.lse = lse;
   p.B = B; p.H = H; p.T = T; p.D = H * dh;
   p.scale = scale; p.scale_log2 = scale * LOG2E; p.p_drop = p_drop;
@@ -639,7 +641,7 @@ extern "C" int fs2_attn_fwd(const void* qkv, int64_t ldq, const uint8_t* key_pad
   return 0;
 }
 
-extern "C" int fs2_attn_bwd(const void* qkv, int64_t ldq, const uint8_t* key_pad,
+extern "C" int fs2_attn_bwd(const void* qkv, int64_t ldq, const uint8_t* key_pad, int mask_mode,
                             const void* out, int64_t ldo, const void* dout, int64_t lddo,
                             const float* lse, int B, int H, int T, int dh, float scale,
                             float p_drop, uint32_t seed, uint32_t salt, void* dqkv,
@@ -649,7 +651,7 @@ extern "C" int fs2_attn_bwd(const void* qkv, int64_t ldq, const uint8_t* key_pad
   if (!a16(out) || !a16(dout) || !a16(dqkv) || (ldo % 8) || (lddo % 8) || (lddq % 8))
     return FS2_EALIGN;
   AttnP p{};
-  p.qkv = (const bf16*)qkv; p.ldq = ldq; p.kpad = key_pad;
+  p.qkv = (const bf16*)qkv; p.ldq = ldq; p.kpad = key_pad; p.tiled = mask_mode != 0;
   p.o = (const bf16*)out; p.ldo = ldo;
   p.dout = (const bf16*)dout; p.lddo = lddo;
   p.dqkv = (bf16*)dqkv; p.lddq = lddq;

@@ -75,6 +75,14 @@ __device__ __forceinline__ u32x4 add_f32x4(u32x4 a, u32x4 b) {
   return __builtin_bit_cast(u32x4, fa + fb);
 }
 
+// epilogue activation: 1 ReLU (SB pos_ffn, model.py:241-267), 2 GELU with erf
+// (nn.GELU() of the IntensityExtractor FFN, rank_model/model.py:30,42)
+__device__ __forceinline__ float epi_act(float v, int act) {
+  if (act == 1) return fmaxf(v, 0.f);
+  if (act == 2) return 0.5f * v * (1.f + erff(v * 0.70710678118654752f));
+  return v;
+}
+
 template <typename T>
 struct Cfg {
   static constexpr int ES = sizeof(T);
@@ -109,6 +117,9 @@ __device__ __forceinline__ void load_kmajor(u32x4 (&st)[4], const char* base, lo
         if (cmode == 1) {
           const int ts = reflect_idx(t + j - P, T_);
           v = ld16(base + ((long)(b * T_ + ts) * ld + c) * ES);
+        } else if (cmode == 5) {  // zero-padded "same" conv (nn.Conv1d(padding=k//2))
+          const int ts = t + j - P;
+          if (ts >= 0 && ts < T_) v = ld16(base + ((long)(b * T_ + ts) * ld + c) * ES);
         } else if (cmode == 4) {  // shift conv over the padded domain, zero outside [0,T)
           const int ts = t - j;
           if (ts >= 0 && ts < T_) v = ld16(base + ((long)(b * T_ + ts) * ld + c) * ES);
@@ -251,7 +262,7 @@ __device__ __forceinline__ void glds_kmajor(char* lds, const char* base, long ld
           const int ts = reflect_idx(rt[i] + j - p.conv_p, T_);
           src = base + ((long)(rb[i] * T_ + ts) * ld + c) * 2;
         } else {
-          const int ts = rt[i] - j;
+          const int ts = cmode == 5 ? rt[i] + j - p.conv_p : rt[i] - j;
           if (ts >= 0 && ts < T_) src = base + ((long)(rb[i] * T_ + ts) * ld + c) * 2;
         }
       }
@@ -389,7 +400,7 @@ __global__ void __launch_bounds__(NT) gemm_kernel(GemmP p) {
 
   // conv row coordinates for the K-major A loader (rows fixed per block)
   int rb[4] = {0, 0, 0, 0}, rt[4] = {0, 0, 0, 0};
-  const int amode = (p.conv_mode == 1 || p.conv_mode == 2 || p.conv_mode == 4) ? p.conv_mode : 0;
+  const int amode = (p.conv_mode == 1 || p.conv_mode == 2 || p.conv_mode == 4 || p.conv_mode == 5) ? p.conv_mode : 0;
   if (AK && amode) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -511,7 +522,7 @@ __global__ void __launch_bounds__(NT) gemm_kernel(GemmP p) {
           if (n >= p.nvalid) continue;
           float v = acc[i][j][r];
           if (p.bias) v += p.bias[n];
-          if (p.relu) v = fmaxf(v, 0.f);
+          v = epi_act(v, p.relu);
           if (p.gate) v = (to_f(((const T*)p.gate)[(long)m * p.ldg + n]) > 0.f) ? v : 0.f;
           v *= rs;
           if (Rb) v += to_f(((const T*)Rb)[(long)m * p.ldr + n]);
@@ -577,7 +588,7 @@ __global__ void __launch_bounds__(NT) gemm_kernel(GemmP p) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       float x = v[e];
-      if (p.relu) x = fmaxf(x, 0.f);
+      x = epi_act(x, p.relu);
       if (p.gate) x = (g[e] > 0.f) ? x : 0.f;
       x *= rs;
       if (Rb) x += rr[e];
@@ -625,53 +636,6 @@ __device__ __forceinline__ bf16x8 frag_bf16_mnmajor512(const char* lds, int r0, 
   typedef __attribute__((ext_vector_type(8))) short s16x8;
   const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   return __builtin_bit_cast(bf16x8, v);
-}
-
-// MN-major tile of 64 k-rows x (ROWB bytes): 1 KiB pieces of 1024/ROWB rows
-template <int ROWB>
-__device__ __forceinline__ void glds_mn_piece(char* lds, const char* base, long ld, int mn0, int nmn,
-                                              int k0, int kend, const GemmP& p, bool conv3,
-                                              int piece, int lane) {
-  constexpr int CPR = ROWB / 16, RPP = 1024 / ROWB;
-  const int kr = piece * RPP + lane / CPR;
-  const int lc = (lane % CPR) ^ mn_swz<bf16>(kr);
-  const int k = k0 + kr;
-  const int mn = mn0 + lc * 8;
-  const char* src = g_fs2_zero;
-  if (k < kend && mn < nmn) {
-    long srow = k;
-    int col = mn;
-    if (conv3) {
-      const int j = mn / p.conv_c;
-      col = mn - j * p.conv_c;
-      const int b = k / p.conv_t, t = k - b * p.conv_t;
-      srow = (long)b * p.conv_t + reflect_idx(t + j - p.conv_p, p.conv_t);
-    }
-    src = base + (srow * ld + col) * 2;
-  }
-  glds16(src, lds + piece * 1024);
-}
-
-// K-major piece: 8 rows x 128 B
-__device__ __forceinline__ void glds_k_piece(char* lds, const char* base, long ld, int row0,
-                                             int nrows, int k0, int kend, const GemmP& p,
-                                             int cmode, int b, int t, int piece, int lane) {
-  const int r = piece * 8 + (lane >> 3);
-  const int lc = (lane & 7) ^ (r & 7);
-  const int row = row0 + r;
-  const int k = k0 + lc * 8;
-  const char* src = g_fs2_zero;
-  if (row < nrows && k < kend) {
-    if (cmode == 0) {
-      src = base + ((long)row * ld + k) * 2;
-    } else {
-      const int C = p.conv_c, T_ = p.conv_t;
-      const int j = k / C, c = k - j * C;
-      const int ts = reflect_idx(t + j - p.conv_p, T_);
-      src = base + ((long)(b * T_ + ts) * ld + c) * 2;
-    }
-  }
-  glds16(src, lds + piece * 1024);
 }
 
 // Epilogue of a 256-row x 128-column fp32 tile staged in LDS (cs[row][col ^ swz], 512 threads):
@@ -726,7 +690,7 @@ __device__ __forceinline__ void epilogue_256x128(const GemmP& p, const float* cs
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       float x = v[e];
-      if (p.relu) x = fmaxf(x, 0.f);
+      x = epi_act(x, p.relu);
       if (p.gate) x = (g[e] > 0.f) ? x : 0.f;
       x *= rs;
       if (Rb) x += rr[e];
@@ -770,7 +734,7 @@ __global__ void __launch_bounds__(BNT) gemm_big_kernel(GemmP p) {
   const char* Bb = p.B + (zb * p.sB1 + zh * p.sB2) * 2;
   const int K = p.K;
   const int kva = min(K, p.kvalid);
-  const int amode = CM >= 0 ? CM : ((p.conv_mode == 1 || p.conv_mode == 4) ? p.conv_mode : 0);
+  const int amode = CM >= 0 ? CM : ((p.conv_mode == 1 || p.conv_mode == 4 || p.conv_mode == 5) ? p.conv_mode : 0);
   // split-K: this block reduces k-tiles [kt0, kt1) and accumulates with fp32 atomics
   const int nk_all = (K + 63) / 64;
   int kt0 = 0, kt1 = nk_all;
@@ -860,7 +824,7 @@ __global__ void __launch_bounds__(BNT) gemm_big_kernel(GemmP p) {
             if (amode == 1) {
               ts = reflect_idx(at[i] + j - p.conv_p, p.conv_t);
             } else {
-              ts = at[i] - j;
+              ts = amode == 5 ? at[i] + j - p.conv_p : at[i] - j;
               ok = ok && ts >= 0 && ts < p.conv_t;
             }
             avo[i] = ok ? (int)(((long)(abt[i] + ts) * p.lda + alc[i] * 8) * 2) : BUF_OOB;
@@ -889,7 +853,7 @@ __global__ void __launch_bounds__(BNT) gemm_big_kernel(GemmP p) {
           if (amode == 1) {
             ts = reflect_idx(at[i] + j - p.conv_p, p.conv_t);
           } else {
-            ts = at[i] - j;
+            ts = amode == 5 ? at[i] + j - p.conv_p : at[i] - j;
             ok = ok && ts >= 0 && ts < p.conv_t;
           }
           const int vo = ok ? (int)(((long)(abt[i] + ts) * p.lda + c) * 2) : BUF_OOB;
@@ -1045,7 +1009,7 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256_kernel(GemmP p) {
   const char* Bb = p.B + (zb * p.sB1 + zh * p.sB2) * 2;
   const int K = p.K;
   const int kva = min(K, p.kvalid);
-  const int amode = CM >= 0 ? CM : ((p.conv_mode == 1 || p.conv_mode == 4) ? p.conv_mode : 0);
+  const int amode = CM >= 0 ? CM : ((p.conv_mode == 1 || p.conv_mode == 4 || p.conv_mode == 5) ? p.conv_mode : 0);
   const int nk_all = (K + 63) / 64;
   int kt0 = 0, kt1 = nk_all;
   if (p.split_k > 1) {
@@ -1134,7 +1098,7 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256_kernel(GemmP p) {
             if (amode == 1) {
               ts = reflect_idx(at[i] + j - p.conv_p, p.conv_t);
             } else {
-              ts = at[i] - j;
+              ts = amode == 5 ? at[i] + j - p.conv_p : at[i] - j;
               ok = ok && ts >= 0 && ts < p.conv_t;
             }
             avo[i] = ok ? (int)(((long)(abt[i] + ts) * p.lda + ac[i] * 8) * 2) : BUF_OOB;
@@ -1163,7 +1127,7 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256_kernel(GemmP p) {
           if (amode == 1) {
             ts = reflect_idx(at[i] + j - p.conv_p, p.conv_t);
           } else {
-            ts = at[i] - j;
+            ts = amode == 5 ? at[i] + j - p.conv_p : at[i] - j;
             ok = ok && ts >= 0 && ts < p.conv_t;
           }
           const int vo = ok ? (int)(((long)(abt[i] + ts) * p.lda + c) * 2) : BUF_OOB;
@@ -1317,7 +1281,8 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256_kernel(GemmP p) {
 // taps aligned to the k-granule, -1 anything else (run-time generic path)
 int conv_variant(const GemmP& q, int granule) {
   if (q.conv_mode == 0 || q.conv_mode == 3) return 0;
-  if ((q.conv_mode == 1 || q.conv_mode == 4) && q.conv_c % granule == 0) return q.conv_mode;
+  if ((q.conv_mode == 1 || q.conv_mode == 4 || q.conv_mode == 5) && q.conv_c % granule == 0)
+    return q.conv_mode;
   return -1;
 }
 
@@ -1383,6 +1348,7 @@ int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
         if (cm == 0) hipLaunchKernelGGL((gemm256_kernel<true, true, 0, 0>), g2, dim3(G4_NT), 0, s, q);
         else if (cm == 1) hipLaunchKernelGGL((gemm256_kernel<true, true, 1, 0>), g2, dim3(G4_NT), 0, s, q);
         else if (cm == 4) hipLaunchKernelGGL((gemm256_kernel<true, true, 4, 0>), g2, dim3(G4_NT), 0, s, q);
+        else if (cm == 5) hipLaunchKernelGGL((gemm256_kernel<true, true, 5, 0>), g2, dim3(G4_NT), 0, s, q);
         else hipLaunchKernelGGL((gemm256_kernel<true, true, -1, -1>), g2, dim3(G4_NT), 0, s, q);
       } else if (!ak && !bk) {
         if (q.conv_mode == 3) hipLaunchKernelGGL((gemm256_kernel<false, false, 0, 1>), g2, dim3(G4_NT), 0, s, q);
@@ -1417,6 +1383,7 @@ int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
         if (cm == 0) hipLaunchKernelGGL((gemm_big_kernel<true, true, 0, 0>), g2, dim3(BNT), 0, s, q);
         else if (cm == 1) hipLaunchKernelGGL((gemm_big_kernel<true, true, 1, 0>), g2, dim3(BNT), 0, s, q);
         else if (cm == 4) hipLaunchKernelGGL((gemm_big_kernel<true, true, 4, 0>), g2, dim3(BNT), 0, s, q);
+        else if (cm == 5) hipLaunchKernelGGL((gemm_big_kernel<true, true, 5, 0>), g2, dim3(BNT), 0, s, q);
         else hipLaunchKernelGGL((gemm_big_kernel<true, true, -1, -1>), g2, dim3(BNT), 0, s, q);
       } else if (!ak && !bk) {
         if (q.conv_mode == 3) hipLaunchKernelGGL((gemm_big_kernel<false, false, 0, 1>), g2, dim3(BNT), 0, s, q);
@@ -1480,10 +1447,11 @@ extern "C" int fs2_gemm(const fs2_gemm_desc* d, void* stream) {
   if (!d->b_kmajor && (p.N % epc)) return FS2_EINVAL;
   if (p.conv_mode) {
     if (p.conv_t <= 0 || p.conv_kw <= 0 || p.conv_c <= 0 || (p.conv_c % epc)) return FS2_EINVAL;
-    if (p.conv_mode != 4 && p.conv_p >= p.conv_t) return FS2_EINVAL;  // reflect pad needs pad < T
-    if ((p.conv_mode == 1 || p.conv_mode == 2) && (!d->a_kmajor || p.K != p.conv_kw * p.conv_c))
+    if ((p.conv_mode == 1 || p.conv_mode == 2 || p.conv_mode == 3) && p.conv_p >= p.conv_t)
+      return FS2_EINVAL;  // reflect pad needs pad < T
+    if ((p.conv_mode == 1 || p.conv_mode == 2 || p.conv_mode == 5) && (!d->a_kmajor || p.K != p.conv_kw * p.conv_c))
       return FS2_EINVAL;
-    if ((p.conv_mode == 1 || p.conv_mode == 2) && (p.M % p.conv_t)) return FS2_EINVAL;
+    if ((p.conv_mode == 1 || p.conv_mode == 2 || p.conv_mode == 5) && (p.M % p.conv_t)) return FS2_EINVAL;
     if (p.conv_mode == 4 && (p.M % (p.conv_t + 2 * p.conv_p))) return FS2_EINVAL;
     if (p.conv_mode == 4 && !d->a_kmajor) return FS2_EINVAL;
     if (p.conv_mode == 4 && p.K != p.conv_kw * p.conv_c) return FS2_EINVAL;

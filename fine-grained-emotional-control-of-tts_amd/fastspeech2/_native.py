@@ -83,11 +83,11 @@ SIGNATURES = {
                        I, I, I, U32, P, P]),
     "fs2_ln_workspace_floats": (I64, [I, I]),
     "fs2_attn_supported": (I, [I, I, I]),
-    "fs2_attn_fwd": (I, [P, I64, P, I, I, I, I, Fl, Fl, U32, U32, P, I64, P, I, P]),
-    "fs2_attn_bwd": (I, [P, I64, P, P, I64, P, I64, P, I, I, I, I, Fl, Fl, U32, U32, P, I64, P,
-                         I, P]),
+    "fs2_attn_fwd": (I, [P, I64, P, I, I, I, I, I, Fl, Fl, U32, U32, P, I64, P, I, P]),
+    "fs2_attn_bwd": (I, [P, I64, P, I, P, I64, P, I64, P, I, I, I, I, Fl, Fl, U32, U32, P, I64,
+                         P, I, P]),
     "fs2_attn_workspace_floats": (I64, [I, I, I]),
-    "fs2_softmax_fwd": (I, [P, P, I, I, I, I, I, Fl, Fl, U32, U32, P, P, I, P]),
+    "fs2_softmax_fwd": (I, [P, P, I, I, I, I, I, I, Fl, Fl, U32, U32, P, P, I, P]),
     "fs2_softmax_bwd": (I, [P, P, I, I, I, I, I, Fl, Fl, U32, U32, P, I, P]),
     "fs2_embed_fwd": (I, [P, P, P, I, I, I, I, P, P, I, P]),
     "fs2_embed_bwd": (I, [P, P, P, I, I, I, P, I, P]),
@@ -109,6 +109,9 @@ SIGNATURES = {
     "fs2_loss_workspace_floats": (I64, [I, I, I]),
     "fs2_adamw": (I, [P, P, P, P, I64, Fl, Fl, Fl, Fl, Fl, Fl, Fl, Fl, P]),
     "fs2_weight_prep": (I, [P, I, I, I, I, P, I, P, I, I, P]),
+    "fs2_intensity_input": (I, [P, I, I, I, I, P, I, I, P]),
+    "fs2_intensity_head": (I, [P, I64, P, P, P, P, P, I, I, I, I, P, I, P]),
+    "fs2_phoneme_average": (I, [P, I, I, P, P, I, I, P, P]),
     "fs2_fill": (I, [P, I64, Fl, I, P]),
     "fs2_add": (I, [P, P, I64, Fl, I, P]),
     "fs2_cast": (I, [P, I, P, I, I64, P]),

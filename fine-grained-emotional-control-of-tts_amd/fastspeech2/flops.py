@@ -24,3 +24,12 @@ def forward_flops(cfg, B, Tp, Tm):
 
 def train_flops(cfg, B, Tp, Tm):
     return 3 * forward_flops(cfg, B, Tp, Tm)
+
+
+def extractor_flops(B, T, hidden, n_layers, kernel, n_in=82, n_emo=5):
+    """Frozen IntensityExtractor forward (rank_model/model.py:96-109) over the padded (B, T)
+    frames: input projection, per layer QKV + out projection 8TD^2, scores + context 4T^2D,
+    two k-tap convs D<->4D 2*2*k*T*D*4D; classifier."""
+    D = hidden
+    per_layer = 8 * T * D * D + 4 * T * T * D + 2 * 2 * kernel * T * D * 4 * D
+    return B * (2 * T * n_in * D + n_layers * per_layer + 2 * T * D * n_emo)

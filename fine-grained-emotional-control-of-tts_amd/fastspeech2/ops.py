@@ -99,25 +99,28 @@ def attn_supported(T, dh, dt):
     return bool(N.lib().fs2_attn_supported(T, dh, dt))
 
 
-def attn_fwd(qkv, ldq, key_pad, B, H, T, dh, scale, p_drop, seed, salt, out, ldo, lse, *, dt):
-    _chk(N.lib().fs2_attn_fwd(_p(qkv), ldq, _p(key_pad), B, H, T, dh, scale, p_drop,
+def attn_fwd(qkv, ldq, key_pad, B, H, T, dh, scale, p_drop, seed, salt, out, ldo, lse, *, dt,
+             mask_mode=1):
+    """mask_mode 1: the FS2 head-major tiling quirk; 0: plain key padding."""
+    _chk(N.lib().fs2_attn_fwd(_p(qkv), ldq, _p(key_pad), mask_mode, B, H, T, dh, scale, p_drop,
                               seed & 0xffffffff, salt, _p(out), ldo, _p(lse), dt, _s()),
          "fs2_attn_fwd")
 
 
 def attn_bwd(qkv, ldq, key_pad, out, ldo, dout, lddo, lse, B, H, T, dh, scale, p_drop, seed, salt,
-             dqkv, lddq, *, dt, ws):
-    _chk(N.lib().fs2_attn_bwd(_p(qkv), ldq, _p(key_pad), _p(out), ldo, _p(dout), lddo, _p(lse), B,
-                              H, T, dh, scale, p_drop, seed & 0xffffffff, salt, _p(dqkv), lddq,
-                              _p(ws), dt, _s()), "fs2_attn_bwd")
+             dqkv, lddq, *, dt, ws, mask_mode=1):
+    _chk(N.lib().fs2_attn_bwd(_p(qkv), ldq, _p(key_pad), mask_mode, _p(out), ldo, _p(dout), lddo,
+                              _p(lse), B, H, T, dh, scale, p_drop, seed & 0xffffffff, salt,
+                              _p(dqkv), lddq, _p(ws), dt, _s()), "fs2_attn_bwd")
 
 
 def attn_ws(B, H, T):
     return N.lib().fs2_attn_workspace_floats(B, H, T)
 
 
-def softmax_fwd(S, key_pad, B, H, Tq, Tk, ldt, scale, p_drop, seed, salt, P, Pd, *, dt):
-    _chk(N.lib().fs2_softmax_fwd(_p(S), _p(key_pad), B, H, Tq, Tk, ldt, scale, p_drop,
+def softmax_fwd(S, key_pad, B, H, Tq, Tk, ldt, scale, p_drop, seed, salt, P, Pd, *, dt,
+                mask_mode=1):
+    _chk(N.lib().fs2_softmax_fwd(_p(S), _p(key_pad), mask_mode, B, H, Tq, Tk, ldt, scale, p_drop,
                                  seed & 0xffffffff, salt, _p(P), _p(Pd), dt, _s()), "fs2_softmax_fwd")
 
 
@@ -221,6 +224,21 @@ def adamw(param, grad, m, v, n, decay_mul, omb1, beta2, omb2, step_size, bc2_sqr
 def weight_prep(W, O, C, KW, Wf, ldf, Wb, ldb, *, dt, w_okc=0):
     _chk(N.lib().fs2_weight_prep(_p(W), O, C, KW, w_okc, _p(Wf), ldf, _p(Wb), ldb, dt, _s()),
          "fs2_weight_prep")
+
+
+def intensity_input(x, layout_bct, B, T, C, X, ldx, *, dt):
+    _chk(N.lib().fs2_intensity_input(_p(x), layout_bct, B, T, C, _p(X), ldx, dt, _s()),
+         "fs2_intensity_input")
+
+
+def intensity_head(H, ldh, emo_table, emotions, lengths, Wc, bc, B, T, D, E, I, *, dt):
+    _chk(N.lib().fs2_intensity_head(_p(H), ldh, _p(emo_table), _p(emotions), _p(lengths), _p(Wc),
+                                    _p(bc), B, T, D, E, _p(I), dt, _s()), "fs2_intensity_head")
+
+
+def phoneme_average(I, T, E, durations, phon_len, B, Tp, out):
+    _chk(N.lib().fs2_phoneme_average(_p(I), T, E, _p(durations), _p(phon_len), B, Tp, _p(out),
+                                     _s()), "fs2_phoneme_average")
 
 
 def fill(X, n, value, *, dt):

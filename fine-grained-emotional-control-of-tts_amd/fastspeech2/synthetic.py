@@ -9,7 +9,8 @@ durations summing exactly to each mel length (MFA alignments).  ``intensity`` is
 Draws: tokens ~ U{1..n_char-1} (0 = pad), T_phon ~ U{tp_min..tp_max}, durations ~ U{1..9}
 rescaled so that sum <= t_mel_cap, mel ~ N(-4, 2) clipped to [-11.5, 2.5] (log-mel range),
 pitch / energy ~ N(0, 1) with 15 % unvoiced (exact zero) pitch frames, speakers ~ U{0..n_spk-1},
-intensity ~ N(0, 1) (zeros if ``emotion=False``).
+intensity ~ N(0, 1) (zeros if ``emotion=False``), emotion ids ~ U{0..4}; ``rank_x`` is the collate's
+(B, n_mels + 2, T_mel) extractor input built from mel / pitch / energy.
 """
 
 import torch
@@ -61,9 +62,14 @@ def make_batch(B=32, tp_min=100, tp_max=200, t_mel_cap=1000, n_mels=80, n_char=9
         pitch[b, :L] = p
         energy[b, :L] = torch.randn(L, generator=g)
     speakers = torch.randint(0, n_spk, (B,), generator=g)
+    emotions = torch.randint(0, 5, (B,), generator=g)     # drawn last: earlier fields unchanged
+    # rank_X as the collate builds it: cat(mel^T, pitch, energy) -> (B, n_mels + 2, T_mel)
+    # (dataset.py:94,116-117), the frozen IntensityExtractor's input (train.py:27)
+    rank_x = torch.cat([mel.transpose(1, 2), pitch[:, None], energy[:, None]], dim=1)
     batch = dict(phoneme=phoneme, speakers=speakers, phon_len=torch.tensor(tps, dtype=torch.long),
                  mel=mel, pitch=pitch, energy=energy, duration=duration,
-                 mel_len=torch.tensor(mel_lens, dtype=torch.long), intensity=intensity)
+                 mel_len=torch.tensor(mel_lens, dtype=torch.long), intensity=intensity,
+                 rank_x=rank_x, emotions=emotions)
     return {k: v.to(device) for k, v in batch.items()}
 
 
@@ -71,6 +77,13 @@ def as_tuple(batch):
     """The reference train loop's 8 leading collate fields (train.py:62-65) + intensity."""
     return ((batch["phoneme"], batch["speakers"], batch["phon_len"], batch["mel"], batch["pitch"],
              batch["energy"], batch["duration"], batch["mel_len"]), batch["intensity"])
+
+
+def as_collate(batch):
+    """The reference collate's full 12-tuple (dataset.py:120-133; labels / wavs are None)."""
+    return (batch["phoneme"], batch["speakers"], batch["phon_len"], batch["mel"], batch["pitch"],
+            batch["energy"], batch["duration"], batch["mel_len"], None, None, batch["rank_x"],
+            batch["emotions"])
 
 
 def valid_frames(batch):

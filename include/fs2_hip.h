@@ -51,12 +51,14 @@ typedef struct fs2_gemm_desc {
    *   3: B wgrad B(k=(b,t), n=(j,c)) = X[b, reflect(t+j-P), c]                  (!b_kmajor)
    *   4: A shift A(m=(b,p), k=(j,o)) = dY[b, p-j, o] (0 outside [0,T)), T+2P rows per
    *      utterance: the data gradient in the padded domain, finished by fs2_conv_fold
+   *   5: A fwd   A(m=(b,t), k=(j,c)) = X[b, t+j-P, c], 0 outside [0,T): zero-padded "same"
+   *      conv (torch nn.Conv1d(padding=k//2), IntensityExtractor FFN, rank_model/model.py:23-24)
    * P = (conv_kw-1)/2, conv_c = channels per tap, conv_t = tokens per utterance.          */
   int conv_mode, conv_t, conv_kw, conv_c;
   void* C; int64_t ldc; int c_fp32;           /* output; c_fp32: float output else dtype     */
   int c_conv_kw;        /* >0: output column n=(j,c) is stored at c*c_conv_kw + j            */
   const float* bias;    /* [N]       v += bias[n]                                             */
-  int relu;             /*           v = max(v, 0)                                            */
+  int relu;             /* 1: v = max(v, 0); 2: v = GELU(v) = v/2 (1 + erf(v/sqrt 2))        */
   const void* gate; int64_t ldg;              /* dtype [M][ldg]: v *= (gate > 0)             */
   const float* row_scale;                     /* [M]: v *= row_scale[m]                      */
   const void* residual; int64_t ldr;          /* dtype [M][ldr]: v += residual               */
@@ -113,13 +115,15 @@ int64_t fs2_ln_workspace_floats(int M, int D);
 /* ------------------------------------------------------------------------------------------
  * Attention softmax over materialised scores, with the reference's key masking
  * (model.py:338-343 / 414-419 + key_padding_mask; head-major tiling quirk):
- *   batch z = b*H + h masks key k iff key_pad[b][k] || key_pad[(b*H+h) % B][k].
+ *   mask_mode 1: batch z = b*H + h masks key k iff key_pad[b][k] || key_pad[(b*H+h) % B][k];
+ *   mask_mode 0: plain key padding key_pad[b][k] (IntensityExtractor MHA,
+ *                rank_model/model.py:35,101).
  * S: fp32 [z][Tq][ldt]; P, Pd: dtype [z][Tq][ldt] (softmax and dropped softmax, zero-padded
  * to ldt); scale applied to S before the softmax (torch MHA q-scaling).
  * ------------------------------------------------------------------------------------------ */
-int fs2_softmax_fwd(const float* S, const uint8_t* key_pad, int B, int H, int Tq, int Tk,
-                    int ldt, float scale, float p_drop, uint32_t seed, uint32_t salt, void* P,
-                    void* Pd, int dtype, void* stream);
+int fs2_softmax_fwd(const float* S, const uint8_t* key_pad, int mask_mode, int B, int H, int Tq,
+                    int Tk, int ldt, float scale, float p_drop, uint32_t seed, uint32_t salt,
+                    void* P, void* Pd, int dtype, void* stream);
 /* dS = scale * P * (dP - rowsum(P*dP)) with dP = dPd * dropmask / (1-p). dPd fp32.        */
 int fs2_softmax_bwd(const float* dPd, const void* P, int B, int H, int Tq, int Tk, int ldt,
                     float scale, float p_drop, uint32_t seed, uint32_t salt, void* dS, int dtype,
@@ -135,10 +139,11 @@ int fs2_softmax_bwd(const float* dPd, const void* P, int B, int H, int Tq, int T
  * (fs2_attn_supported); workspace: fs2_attn_workspace_floats.
  * ------------------------------------------------------------------------------------------ */
 int fs2_attn_supported(int T, int dh, int dtype);
-int fs2_attn_fwd(const void* qkv, int64_t ldq, const uint8_t* key_pad, int B, int H, int T,
-                 int dh, float scale, float p_drop, uint32_t seed, uint32_t salt, void* out,
-                 int64_t ldo, float* lse, int dtype, void* stream);
-int fs2_attn_bwd(const void* qkv, int64_t ldq, const uint8_t* key_pad, const void* out,
+int fs2_attn_fwd(const void* qkv, int64_t ldq, const uint8_t* key_pad, int mask_mode, int B,
+                 int H, int T, int dh, float scale, float p_drop, uint32_t seed, uint32_t salt,
+                 void* out, int64_t ldo, float* lse, int dtype, void* stream);
+int fs2_attn_bwd(const void* qkv, int64_t ldq, const uint8_t* key_pad, int mask_mode,
+                 const void* out,
                  int64_t ldo, const void* dout, int64_t lddo, const float* lse, int B, int H,
                  int T, int dh, float scale, float p_drop, uint32_t seed, uint32_t salt,
                  void* dqkv, int64_t lddq, float* workspace, int dtype, void* stream);
@@ -246,6 +251,27 @@ int fs2_adamw(float* param, const float* grad, float* exp_avg, float* exp_avg_sq
  * [O][C][KW] (w_okc = 0) or [O][KW][C] (w_okc = 1, the flat-buffer layout of conv weights). */
 int fs2_weight_prep(const float* W, int O, int C, int KW, int w_okc, void* Wf, int ldf, void* Wb,
                     int ldb, int dtype, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Frozen IntensityExtractor forward pieces + phoneme averaging (SURVEY §8f-1;
+ * rank_model/model.py:96-109, fastspeech2/train.py:16-51).  The extractor's GEMMs use
+ * fs2_gemm (conv_mode 5 zero-padded k=9 convs, relu=2 GELU), fs2_attn_fwd / fs2_softmax_fwd
+ * with mask_mode 0, and fs2_ln_fwd (eps 1e-5).
+ * ------------------------------------------------------------------------------------------ */
+/* rank_X fp32 (B,T,C) (layout_bct=0) or the collate's (B,C,T) (layout_bct=1, the explicit fix of
+ * SURVEY App. B-2) -> GEMM rows X[B*T][ldx] in dtype, columns >= C zero.                    */
+int fs2_intensity_input(const float* x, int layout_bct, int B, int T, int C, void* X, int ldx,
+                        int dtype, void* stream);
+/* I[b,t,e] = (t < lengths[b]) ? (H[b,t] + emo_table[emotions[b]]) . Wc[e] + bc[e] : bc[e]
+ * (model.py:103-107: emotion embedding add, masked_fill, classifier); I fp32 (B,T,E), E <= 8 */
+int fs2_intensity_head(const void* H, int64_t ldh, const float* emo_table,
+                       const int64_t* emotions, const int64_t* lengths, const float* Wc,
+                       const float* bc, int B, int T, int D, int E, float* I, int dtype,
+                       void* stream);
+/* out[b,p,:] = sum of I[b, t, :] over phoneme p's frames [sum d[:p], sum d[:p+1]) (clipped to
+ * T) / max(d[b,p], 1) for p < phon_len[b]; 0 otherwise (train.py:33-49). Tp <= 1024.        */
+int fs2_phoneme_average(const float* I, int T, int E, const int64_t* durations,
+                        const int64_t* phon_len, int B, int Tp, float* out, void* stream);
 
 /* utilities */
 int fs2_fill(void* X, int64_t n, float value, int dtype, void* stream);

@@ -152,3 +152,51 @@ def test_phoneme_average_intensity():
     torch.testing.assert_close(out[0, 2], I[0, 3:7].mean(0))
     torch.testing.assert_close(out[1, 1], I[1, 5])
     assert torch.all(out[1, 2:] == 0)
+
+
+def _intensity_golden(golden_dir):
+    z = np.load(os.path.join(golden_dir, "intensity_ref.npz"))
+    cfg = {k: v for k, v in zip(z["cfg_keys"].tolist(), z["cfg_vals"].tolist())}
+    sd = {k[3:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("sd.")}
+    return z, cfg, sd
+
+
+def test_intensity_extractor_oracle_matches_reference(golden_dir):
+    """oracle/intensity_oracle.py vs outputs of the REFERENCE IntensityExtractor
+    (rank_model/model.py:96-109) on seeded weights, both input layouts (App. B-2 fix)."""
+    from oracle.intensity_oracle import extractor_forward
+    z, cfg, sd = _intensity_golden(golden_dir)
+    x = torch.from_numpy(z["x"])
+    args = (torch.from_numpy(z["lengths"]), torch.from_numpy(z["emotions"]),
+            int(cfg["n_heads"]), int(cfg["n_encoder_layers"]))
+    I = extractor_forward(sd, x, *args)
+    np.testing.assert_allclose(I.numpy(), z["I"], rtol=1e-5, atol=1e-5)
+    I2 = extractor_forward(sd, x.transpose(1, 2).contiguous(), *args, layout="BCT")
+    np.testing.assert_allclose(I2.numpy(), z["I"], rtol=1e-5, atol=1e-5)
+
+
+def test_phoneme_average_matches_reference(golden_dir):
+    """Both restatements of train.py:29-49 vs the reference function's own output."""
+    from oracle.intensity_oracle import phoneme_average_np
+    z, _, _ = _intensity_golden(golden_dir)
+    I, d, pl = torch.from_numpy(z["I"]), torch.from_numpy(z["duration"]), torch.from_numpy(z["phon_len"])
+    np.testing.assert_allclose(phoneme_average_intensity(I, d, pl).numpy(), z["rep"], rtol=1e-6,
+                               atol=1e-6)
+    np.testing.assert_allclose(phoneme_average_np(z["I"], z["duration"], z["phon_len"]), z["rep"],
+                               rtol=1e-5, atol=1e-6)
+
+
+def test_intensity_container_keys_match_reference(golden_dir):
+    """The drop-in IntensityExtractor / RankModel containers carry the reference's state_dict
+    keys and shapes, so reference checkpoints load (train.py:218-221)."""
+    from fastspeech2.intensity import IntensityExtractor, RankModel
+    z, cfg, sd = _intensity_golden(golden_dir)
+    kw = {k: (v if k == "dropout" else int(v)) for k, v in cfg.items()}
+    m = IntensityExtractor(**kw)
+    ours = m.state_dict()
+    assert list(ours) == list(sd)
+    for k in sd:
+        assert ours[k].shape == sd[k].shape, k
+    m.load_state_dict(sd)
+    rm = RankModel(**kw)
+    assert set(rm.state_dict()) == {"intensity_extractor." + k for k in sd} | {"projector.weight"}
