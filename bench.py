@@ -34,6 +34,8 @@ def parse():
     ap.add_argument("--max-shape", action="store_true", help="all T_phon=200, d=5 (T_mel=1000)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-utts", type=int, default=2)
+    ap.add_argument("--detail", action="store_true",
+                    help="HIP-event time every GEMM / attention call site; table on stderr")
     ap.add_argument("--no-extractor", action="store_true",
                     help="skip the second timed loop that adds the frozen IntensityExtractor")
     return ap.parse_args()
@@ -78,12 +80,39 @@ def pmc_traffic():
     return d["hbm_bytes_per_launch"], os.path.relpath(hits[-1], ROOT)
 
 
+def detail_table(ks, eng, B, steps, elapsed):
+    """Per-call-site time (ms/step) and achieved TFLOP/s of every tagged GEMM / attention."""
+    rows = []
+    D = eng.cfg.enc_d_model
+    for tag, (n, ms) in ks.items():
+        if ":" not in tag:
+            continue
+        kind, wname, T = tag.split(":")
+        T = int(T[1:])
+        M = B * T
+        if kind.startswith("attn"):
+            H = eng.cfg.dec_num_head
+            fl = 4.0 * B * T * T * D * (1 if kind == "attn_fwd" else 2.5)
+        else:
+            O, C, KW = eng._wspecs[wname.replace("layers.*", "layers.0")]
+            fl = 2.0 * M * O * C * KW
+        per_step = n / steps
+        rows.append((ms * per_step, tag, per_step, ms, fl / (ms * 1e-3) / 1e12))
+    rows.sort(reverse=True)
+    tot = sum(r[0] for r in rows)
+    print(f"# detail: step {elapsed / steps * 1e3:.2f} ms; tagged {tot:.2f} ms/step", file=sys.stderr)
+    for r in rows:
+        print(f"{r[0]:8.3f} ms/step {r[2]:5.1f}x {r[3] * 1e3:8.1f} us {r[4]:7.1f} TF/s  {r[1]}",
+              file=sys.stderr)
+
+
 def extractor_leg(cfg_all, args, trainer, b, bt, Tm, dt, world, frames_local):
     """The reference train loop body INCLUDING the frozen IntensityExtractor forward + phoneme
     averaging (train.py:69-81), timed the same way over ``steps`` steps.  Reported
     beside ``value`` (whose definition, SURVEY 8d, excludes the extractor)."""
     from fastspeech2.intensity import IntensityExtractor, get_intensity_representation
     from fastspeech2.flops import extractor_flops
+    from fastspeech2.synthetic import as_collate
     rc = cfg_all["model"]["rank_model"]
     torch.manual_seed(1)
     ext = IntensityExtractor(cfg_all["audio"]["n_mels"], rc["n_heads"], 5, rc["n_encoder_layers"],
@@ -153,6 +182,7 @@ def main():
         trainer.step(bt, inten, mel_len_max=Tm)
     torch.cuda.synchronize()
     timer = KernelTimer()
+    timer.detail = args.detail
     trainer.eng.timer = timer
     if world > 1:
         dist.barrier()
@@ -166,6 +196,8 @@ def main():
     elapsed = time.perf_counter() - t0
     trainer.eng.timer = None
     ks = timer.summary()
+    if args.detail and rank == 0:
+        detail_table(ks, trainer.eng, args.batch, args.steps, elapsed)
     tmax = torch.tensor([elapsed], device="cuda")
     ftot = torch.tensor([frames_local], dtype=torch.float64, device="cuda")
     if world > 1:

@@ -15,6 +15,7 @@ gradients, LayerNorm statistics and losses are fp32 in both.
 
 import math
 import os
+import re
 
 import torch
 
@@ -134,14 +135,33 @@ class FS2Engine:
                             w_okc=int(KW > 1))
         self._prepared_version = ver
 
+    def _dtag(self, kind, wname, T):
+        """per-call-site tag for the detailed timer (FS2 layer indices folded)"""
+        if self.timer is None or not getattr(self.timer, "detail", False):
+            return None
+        return f"{kind}:{re.sub(r'layers[.][0-9]+', 'layers.*', wname)}:T{T}"
+
     def _fwd(self, X, ldx, M, T, wname, out, ldo, **epi):
         O, C, KW = self._wspecs[wname]
         Wf, _ = self.w[wname]
         K = Wf.shape[1]
         conv = (1, T, KW, C) if KW > 1 else None
+        tag = self._dtag("fwd", wname, T)
+        if tag:
+            self._tic(tag)
         ops.gemm(M, O, K, X, ldx, Wf, K, out, ldo, dt=self.dt, conv=conv, **epi)
+        if tag:
+            self._toc(tag)
 
     def _dgrad(self, dY, lddy, M, T, wname, out, ldo, n_out=None, **epi):
+        tag = self._dtag("dgrad", wname, T)
+        if tag:
+            self._tic(tag)
+        self._dgrad_impl(dY, lddy, M, T, wname, out, ldo, n_out, **epi)
+        if tag:
+            self._toc(tag)
+
+    def _dgrad_impl(self, dY, lddy, M, T, wname, out, ldo, n_out=None, **epi):
         O, C, KW = self._wspecs[wname]
         _, Wb = self.w[wname]
         if KW == 1:
@@ -163,6 +183,14 @@ class FS2Engine:
                       split_stride=Mp * C)
 
     def _wgrad(self, dY, lddy, X, ldx, M, T, wname, n_cols=None):
+        tag = self._dtag("wgrad", wname, T)
+        if tag:
+            self._tic(tag)
+        self._wgrad_impl(dY, lddy, X, ldx, M, T, wname, n_cols)
+        if tag:
+            self._toc(tag)
+
+    def _wgrad_impl(self, dY, lddy, X, ldx, M, T, wname, n_cols=None):
         """grad[O][KW][C] += sum_m dY[m][o] * X[reflect(t+j-P)][c]   (fp32, accumulate)."""
         O, C, KW = self._wspecs[wname]
         Ncols = n_cols or KW * C
@@ -196,8 +224,13 @@ class FS2Engine:
             # fused attention: no (B*H, T, T) tensors; lse kept for the backward
             lse = torch.empty(B * H, T, dtype=torch.float32, device=self.dev)
             s_att = salt()
+            tag = self._dtag("attn_fwd", "", T)
+            if tag:
+                self._tic(tag)
             ops.attn_fwd(QKV, 3 * D, key_pad, B, H, T, dh, 1.0 / math.sqrt(dh), p_drop, seed,
                          s_att, Att, D, lse, dt=self.dt)
+            if tag:
+                self._toc(tag)
             Pm = Pd = None
             ctx.update(lse=lse, key_pad=key_pad)
         else:
@@ -286,9 +319,14 @@ class FS2Engine:
         QKV, Pm, Pd = ctx["QKV"], ctx["Pm"], ctx["Pd"]
         if "lse" in ctx:     # fused attention backward (dQ, dK, dV in one pass each)
             dQKV = self.empty(M, 3 * D)
+            tag = self._dtag("attn_bwd", "", T)
+            if tag:
+                self._tic(tag)
             ops.attn_bwd(QKV, 3 * D, ctx["key_pad"], ctx["Att"], D, dAtt, D, ctx["lse"], B, H, T,
                          dh, 1.0 / math.sqrt(dh), p_drop, seed, ctx["s_att"], dQKV, 3 * D,
                          dt=self.dt, ws=self.ws(ops.attn_ws(B, H, T)))
+            if tag:
+                self._toc(tag)
             return self._qkv_bwd(dQKV, ctx, M, T, D, prefix, ds1)
         # ---- attention backward over the materialised probabilities
         dPd = torch.empty(B * H, T, ldt, dtype=torch.float32, device=self.dev)
