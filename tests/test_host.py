@@ -127,3 +127,16 @@ def test_flop_count_matches_survey(cfg_all):
     m = FastSpeech2(**cfg_all["model"]["fastspeech2"], n_speakers=4)
     f = forward_flops(m.cfg, 1, 200, 1000)
     assert abs(f / 1e9 - 112.9) < 0.5     # 112.9 GFLOP per utterance forward
+
+
+def test_get_intensity_rep_prototype_lookup():
+    """fastspeech2/inference.py:12-21: prototype bank lookup expanded over the phonemes;
+    neutral -> zeros with n_emotions (=5) channels (the reference's 256 is the App. fix)."""
+    import numpy as np
+    from fastspeech2.inference import get_intensity_rep
+    bank = np.random.default_rng(0).standard_normal((4, 5, 3, 5)).astype(np.float32)
+    z = get_intensity_rep(1, 0, 2, 7, bank)
+    assert z.shape == (1, 7, 5) and torch.all(z == 0)
+    r = get_intensity_rep(2, 3, 1, 7, bank)
+    assert r.shape == (1, 7, 5)
+    assert torch.equal(r[0, 4], torch.from_numpy(bank[2, 3, 1]))
