@@ -112,6 +112,8 @@ SIGNATURES = {
     "fs2_intensity_input": (I, [P, I, I, I, I, P, I, I, P]),
     "fs2_intensity_head": (I, [P, I64, P, P, P, P, P, I, I, I, I, P, I, P]),
     "fs2_phoneme_average": (I, [P, I, I, P, P, I, I, P, P]),
+    "fs2_collate_phonemes": (I, [P, P, P, P, I, I, P, P, P, P]),
+    "fs2_collate_frames": (I, [P, P, P, P, P, I, I, I, P, P, P, P, P, P]),
     "fs2_fill": (I, [P, I64, Fl, I, P]),
     "fs2_add": (I, [P, P, I64, Fl, I, P]),
     "fs2_cast": (I, [P, I, P, I, I64, P]),

@@ -241,6 +241,19 @@ def phoneme_average(I, T, E, durations, phon_len, B, Tp, out):
                                      _s()), "fs2_phoneme_average")
 
 
+def collate_phonemes(order, offsets, phonemes, durations, B, Tp, phon_out, dur_out, in_len):
+    _chk(N.lib().fs2_collate_phonemes(_p(order), _p(offsets), _p(phonemes), _p(durations), B, Tp,
+                                      _p(phon_out), _p(dur_out), _p(in_len), _s()),
+         "fs2_collate_phonemes")
+
+
+def collate_frames(order, frame_offsets, mel, pitch, energy, B, Tm, n_mels, mel_out, pitch_out,
+                   energy_out, rank_x, out_len):
+    _chk(N.lib().fs2_collate_frames(_p(order), _p(frame_offsets), _p(mel), _p(pitch), _p(energy),
+                                    B, Tm, n_mels, _p(mel_out), _p(pitch_out), _p(energy_out),
+                                    _p(rank_x), _p(out_len), _s()), "fs2_collate_frames")
+
+
 def fill(X, n, value, *, dt):
     _chk(N.lib().fs2_fill(_p(X), n, value, dt, _s()), "fs2_fill")
 

@@ -273,6 +273,23 @@ int fs2_intensity_head(const void* H, int64_t ldh, const float* emo_table,
 int fs2_phoneme_average(const float* I, int T, int E, const int64_t* durations,
                         const int64_t* phon_len, int B, int Tp, float* out, void* stream);
 
+/* ------------------------------------------------------------------------------------------
+ * GPU collate: TextMelCollateWithAlignment (fastspeech2/dataset.py:62-133) over
+ * one packed upload.  Item u's phonemes / durations are [offsets[u], offsets[u+1]) of the
+ * packed int64 arrays; its mel is (n_mels, T_u) channel-major at frame_offsets[u] * n_mels,
+ * pitch / energy at frame_offsets[u].  order[i] = item placed at batch row i (the collate's
+ * descending torch.sort of phoneme lengths).  Outputs are zero padded: phoneme / duration
+ * (B, Tp) int64, mel (B, Tm, n_mels) (the collate's permute(0,2,1), contiguous), pitch /
+ * energy (B, Tm), rank_x (B, n_mels+2, Tm) = cat(mel, pitch, energy), lengths (B,) int64.
+ * ------------------------------------------------------------------------------------------ */
+int fs2_collate_phonemes(const int32_t* order, const int64_t* offsets, const int64_t* phonemes,
+                         const int64_t* durations, int B, int Tp, int64_t* phoneme_padded,
+                         int64_t* duration_padded, int64_t* input_lengths, void* stream);
+int fs2_collate_frames(const int32_t* order, const int64_t* frame_offsets, const float* mel,
+                       const float* pitch, const float* energy, int B, int Tm, int n_mels,
+                       float* mel_padded, float* pitch_padded, float* energy_padded,
+                       float* rank_x, int64_t* output_lengths, void* stream);
+
 /* utilities */
 int fs2_fill(void* X, int64_t n, float value, int dtype, void* stream);
 /* X[i] += alpha * Y[i] over n elements of dtype                                           */

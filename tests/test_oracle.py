@@ -200,3 +200,17 @@ def test_intensity_container_keys_match_reference(golden_dir):
     m.load_state_dict(sd)
     rm = RankModel(**kw)
     assert set(rm.state_dict()) == {"intensity_extractor." + k for k in sd} | {"projector.weight"}
+
+
+def test_collate_oracle_matches_reference(golden_dir):
+    """oracle/collate_oracle.py vs the reference TextMelCollateWithAlignment's own output
+    (dataset.py:62-133, run by make_golden_collate.py), bit-exact incl. tie order."""
+    from oracle.collate_oracle import collate_np, items_from_golden
+    z = np.load(os.path.join(golden_dir, "collate_ref.npz"))
+    out = collate_np(items_from_golden(z))
+    for k, v in out.items():
+        ref = z["out_" + k]
+        if k in ("labels", "wavs"):
+            assert list(v) == [str(s) for s in ref.tolist()], k
+        else:
+            assert np.array_equal(np.asarray(v), ref), k
