@@ -60,7 +60,68 @@ __global__ void weight_prep_kernel(const float* W, int O, int C, int KW, int okc
   }
 }
 
+// one block per 64x64 tile (o, k = j*C + c) of one weight's forward image; the weight is found
+// by binary search over the descriptor prefix sums (staged in LDS)
+template <typename T>
+__global__ void __launch_bounds__(256) weight_prep_batched_kernel(const fs2_wprep_desc* descs,
+                                                                  int n) {
+  __shared__ int t0s[256];
+  __shared__ float tile[64][65];
+  for (int i = threadIdx.x; i < n; i += blockDim.x) t0s[i] = descs[i].tile0;
+  __syncthreads();
+  const int blk = blockIdx.x;
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {               // last descriptor with tile0 <= blk
+    const int mid = (lo + hi + 1) >> 1;
+    if (t0s[mid] <= blk) lo = mid; else hi = mid - 1;
+  }
+  const fs2_wprep_desc d = descs[lo];
+  const int t = blk - d.tile0;
+  const int to = t / d.tiles_k, tk = t - to * d.tiles_k;
+  const int o0 = to * 64, k0 = tk * 64;
+  const int KC = d.KW * d.C;
+  T* Wf = (T*)d.Wf;
+  // read (coalesced along k for the [O][KW][C] layout) -> Wf, and stage for the transpose
+  for (int i = threadIdx.x; i < 64 * 64; i += blockDim.x) {
+    const int ol = i >> 6, kl = i & 63, o = o0 + ol, k = k0 + kl;
+    if (o >= d.O || k >= d.ldf) continue;
+    float v = 0.f;
+    if (k < KC) {
+      const int j = k / d.C, c = k - j * d.C;
+      v = d.w_okc ? d.W[(long)o * KC + k] : d.W[((long)o * d.C + c) * d.KW + j];
+    }
+    Wf[(long)o * d.ldf + k] = from_f<T>(v);
+    tile[ol][kl] = v;
+  }
+  if (!d.Wb) return;
+  __syncthreads();
+  // Wb[c][j*O + o]: consecutive threads take consecutive o
+  T* Wb = (T*)d.Wb;
+  for (int i = threadIdx.x; i < 64 * 64; i += blockDim.x) {
+    const int kl = i >> 6, ol = i & 63, o = o0 + ol, k = k0 + kl;
+    if (o >= d.O || k >= KC) continue;
+    const int j = k / d.C, c = k - j * d.C;
+    Wb[(long)c * d.ldb + (long)j * d.O + o] = from_f<T>(tile[ol][kl]);
+  }
+}
+
 }  // namespace
+
+extern "C" int fs2_weight_prep_batched(const fs2_wprep_desc* descs, int n, int total_tiles,
+                                       int dtype, void* stream) {
+  if (n == 0 || total_tiles == 0) return 0;
+  if (!descs || n < 0 || n > 256 || total_tiles < 0) return FS2_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == FS2_BF16)
+    hipLaunchKernelGGL(weight_prep_batched_kernel<bf16>, dim3(total_tiles), dim3(256), 0, s,
+                       descs, n);
+  else if (dtype == FS2_F32)
+    hipLaunchKernelGGL(weight_prep_batched_kernel<float>, dim3(total_tiles), dim3(256), 0, s,
+                       descs, n);
+  else return FS2_EINVAL;
+  FS2_CHECK_LAUNCH();
+  return 0;
+}
 
 extern "C" int fs2_adamw(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
                          int64_t n, float decay_mul, float one_minus_beta1, float beta2,

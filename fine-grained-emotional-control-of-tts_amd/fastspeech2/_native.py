@@ -65,6 +65,15 @@ class LossDesc(ctypes.Structure):
     ]
 
 
+class WPrepDesc(ctypes.Structure):
+    _fields_ = [
+        ("W", ctypes.c_void_p), ("Wf", ctypes.c_void_p), ("Wb", ctypes.c_void_p),
+        ("O", ctypes.c_int), ("C", ctypes.c_int), ("KW", ctypes.c_int), ("w_okc", ctypes.c_int),
+        ("ldf", ctypes.c_int), ("ldb", ctypes.c_int), ("tile0", ctypes.c_int),
+        ("tiles_k", ctypes.c_int),
+    ]
+
+
 P = ctypes.c_void_p
 I = ctypes.c_int
 I64 = ctypes.c_int64
@@ -109,6 +118,7 @@ SIGNATURES = {
     "fs2_loss_workspace_floats": (I64, [I, I, I]),
     "fs2_adamw": (I, [P, P, P, P, I64, Fl, Fl, Fl, Fl, Fl, Fl, Fl, Fl, P]),
     "fs2_weight_prep": (I, [P, I, I, I, I, P, I, P, I, I, P]),
+    "fs2_weight_prep_batched": (I, [P, I, I, I, P]),
     "fs2_intensity_input": (I, [P, I, I, I, I, P, I, I, P]),
     "fs2_intensity_head": (I, [P, I64, P, P, P, P, P, I, I, I, I, P, I, P]),
     "fs2_phoneme_average": (I, [P, I, I, P, P, I, I, P, P]),

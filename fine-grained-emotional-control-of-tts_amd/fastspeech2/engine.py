@@ -76,6 +76,7 @@ class FS2Engine:
         self.w = {}
         self._wspecs = self._weight_specs()
         self._prepared_version = None
+        self._wtable = None          # device descriptor table of every GEMM weight image
         self.on_grads_ready = None   # optional callback(tag) for DP overlap
         self.timer = None            # optional KernelTimer: HIP events around tagged launches
 
@@ -130,18 +131,24 @@ class FS2Engine:
         return specs
 
     def prepare_weights(self, force=False):
-        """fp32 master weights -> K-major GEMM images in the activation dtype (fwd + dgrad)."""
+        """fp32 master weights -> K-major GEMM images in the activation dtype (fwd + dgrad), all
+        weights in one fs2_weight_prep_batched launch per parameter update."""
         ver = (self.m._param_version, self.m._flat._version)
         if not force and self._prepared_version == ver:
             return
-        for name, (O, C, KW) in self._wspecs.items():
-            ldf = round_up(KW * C, self.epc)
-            ldb = KW * O
-            if name not in self.w:
-                self.w[name] = (self.empty(O, ldf), self.empty(C, ldb))
-            Wf, Wb = self.w[name]
-            ops.weight_prep(self.params[name], O, C, KW, Wf, ldf, Wb, ldb, dt=self.dt,
-                            w_okc=int(KW > 1))
+        if self._wtable is None:
+            entries = []
+            for name, (O, C, KW) in self._wspecs.items():
+                ldf = round_up(KW * C, self.epc)
+                ldb = KW * O
+                if name not in self.w:
+                    self.w[name] = (self.empty(O, ldf), self.empty(C, ldb))
+                Wf, Wb = self.w[name]
+                W = self.params[name]
+                # conv weights are [O][KW][C] in the flat buffer (model._kw_major)
+                entries.append((W, O, C, KW, int(KW > 1), Wf, ldf, Wb, ldb))
+            self._wtable = ops.weight_prep_table(entries)
+        ops.weight_prep_batched(*self._wtable, dt=self.dt)
         self._prepared_version = ver
 
     def _dtag(self, kind, wname, T):

@@ -254,6 +254,26 @@ def collate_frames(order, frame_offsets, mel, pitch, energy, B, Tm, n_mels, mel_
                                     _p(rank_x), _p(out_len), _s()), "fs2_collate_frames")
 
 
+def weight_prep_table(entries):
+    """Device table of fs2_wprep_desc for fs2_weight_prep_batched.  entries: list of
+    (W, O, C, KW, w_okc, Wf, ldf, Wb, ldb); returns (table tensor, n, total_tiles).  The tensors
+    must stay alive (and in place) as long as the table is used."""
+    arr = (N.WPrepDesc * len(entries))()
+    t0 = 0
+    for i, (W, O, C, KW, okc, Wf, ldf, Wb, ldb) in enumerate(entries):
+        tk = (ldf + 63) // 64
+        arr[i] = N.WPrepDesc(_p(W), _p(Wf), _p(Wb), O, C, KW, okc, ldf, ldb, t0, tk)
+        t0 += ((O + 63) // 64) * tk
+    raw = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
+    dev = entries[0][0].device
+    return raw.to(dev), len(entries), t0
+
+
+def weight_prep_batched(table, n, total_tiles, *, dt):
+    _chk(N.lib().fs2_weight_prep_batched(_p(table), n, total_tiles, dt, _s()),
+         "fs2_weight_prep_batched")
+
+
 def fill(X, n, value, *, dt):
     _chk(N.lib().fs2_fill(_p(X), n, value, dt, _s()), "fs2_fill")
 

@@ -252,6 +252,19 @@ int fs2_adamw(float* param, const float* grad, float* exp_avg, float* exp_avg_sq
 int fs2_weight_prep(const float* W, int O, int C, int KW, int w_okc, void* Wf, int ldf, void* Wb,
                     int ldb, int dtype, void* stream);
 
+/* All of a model's weight images in ONE launch: descs (DEVICE memory) lists n weights, each
+ * cut into 64 x 64 tiles of its [O][ldf] forward image; tile0 = first tile index of weight i
+ * (prefix sum, ascending), tiles_k = ceil(ldf / 64).  Each tile is read once (coalesced),
+ * written to Wf, and transposed through LDS into Wb (coalesced along o); Wb may be NULL.
+ * total_tiles = tile0 + tiles of the last weight; n <= 256.                               */
+typedef struct fs2_wprep_desc {
+  const float* W; void* Wf; void* Wb;
+  int O, C, KW, w_okc, ldf, ldb;
+  int tile0, tiles_k;
+} fs2_wprep_desc;
+int fs2_weight_prep_batched(const fs2_wprep_desc* descs, int n, int total_tiles, int dtype,
+                            void* stream);
+
 /* ------------------------------------------------------------------------------------------
  * Frozen IntensityExtractor forward pieces + phoneme averaging (SURVEY §8f-1;
  * rank_model/model.py:96-109, fastspeech2/train.py:16-51).  The extractor's GEMMs use
