@@ -186,40 +186,63 @@ __device__ __forceinline__ void norm_xy(const LossP& p, int b, int t, int f, flo
 }
 
 // ---- 3: SSIM map and its partial derivatives wrt the prediction's local statistics --------
+// Separable Gaussian: a block takes SSIM_TI output rows of one utterance, stages the
+// normalised X / Y of the SSIM_TI + 10 input rows in LDS, filters along the mel axis (5 moment
+// planes), then along time -- 2 x 11 taps per moment instead of 121.
+constexpr int SSIM_TI = 16;
+constexpr int SSIM_MAXW = 96;                  // n_mels <= 96
+constexpr int SSIM_R = SSIM_TI + WIN - 1;
 template <typename T>
 __global__ void __launch_bounds__(256) ssim_map_kernel(LossP p) {
   __shared__ float sh[8];
   __shared__ float w1[WIN];
+  __shared__ float xs[SSIM_R][SSIM_MAXW], ys[SSIM_R][SSIM_MAXW];
+  __shared__ float hs[5][SSIM_R][SSIM_MAXW - WIN + 1];
   if (threadIdx.x < WIN) w1[threadIdx.x] = gauss1(threadIdx.x);
+  const int b = blockIdx.y, i0 = blockIdx.x * SSIM_TI;
+  const int NM = p.NM, OW = NM - (WIN - 1), OH = p.Tm - (WIN - 1);
+  for (int idx = threadIdx.x; idx < SSIM_R * NM; idx += blockDim.x) {
+    const int r = idx / NM, f = idx - r * NM, t = i0 + r;
+    float X = 0.f, Y = 0.f;
+    if (t < p.Tm) norm_xy<T>(p, b, t, f, X, Y);
+    xs[r][f] = X;
+    ys[r][f] = Y;
+  }
   __syncthreads();
-  const int b = blockIdx.y;
-  const int OW = p.NM - (WIN - 1);
-  const int pix = blockIdx.x * blockDim.x + threadIdx.x;
-  float ss = 0.f;
-  if (pix < p.npix) {
-    const int i = pix / OW, j = pix - i * OW;
+  for (int idx = threadIdx.x; idx < SSIM_R * OW; idx += blockDim.x) {
+    const int r = idx / OW, j = idx - r * OW;
     float mx = 0.f, my = 0.f, exx = 0.f, eyy = 0.f, exy = 0.f;
-    for (int di = 0; di < WIN; ++di) {
-      for (int dj = 0; dj < WIN; ++dj) {
-        float X, Y;
-        norm_xy<T>(p, b, i + di, j + dj, X, Y);
-        const float w = w1[di] * w1[dj];
-        mx += w * X; my += w * Y; exx += w * X * X; eyy += w * Y * Y; exy += w * X * Y;
-      }
+#pragma unroll
+    for (int dj = 0; dj < WIN; ++dj) {
+      const float w = w1[dj], X = xs[r][j + dj], Y = ys[r][j + dj];
+      mx += w * X; my += w * Y; exx += w * X * X; eyy += w * Y * Y; exy += w * X * Y;
     }
-    const float a = mx, bb = my;
+    hs[0][r][j] = mx; hs[1][r][j] = my; hs[2][r][j] = exx; hs[3][r][j] = eyy; hs[4][r][j] = exy;
+  }
+  __syncthreads();
+  float ss = 0.f;
+  const long plane = (long)p.B * p.npix;
+  for (int idx = threadIdx.x; idx < SSIM_TI * OW; idx += blockDim.x) {
+    const int ti = idx / OW, j = idx - ti * OW, i = i0 + ti;
+    if (i >= OH) continue;
+    float a = 0.f, bb = 0.f, exx = 0.f, eyy = 0.f, exy = 0.f;
+#pragma unroll
+    for (int di = 0; di < WIN; ++di) {
+      const float w = w1[di];
+      a += w * hs[0][ti + di][j]; bb += w * hs[1][ti + di][j]; exx += w * hs[2][ti + di][j];
+      eyy += w * hs[3][ti + di][j]; exy += w * hs[4][ti + di][j];
+    }
     const float sxx = exx - a * a, syy = eyy - bb * bb, sxy = exy - a * bb;
     const float L1 = 2.f * a * bb + C1, D1 = a * a + bb * bb + C1;
     const float N2 = 2.f * sxy + C2, D2 = sxx + syy + C2;
     const float cs = N2 / D2;
-    ss = (L1 / D1) * cs;
+    ss += (L1 / D1) * cs;
     const float dl_db = (2.f * a * D1 - L1 * 2.f * bb) / (D1 * D1);
     const float dn_db = (-2.f * a * D2 + 2.f * bb * N2) / (D2 * D2);
     const float Db = cs * dl_db + (L1 / D1) * dn_db;
     const float Deyy = (L1 / D1) * (-N2 / (D2 * D2));
     const float Dexy = (L1 / D1) * (2.f / D2);
-    const long o = (long)b * p.npix + pix;
-    const long plane = (long)p.B * p.npix;
+    const long o = (long)b * p.npix + (long)i * OW + j;
     p.dmap[o] = Db; p.dmap[plane + o] = Deyy; p.dmap[2 * plane + o] = Dexy;
   }
   ss = block_sum(ss, sh);
@@ -277,42 +300,63 @@ __global__ void __launch_bounds__(256) finalize_kernel(LossP p) {
 // ---- 5: gradient wrt the normalised prediction (transposed filtering) ---------------------
 template <typename T>
 __global__ void __launch_bounds__(256) ssim_grad_kernel(LossP p) {
+  // dL/dY at input rows t0 .. t0 + SSIM_TI - 1: the transposed (correlation) Gaussian of the
+  // three dmap planes over output rows t0 - 10 .. t0 + SSIM_TI - 1, separable as in the map
   __shared__ float sh[8];
   __shared__ float w1[WIN];
+  __shared__ float dsm[3][SSIM_R][SSIM_MAXW - WIN + 1];
+  __shared__ float hsm[3][SSIM_R][SSIM_MAXW];
   if (threadIdx.x < WIN) w1[threadIdx.x] = gauss1(threadIdx.x);
-  __syncthreads();
-  const int b = blockIdx.y;
+  const int b = blockIdx.y, t0 = blockIdx.x * SSIM_TI;
   const int Tm = p.Tm, NM = p.NM, B = p.B;
   const int OH = Tm - (WIN - 1), OW = NM - (WIN - 1);
-  const long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long plane = (long)B * p.npix;
+  const float* Db = p.dmap + (long)b * p.npix;
+  for (int idx = threadIdx.x; idx < SSIM_R * OW; idx += blockDim.x) {
+    const int r = idx / OW, j = idx - r * OW, i = t0 - (WIN - 1) + r;
+    const bool ok = i >= 0 && i < OH;
+    const long o = (long)i * OW + j;
+    dsm[0][r][j] = ok ? Db[o] : 0.f;
+    dsm[1][r][j] = ok ? Db[plane + o] : 0.f;
+    dsm[2][r][j] = ok ? Db[2 * plane + o] : 0.f;
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < SSIM_R * NM; idx += blockDim.x) {
+    const int r = idx / NM, f = idx - r * NM;
+    float u = 0.f, v = 0.f, w = 0.f;
+#pragma unroll
+    for (int dj = 0; dj < WIN; ++dj) {
+      const int j = f - dj;
+      if (j < 0 || j >= OW) continue;
+      const float g = w1[dj];
+      u += g * dsm[0][r][j]; v += g * dsm[1][r][j]; w += g * dsm[2][r][j];
+    }
+    hsm[0][r][f] = u; hsm[1][r][f] = v; hsm[2][r][f] = w;
+  }
+  __syncthreads();
   const float g = p.scal[0];
+  const int L = (int)min((int64_t)Tm, p.mel_len[b]);
   float s1 = 0.f, s2 = 0.f;
-  if (q < (long)Tm * NM) {
-    const int t = (int)(q / NM), f = (int)(q - (long)t * NM);
+  for (int idx = threadIdx.x; idx < SSIM_TI * NM; idx += blockDim.x) {
+    const int tt = idx / NM, f = idx - tt * NM, t = t0 + tt;
+    if (t >= Tm) continue;
+    float U = 0.f, V = 0.f, W = 0.f;
+#pragma unroll
+    for (int di = 0; di < WIN; ++di) {
+      const int r = tt + (WIN - 1) - di;
+      const float w = w1[di];
+      U += w * hsm[0][r][f]; V += w * hsm[1][r][f]; W += w * hsm[2][r][f];
+    }
     float X, Y;
     norm_xy<T>(p, b, t, f, X, Y);
-    float U = 0.f, V = 0.f, W = 0.f;
-    const long plane = (long)B * p.npix;
-    const float* Db = p.dmap + (long)b * p.npix;
-    for (int di = 0; di < WIN; ++di) {
-      const int i = t - di;
-      if (i < 0 || i >= OH) continue;
-      for (int dj = 0; dj < WIN; ++dj) {
-        const int j = f - dj;
-        if (j < 0 || j >= OW) continue;
-        const float w = w1[di] * w1[dj];
-        const long o = (long)i * OW + j;
-        U += w * Db[o]; V += w * Db[plane + o]; W += w * Db[2 * plane + o];
-      }
-    }
-    const int L = (int)min((int64_t)Tm, p.mel_len[b]);
     float dn = 0.f;
     if (t < L) dn = g * (U + 2.f * Y * V + X * W);
+    const long q = (long)t * NM + f;
     p.dnmap[(long)b * Tm * NM + q] = dn;
     if (t < L) {
       const float hv = to_f(((const T*)p.mel_out)[(long)b * Tm * NM + q]);
-      s1 = dn;
-      s2 = dn * (hv - p.stats[3 * B + b]);
+      s1 += dn;
+      s2 += dn * (hv - p.stats[3 * B + b]);
     }
   }
   s1 = block_sum(s1, sh);
@@ -356,7 +400,8 @@ int run_loss(LossP& p, hipStream_t s) {
   hipLaunchKernelGGL(ssim_map_kernel<T>, dim3(p.nblk_pix, p.B), dim3(256), 0, s, p);
   hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(256), 0, s, p);
   const unsigned nq = (unsigned)(((long)p.Tm * p.NM + 255) / 256);
-  hipLaunchKernelGGL(ssim_grad_kernel<T>, dim3(nq, p.B), dim3(256), 0, s, p);
+  hipLaunchKernelGGL(ssim_grad_kernel<T>, dim3((p.Tm + SSIM_TI - 1) / SSIM_TI, p.B), dim3(256),
+                     0, s, p);
   hipLaunchKernelGGL(ssim_apply_kernel<T>, dim3(nq, p.B), dim3(256), 0, s, p);
   FS2_CHECK_LAUNCH();
   return 0;
@@ -365,7 +410,7 @@ int run_loss(LossP& p, hipStream_t s) {
 void carve(LossP& p, float* ws) {
   const int B = p.B;
   p.npix = (p.Tm - (WIN - 1)) * (p.NM - (WIN - 1));
-  p.nblk_pix = (p.npix + 255) / 256;
+  p.nblk_pix = (p.Tm - (WIN - 1) + SSIM_TI - 1) / SSIM_TI;   // ssim_map blocks per utterance
   p.nch = (p.Tm * p.NM + LOSS_CHUNK - 1) / LOSS_CHUNK;
   float* w = ws;
   p.per_b = w; w += 5L * B;
@@ -382,7 +427,7 @@ void carve(LossP& p, float* ws) {
 
 extern "C" int64_t fs2_loss_workspace_floats(int B, int Tm, int NM) {
   const long npix = (long)(Tm - (WIN - 1)) * (NM - (WIN - 1));
-  const long nblk = (npix + 255) / 256;
+  const long nblk = (Tm - (WIN - 1) + SSIM_TI - 1) / SSIM_TI;
   const long nch = ((long)Tm * NM + LOSS_CHUNK - 1) / LOSS_CHUNK;
   return 5L * B + 2L * B * nch + 8L * B + 4 + B * nblk + 4 + 3L * B * npix + (long)B * Tm * NM;
 }
@@ -391,6 +436,7 @@ extern "C" int fs2_loss_fwd_bwd(const fs2_loss_desc* d, void* stream) {
   if (!d) return FS2_EINVAL;
   if (d->B <= 0) return 0;
   if (d->Tm < WIN || d->NM < WIN) return FS2_EINVAL;  // SSIM: kernel larger than input
+  if (d->NM > SSIM_MAXW) return FS2_EINVAL;           // SSIM LDS tiles
   if (!d->mel_out || !d->postnet_out || !d->log_dur || !d->pitch_pred || !d->energy_pred ||
       !d->mel_tgt || !d->dur_tgt || !d->pitch_avg || !d->energy_avg || !d->mel_len ||
       !d->phon_len || !d->loss_out || !d->d_mel_out || !d->d_postnet_out || !d->d_log_dur ||

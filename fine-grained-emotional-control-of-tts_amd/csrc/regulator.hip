@@ -26,14 +26,16 @@ __global__ void embed_fwd_kernel(const int64_t* tok, const float* table, const f
 // grid (V, D/64): 4 waves split the tokens; each wave ballots 64 tokens at a time and adds the
 // matching rows in token order (lane = column); fixed-order combine -> deterministic.
 template <typename T>
-__global__ void __launch_bounds__(256) embed_bwd_kernel(const int64_t* tok, const T* dX,
-                                                        const float* keep, int M, int D,
-                                                        float* dtable) {
-  __shared__ float red[4][64];
+__global__ void __launch_bounds__(1024) embed_bwd_kernel(const int64_t* tok, const T* dX,
+                                                         const float* keep, int M, int D,
+                                                         float* dtable) {
+  // block (v, 64 features): 16 waves each scan M/16 tokens (ballot of the hits, ~M/(16V)
+  // dependent row loads per wave), then a fixed-order LDS combine (deterministic)
+  __shared__ float red[16][64];
   const int v = blockIdx.x;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int d = blockIdx.y * 64 + lane;
-  const int per = (M + 3) / 4;
+  const int per = (M + 15) / 16;
   const int m0 = w * per, m1 = min(M, m0 + per);
   float s = 0.f;
   for (int base = m0; base < m1; base += 64) {
@@ -49,8 +51,12 @@ __global__ void __launch_bounds__(256) embed_bwd_kernel(const int64_t* tok, cons
   }
   red[w][lane] = s;
   __syncthreads();
-  if (w == 0 && d < D)
-    dtable[(long)v * D + d] += (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+  if (w == 0 && d < D) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t += red[i][lane];
+    dtable[(long)v * D + d] += t;
+  }
 }
 
 __global__ void keypad_tokens_kernel(const int64_t* tok, int pad, int M, uint8_t* kp) {
@@ -145,6 +151,7 @@ __global__ void __launch_bounds__(256) rowdot_bwd_kernel(const T* dy, const T* u
   const int rbeg = blockIdx.x * rows_per_block, rend = min(M, rbeg + rows_per_block);
   for (int d = threadIdx.x; d <= D; d += blockDim.x) {
     float s = 0.f;
+#pragma unroll 8
     for (int m = rbeg; m < rend; ++m) {
       const float g = to_f(dy[m]) * scale;
       s += (d < D) ? g * to_f(u[(long)m * ldu + d]) : g;
@@ -158,15 +165,27 @@ __global__ void __launch_bounds__(256) rowdot_bwd_kernel(const T* dy, const T* u
   }
 }
 
-__global__ void reduce_cols_kernel(const float* part, int nb, int N, float* out, float* out2,
-                                   int split) {
-  // out[n] += sum_b part[b][n] for n < split; out2[n - split] += ... for n >= split
-  const int n = blockIdx.x * blockDim.x + threadIdx.x;
-  if (n >= N) return;
+__global__ void __launch_bounds__(256) reduce_cols_kernel(const float* part, int nb, int N,
+                                                          float* out, float* out2, int split) {
+  // out[n] += sum_b part[b][n] for n < split; out2[n - split] += ... for n >= split.
+  // 16 columns x 16 row-slices per block, fixed-order LDS combine (deterministic)
+  __shared__ float red[16][17];
+  const int c = threadIdx.x & 15, sl = threadIdx.x >> 4;
+  const int n = blockIdx.x * 16 + c;
   float s = 0.f;
-  for (int b = 0; b < nb; ++b) s += part[(long)b * N + n];
-  if (n < split) out[n] += s;
-  else out2[n - split] += s;
+  if (n < N) {
+#pragma unroll 4
+    for (int b = sl; b < nb; b += 16) s += part[(long)b * N + n];
+  }
+  red[sl][c] = s;
+  __syncthreads();
+  if (sl == 0 && n < N) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t += red[i][c];
+    if (n < split) out[n] += t;
+    else out2[n - split] += t;
+  }
 }
 
 // ---------------------------------------------------------------- average_over_durations (K9)
@@ -381,8 +400,8 @@ extern "C" int fs2_embed_bwd(const int64_t* tokens, const void* dX, const float*
   if (!tokens || !dX || !keep || !dtable) return FS2_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   DISPATCH_T(dtype,
-    hipLaunchKernelGGL(embed_bwd_kernel<bf16>, dim3(V, (D + 63) / 64), dim3(256), 0, s, tokens, (const bf16*)dX, keep, M, D, dtable),
-    hipLaunchKernelGGL(embed_bwd_kernel<float>, dim3(V, (D + 63) / 64), dim3(256), 0, s, tokens, (const float*)dX, keep, M, D, dtable));
+    hipLaunchKernelGGL(embed_bwd_kernel<bf16>, dim3(V, (D + 63) / 64), dim3(1024), 0, s, tokens, (const bf16*)dX, keep, M, D, dtable),
+    hipLaunchKernelGGL(embed_bwd_kernel<float>, dim3(V, (D + 63) / 64), dim3(1024), 0, s, tokens, (const float*)dX, keep, M, D, dtable));
   return 0;
 }
 
@@ -470,8 +489,8 @@ extern "C" int fs2_rowdot_bwd(const void* dy, const void* u, int64_t ldu, const 
   DISPATCH_T(dtype,
     hipLaunchKernelGGL(rowdot_bwd_kernel<bf16>, dim3(nb), dim3(256), 0, s, (const bf16*)dy, (const bf16*)u, ldu, w, scale, M, D, (bf16*)du, workspace, rpb),
     hipLaunchKernelGGL(rowdot_bwd_kernel<float>, dim3(nb), dim3(256), 0, s, (const float*)dy, (const float*)u, ldu, w, scale, M, D, (float*)du, workspace, rpb));
-  hipLaunchKernelGGL(reduce_cols_kernel, dim3(nblk(D + 1)), dim3(256), 0, s, workspace, nb, D + 1,
-                     dw, db, D);
+  hipLaunchKernelGGL(reduce_cols_kernel, dim3((D + 1 + 15) / 16), dim3(256), 0, s, workspace, nb,
+                     D + 1, dw, db, D);
   FS2_CHECK_LAUNCH();
   return 0;
 }
