@@ -172,10 +172,11 @@ __device__ __forceinline__ int build_kvalid(uint8_t* kval, int* kend_s, const At
 }
 
 // ------------------------------------------------------------------------------ forward
-// block: 128 queries = (8 / QG) waves x QG 16-query groups; K/V tiles of 64 keys
-template <int DH, int QG>
-__global__ void __launch_bounds__(512 / QG, 1) attn_fwd_kernel(AttnP p) {
-  constexpr int NT = 512 / QG;
+// block: 16 * W8 queries = (W8 / QG) waves x QG 16-query groups; K/V tiles of 64 keys
+// (W8 = 8: 128 queries; W8 = 4 for short sequences, so B*H*ceil(T/64) blocks fill the chip)
+template <int DH, int QG, int W8 = 8>
+__global__ void __launch_bounds__(W8 * 64 / QG, 1) attn_fwd_kernel(AttnP p) {
+  constexpr int NT = W8 * 64 / QG;
   constexpr int NS = DH / 32, ND = DH / 16;
   constexpr int TB = 64 * DH * 2;
   // one LDS array (a second __shared__ object can make hipcc drain the DMA ring early):
@@ -196,7 +197,7 @@ __global__ void __launch_bounds__(512 / QG, 1) attn_fwd_kernel(AttnP p) {
   bf16x8 qf[QG][NS];
 #pragma unroll
   for (int qg = 0; qg < QG; ++qg) {
-    qi[qg] = blockIdx.x * 128 + wave * 16 * QG + qg * 16 + (lane & 15);
+    qi[qg] = blockIdx.x * (16 * W8) + wave * 16 * QG + qg * 16 + (lane & 15);
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
       if (qi[qg] < p.T) qf[qg][s] = ld_frag(Qb + (long)qi[qg] * p.ldq + 32 * s + 8 * g);
@@ -328,11 +329,11 @@ __global__ void __launch_bounds__(512 / QG, 1) attn_fwd_kernel(AttnP p) {
 }
 
 // ------------------------------------------------------------------------------ backward dQ
-// block: 128 queries = (8 / QG) waves x QG 16-query groups; also writes D = rowsum(dO * O)
-// for the dK/dV kernel
-template <int DH, int QG>
-__global__ void __launch_bounds__(512 / QG, 1) attn_bwd_dq_kernel(AttnP p) {
-  constexpr int NT = 512 / QG;
+// block: 16 * W8 queries = (W8 / QG) waves x QG 16-query groups; also writes
+// D = rowsum(dO * O) for the dK/dV kernel
+template <int DH, int QG, int W8 = 8>
+__global__ void __launch_bounds__(W8 * 64 / QG, 1) attn_bwd_dq_kernel(AttnP p) {
+  constexpr int NT = W8 * 64 / QG;
   constexpr int NS = DH / 32, ND = DH / 16;
   constexpr int TB = 64 * DH * 2;
   // one LDS array (a second __shared__ object can make hipcc drain the DMA ring early):
@@ -354,7 +355,7 @@ __global__ void __launch_bounds__(512 / QG, 1) attn_bwd_dq_kernel(AttnP p) {
   float lse[QG], dsum[QG];
 #pragma unroll
   for (int qg = 0; qg < QG; ++qg) {
-    qi[qg] = blockIdx.x * 128 + wave * 16 * QG + qg * 16 + (lane & 15);
+    qi[qg] = blockIdx.x * (16 * W8) + wave * 16 * QG + qg * 16 + (lane & 15);
     const bool in = qi[qg] < p.T;
     float dot = 0.f;
 #pragma unroll
@@ -475,9 +476,9 @@ __global__ void __launch_bounds__(512 / QG, 1) attn_bwd_dq_kernel(AttnP p) {
 }
 
 // ------------------------------------------------------------------------------ backward dK dV
-// block: 8 waves x 16 keys; query tiles of 64 (Q, dO, lse, D staged in LDS)
-template <int DH>
-__global__ void __launch_bounds__(512, 1) attn_bwd_dkv_kernel(AttnP p) {
+// block: W8 waves x 16 keys; query tiles of 64 (Q, dO, lse, D staged in LDS)
+template <int DH, int W8 = 8>
+__global__ void __launch_bounds__(W8 * 64, 1) attn_bwd_dkv_kernel(AttnP p) {
   constexpr int NS = DH / 32, ND = DH / 16;
   __shared__ __attribute__((aligned(16))) char Qs[64 * DH * 2];
   __shared__ __attribute__((aligned(16))) char Os[64 * DH * 2];  // dO tile
@@ -494,7 +495,7 @@ __global__ void __launch_bounds__(512, 1) attn_bwd_dkv_kernel(AttnP p) {
   const bf16* Vb = Qb + 2 * p.D;
   const bf16* dOb = p.dout + (long)b * p.T * p.lddo + h * DH;
 
-  const int key = blockIdx.x * 128 + wave * 16 + (lane & 15);   // this lane's key (B col)
+  const int key = blockIdx.x * (16 * W8) + wave * 16 + (lane & 15);   // this lane's key (B col)
   const bool kin = key < p.T;
   const bool kok = kin && kval[key];
   bf16x8 kf[NS], vf[NS];
@@ -506,13 +507,13 @@ __global__ void __launch_bounds__(512, 1) attn_bwd_dkv_kernel(AttnP p) {
   f32x4 dk[ND], dv[ND];
 #pragma unroll
   for (int d = 0; d < ND; ++d) { dk[d] = f32x4{0, 0, 0, 0}; dv[d] = f32x4{0, 0, 0, 0}; }
-  // a block whose 128 keys are all masked contributes nothing: skip the query loop
+  // a block whose keys are all masked contributes nothing: skip the query loop
   const int anyk = __syncthreads_or(kok);
 
   for (int q0 = 0; anyk && q0 < p.T; q0 += 64) {
     __syncthreads();
-    load_tile<DH, 64>(Qs, Qb, p.ldq, q0, p.T, threadIdx.x, 512);
-    load_tile<DH, 64>(Os, dOb, p.lddo, q0, p.T, threadIdx.x, 512);
+    load_tile<DH, 64>(Qs, Qb, p.ldq, q0, p.T, threadIdx.x, W8 * 64);
+    load_tile<DH, 64>(Os, dOb, p.lddo, q0, p.T, threadIdx.x, W8 * 64);
     if (threadIdx.x < 64) {
       const int q = q0 + threadIdx.x;
       ls_s[threadIdx.x] = q < p.T ? p.lse[(long)z * p.T + q] : 0.f;
@@ -567,7 +568,7 @@ __global__ void __launch_bounds__(512, 1) attn_bwd_dkv_kernel(AttnP p) {
   // C layout: col = feature (lane & 15), rows = keys 4g + r of this wave's 16
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const int kr = blockIdx.x * 128 + wave * 16 + 4 * g + r;
+    const int kr = blockIdx.x * (16 * W8) + wave * 16 + 4 * g + r;
     if (kr >= p.T) continue;
     bf16* krow = p.dqkv + ((long)b * p.T + kr) * p.lddq + p.D + h * DH;
     bf16* vrow = krow + p.D;
@@ -585,14 +586,38 @@ int attn_qg_fwd(int dh) {
   return dh <= 128 ? 2 : 1;
 }
 
+// half-size forward blocks (64 queries) when 128-row blocks would leave CUs idle (the
+// encoder: T = 200, B*H = 64 -> 128 blocks of 128 rows for 256 CUs; 26.3 -> 24.2 us)
+bool attn_small_blocks(const AttnP& p) {
+  static const int env = [] { const char* v = std::getenv("FS2_ATTN_W8"); return v ? std::atoi(v) : 0; }();
+  if (env == 4) return true;
+  if (env == 8) return false;
+  return (long)((p.T + 127) / 128) * p.B * p.H < 256;
+}
+
 template <int DH>
 void launch_fwd(const AttnP& p, hipStream_t s) {
+  if (attn_small_blocks(p)) {
+    dim3 grid((p.T + 63) / 64, p.B * p.H);
+    if (attn_qg_fwd(DH) == 2) hipLaunchKernelGGL((attn_fwd_kernel<DH, 2, 4>), grid, dim3(128), 0, s, p);
+    else hipLaunchKernelGGL((attn_fwd_kernel<DH, 1, 4>), grid, dim3(256), 0, s, p);
+    return;
+  }
   dim3 grid((p.T + 127) / 128, p.B * p.H);
   if (attn_qg_fwd(DH) == 2) hipLaunchKernelGGL((attn_fwd_kernel<DH, 2>), grid, dim3(256), 0, s, p);
   else hipLaunchKernelGGL((attn_fwd_kernel<DH, 1>), grid, dim3(512), 0, s, p);
 }
 template <int DH>
 void launch_bwd(const AttnP& p, hipStream_t s) {
+  // measured neutral for the backward at T = 200 (67.5 vs 68.4 us): only on explicit request
+  static const bool small_bwd = [] { const char* v = std::getenv("FS2_ATTN_W8"); return v && std::atoi(v) == 4; }();
+  if (small_bwd) {
+    dim3 g1((p.T + 63) / 64, p.B * p.H);
+    if (DH <= 64) hipLaunchKernelGGL((attn_bwd_dq_kernel<DH, 2, 4>), g1, dim3(128), 0, s, p);
+    else hipLaunchKernelGGL((attn_bwd_dq_kernel<DH, 1, 4>), g1, dim3(256), 0, s, p);
+    hipLaunchKernelGGL((attn_bwd_dkv_kernel<DH, 4>), g1, dim3(256), 0, s, p);
+    return;
+  }
   dim3 g1((p.T + 127) / 128, p.B * p.H);
   if (DH <= 64) hipLaunchKernelGGL((attn_bwd_dq_kernel<DH, 2>), g1, dim3(256), 0, s, p);
   else hipLaunchKernelGGL((attn_bwd_dq_kernel<DH, 1>), g1, dim3(512), 0, s, p);
