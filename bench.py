@@ -34,11 +34,24 @@ def parse():
     ap.add_argument("--max-shape", action="store_true", help="all T_phon=200, d=5 (T_mel=1000)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-utts", type=int, default=2)
+    ap.add_argument("--scaled", action="store_true",
+                    help="BASELINE config 4: scaled FastSpeech2, hidden 512, FFN 2048, 6+6 layers")
     ap.add_argument("--detail", action="store_true",
                     help="HIP-event time every GEMM / attention call site; table on stderr")
     ap.add_argument("--no-extractor", action="store_true",
                     help="skip the second timed loop that adds the frozen IntensityExtractor")
     return ap.parse_args()
+
+
+def scaled_config(cfg_all):
+    """BASELINE config 4 / SURVEY 8d: hidden 512, FFN 2048 (k/v dims follow), 6+6 layers."""
+    import copy
+    c = copy.deepcopy(cfg_all)
+    m = c["model"]["fastspeech2"]
+    for k in ("enc_d_model", "enc_k_dim", "enc_v_dim", "dec_d_model", "dec_k_dim", "dec_v_dim"):
+        m[k] = 512
+    m["enc_ffn_dim"] = m["dec_ffn_dim"] = 2048
+    return c
 
 
 def cpu_baseline(cfg_all, args):
@@ -169,6 +182,8 @@ def main():
     from fastspeech2.timing import KernelTimer
     from fastspeech2.flops import train_flops, extractor_flops
     cfg_all = load_config()
+    if args.scaled:
+        cfg_all = scaled_config(cfg_all)
     dt = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     torch.manual_seed(0)
     model = FastSpeech2(**cfg_all["model"]["fastspeech2"], n_speakers=4, act_dtype=dt).cuda().train()
@@ -215,7 +230,7 @@ def main():
         n, ms = ks.get("ffn_conv1_fwd.decoder", (0, float("nan")))
         kflop = 2.0 * (args.batch * Tm) * F * (KW * D)
         achieved = kflop / (ms * 1e-3) / 1e12 if n else None
-        traffic, traffic_src = pmc_traffic()
+        traffic, traffic_src = pmc_traffic() if not args.scaled else (None, None)
         step_ms = elapsed / args.steps * 1e3
         step_tflops = train_flops(c, args.batch, Tp, Tm) * world / (step_ms * 1e-3) / 1e12
         line = {
@@ -228,7 +243,8 @@ def main():
             "dtype": args.dtype, "data": "synthetic (seeded EmoV-DB-shaped batches, random-init weights)",
             "config": {"workload": f"FastSpeech2 train step (fwd+loss+bwd+allreduce+AdamW), "
                                    f"B={args.batch}/GPU, T_phon_max={Tp}, T_mel_max={Tm}, "
-                                   f"D=384 F=1536 6+6 FFT layers, 80 mels"
+                                   f"D={c.enc_d_model} F={c.enc_ffn_dim} "
+                                   f"{c.enc_num_layers}+{c.dec_num_layers} FFT layers, 80 mels"
                                    + (", max-shape" if args.max_shape else ""),
                        "global_batch": args.batch * world, "seq_len": Tm,
                        "valid_mel_frames_per_step": frames_all, "parallelism": f"dp{world}"},

@@ -207,3 +207,37 @@ def test_full_size_train_properties_bf16(cuda, cfg_all):
     mel = out[0].float()
     for i in range(B):
         assert torch.all(mel[i, int(b["mel_len"][i]):] == 0)
+
+
+def test_scaled_config4_fp32_matches_oracle(cuda, cfg_all):
+    """BASELINE config 4 width (hidden 512, FFN 2048; dh = 256 in the fused attention on the
+    bf16 path) -- 2+2 layers keep the fp32 oracle fast; B=2, T_phon=40."""
+    import copy
+    from fastspeech2.model import FastSpeech2
+    from fastspeech2.synthetic import make_batch
+    from oracle.fs2_oracle import FastSpeech2Oracle
+    kw = copy.deepcopy(cfg_all["model"]["fastspeech2"])
+    for k in ("enc_d_model", "enc_k_dim", "enc_v_dim", "dec_d_model", "dec_k_dim", "dec_v_dim"):
+        kw[k] = 512
+    kw.update(enc_ffn_dim=2048, dec_ffn_dim=2048, enc_num_layers=2, dec_num_layers=2)
+    torch.manual_seed(6)
+    o = FastSpeech2Oracle(**kw, n_speakers=4).eval()
+    torch.manual_seed(6)
+    m = FastSpeech2(**kw, n_speakers=4).cuda().eval()
+    b = make_batch(B=2, tp_min=40, tp_max=40, seed=11)
+    po, lo, pm, lm = _run_both(o, m, cfg_all, b)
+    for i in range(7):
+        assert rel(pm[i], po[i]) <= 1e-3, i
+    assert abs(lm["total_loss"].item() - lo["total_loss"].item()) <= 1e-4 * abs(lo["total_loss"].item())
+    go = dict(o.named_parameters())
+    errs = [rel(p.grad, go[n].grad) for n, p in m.named_parameters()]
+    assert max(errs) <= 1e-2 and float(np.median(errs)) <= 1e-4
+    # bf16: fused attention at dh = 256
+    torch.manual_seed(6)
+    mb = FastSpeech2(**kw, n_speakers=4, act_dtype=torch.bfloat16).cuda().eval()
+    from fastspeech2.synthetic import as_tuple
+    bt, inten = as_tuple(b)
+    g = [t.cuda() for t in bt]
+    with torch.no_grad():
+        pb = mb(g[0], g[1], g[6], g[4], g[5], intensity=inten.cuda())
+    assert rel(pb[0], po[0]) <= 5e-2
