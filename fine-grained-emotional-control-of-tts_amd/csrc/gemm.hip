@@ -42,6 +42,7 @@ struct GemmP {
   int M, N, K, kvalid, mvalid, nvalid;
   const char* A; long lda; const char* B; long ldb;
   int conv_mode, conv_t, conv_kw, conv_c, conv_p;
+  int conv_dil;       // dilation of the forward conv modes 1 and 5 (tap j at (j - P) * dil)
   char* C; long ldc; int c_fp32; int c_conv_kw;
   const float* bias; int relu;
   const char* gate; long ldg;
@@ -76,10 +77,13 @@ __device__ __forceinline__ u32x4 add_f32x4(u32x4 a, u32x4 b) {
 }
 
 // epilogue activation: 1 ReLU (SB pos_ffn, model.py:241-267), 2 GELU with erf
-// (nn.GELU() of the IntensityExtractor FFN, rank_model/model.py:30,42)
+// (nn.GELU() of the IntensityExtractor FFN, rank_model/model.py:30,42), 3 leaky ReLU 0.1 and
+// 4 tanh (HiFi-GAN generator: LRELU_SLOPE, output tanh)
 __device__ __forceinline__ float epi_act(float v, int act) {
   if (act == 1) return fmaxf(v, 0.f);
   if (act == 2) return 0.5f * v * (1.f + erff(v * 0.70710678118654752f));
+  if (act == 3) return v >= 0.f ? v : 0.1f * v;
+  if (act == 4) return tanhf(v);
   return v;
 }
 
@@ -115,10 +119,10 @@ __device__ __forceinline__ void load_kmajor(u32x4 (&st)[4], const char* base, lo
         const int j = k / C, c = k - j * C;
         const int b = rb[i], t = rt[i];
         if (cmode == 1) {
-          const int ts = reflect_idx(t + j - P, T_);
+          const int ts = reflect_idx(t + (j - P) * p.conv_dil, T_);
           v = ld16(base + ((long)(b * T_ + ts) * ld + c) * ES);
         } else if (cmode == 5) {  // zero-padded "same" conv (nn.Conv1d(padding=k//2))
-          const int ts = t + j - P;
+          const int ts = t + (j - P) * p.conv_dil;
           if (ts >= 0 && ts < T_) v = ld16(base + ((long)(b * T_ + ts) * ld + c) * ES);
         } else if (cmode == 4) {  // shift conv over the padded domain, zero outside [0,T)
           const int ts = t - j;
@@ -259,10 +263,10 @@ __device__ __forceinline__ void glds_kmajor(char* lds, const char* base, long ld
         const int C = p.conv_c, T_ = p.conv_t;
         const int j = k / C, c = k - j * C;
         if (cmode == 1) {
-          const int ts = reflect_idx(rt[i] + j - p.conv_p, T_);
+          const int ts = reflect_idx(rt[i] + (j - p.conv_p) * p.conv_dil, T_);
           src = base + ((long)(rb[i] * T_ + ts) * ld + c) * 2;
         } else {
-          const int ts = cmode == 5 ? rt[i] + j - p.conv_p : rt[i] - j;
+          const int ts = cmode == 5 ? rt[i] + (j - p.conv_p) * p.conv_dil : rt[i] - j;
           if (ts >= 0 && ts < T_) src = base + ((long)(rb[i] * T_ + ts) * ld + c) * 2;
         }
       }
@@ -822,9 +826,9 @@ __global__ void __launch_bounds__(BNT) gemm_big_kernel(GemmP p) {
             int ts;
             bool ok = aval[i];
             if (amode == 1) {
-              ts = reflect_idx(at[i] + j - p.conv_p, p.conv_t);
+              ts = reflect_idx(at[i] + (j - p.conv_p) * p.conv_dil, p.conv_t);
             } else {
-              ts = amode == 5 ? at[i] + j - p.conv_p : at[i] - j;
+              ts = amode == 5 ? at[i] + (j - p.conv_p) * p.conv_dil : at[i] - j;
               ok = ok && ts >= 0 && ts < p.conv_t;
             }
             avo[i] = ok ? (int)(((long)(abt[i] + ts) * p.lda + alc[i] * 8) * 2) : BUF_OOB;
@@ -851,9 +855,9 @@ __global__ void __launch_bounds__(BNT) gemm_big_kernel(GemmP p) {
           const int j = k / p.conv_c, c = k - j * p.conv_c;
           int ts;
           if (amode == 1) {
-            ts = reflect_idx(at[i] + j - p.conv_p, p.conv_t);
+            ts = reflect_idx(at[i] + (j - p.conv_p) * p.conv_dil, p.conv_t);
           } else {
-            ts = amode == 5 ? at[i] + j - p.conv_p : at[i] - j;
+            ts = amode == 5 ? at[i] + (j - p.conv_p) * p.conv_dil : at[i] - j;
             ok = ok && ts >= 0 && ts < p.conv_t;
           }
           const int vo = ok ? (int)(((long)(abt[i] + ts) * p.lda + c) * 2) : BUF_OOB;
@@ -1096,9 +1100,9 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256_kernel(GemmP p) {
             int ts;
             bool ok = aval[i];
             if (amode == 1) {
-              ts = reflect_idx(at[i] + j - p.conv_p, p.conv_t);
+              ts = reflect_idx(at[i] + (j - p.conv_p) * p.conv_dil, p.conv_t);
             } else {
-              ts = amode == 5 ? at[i] + j - p.conv_p : at[i] - j;
+              ts = amode == 5 ? at[i] + (j - p.conv_p) * p.conv_dil : at[i] - j;
               ok = ok && ts >= 0 && ts < p.conv_t;
             }
             avo[i] = ok ? (int)(((long)(abt[i] + ts) * p.lda + ac[i] * 8) * 2) : BUF_OOB;
@@ -1125,9 +1129,9 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256_kernel(GemmP p) {
           const int j = k / p.conv_c, c = k - j * p.conv_c;
           int ts;
           if (amode == 1) {
-            ts = reflect_idx(at[i] + j - p.conv_p, p.conv_t);
+            ts = reflect_idx(at[i] + (j - p.conv_p) * p.conv_dil, p.conv_t);
           } else {
-            ts = amode == 5 ? at[i] + j - p.conv_p : at[i] - j;
+            ts = amode == 5 ? at[i] + (j - p.conv_p) * p.conv_dil : at[i] - j;
             ok = ok && ts >= 0 && ts < p.conv_t;
           }
           const int vo = ok ? (int)(((long)(abt[i] + ts) * p.lda + c) * 2) : BUF_OOB;
@@ -1421,6 +1425,7 @@ extern "C" int fs2_gemm(const fs2_gemm_desc* d, void* stream) {
   p.A = (const char*)d->A; p.lda = d->lda; p.B = (const char*)d->B; p.ldb = d->ldb;
   p.conv_mode = d->conv_mode; p.conv_t = d->conv_t; p.conv_kw = d->conv_kw; p.conv_c = d->conv_c;
   p.conv_p = d->conv_kw > 0 ? (d->conv_kw - 1) / 2 : 0;
+  p.conv_dil = d->conv_dil > 1 ? d->conv_dil : 1;
   p.C = (char*)d->C; p.ldc = d->ldc; p.c_fp32 = d->c_fp32; p.c_conv_kw = d->c_conv_kw;
   p.bias = d->bias; p.relu = d->relu;
   p.gate = (const char*)d->gate; p.ldg = d->ldg;
@@ -1447,7 +1452,8 @@ extern "C" int fs2_gemm(const fs2_gemm_desc* d, void* stream) {
   if (!d->b_kmajor && (p.N % epc)) return FS2_EINVAL;
   if (p.conv_mode) {
     if (p.conv_t <= 0 || p.conv_kw <= 0 || p.conv_c <= 0 || (p.conv_c % epc)) return FS2_EINVAL;
-    if ((p.conv_mode == 1 || p.conv_mode == 2 || p.conv_mode == 3) && p.conv_p >= p.conv_t)
+    if (p.conv_dil > 1 && p.conv_mode != 1 && p.conv_mode != 5) return FS2_EINVAL;
+    if ((p.conv_mode == 1 || p.conv_mode == 2 || p.conv_mode == 3) && p.conv_p * p.conv_dil >= p.conv_t)
       return FS2_EINVAL;  // reflect pad needs pad < T
     if ((p.conv_mode == 1 || p.conv_mode == 2 || p.conv_mode == 5) && (!d->a_kmajor || p.K != p.conv_kw * p.conv_c))
       return FS2_EINVAL;

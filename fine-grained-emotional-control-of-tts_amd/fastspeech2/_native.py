@@ -42,7 +42,7 @@ class GemmDesc(ctypes.Structure):
         ("batch", ctypes.c_int), ("batch_div", ctypes.c_int),
         ("sA1", ctypes.c_int64), ("sA2", ctypes.c_int64), ("sB1", ctypes.c_int64),
         ("sB2", ctypes.c_int64), ("sC1", ctypes.c_int64), ("sC2", ctypes.c_int64),
-        ("sR1", ctypes.c_int64), ("sR2", ctypes.c_int64),
+        ("sR1", ctypes.c_int64), ("sR2", ctypes.c_int64), ("conv_dil", ctypes.c_int),
     ]
 
 
@@ -124,6 +124,9 @@ SIGNATURES = {
     "fs2_phoneme_average": (I, [P, I, I, P, P, I, I, P, P]),
     "fs2_collate_phonemes": (I, [P, P, P, P, I, I, P, P, P, P]),
     "fs2_collate_frames": (I, [P, P, P, P, P, I, I, I, P, P, P, P, P, P]),
+    "fs2_vocoder_input": (I, [P, I, I, I, I, P, I, I, P]),
+    "fs2_leaky_relu": (I, [P, P, I64, Fl, I, P]),
+    "fs2_mean3_leaky_relu": (I, [P, P, P, P, I64, Fl, I, P]),
     "fs2_fill": (I, [P, I64, Fl, I, P]),
     "fs2_add": (I, [P, P, I64, Fl, I, P]),
     "fs2_cast": (I, [P, I, P, I, I64, P]),

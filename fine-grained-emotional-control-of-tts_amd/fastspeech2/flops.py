@@ -33,3 +33,23 @@ def extractor_flops(B, T, hidden, n_layers, kernel, n_in=82, n_emo=5):
     D = hidden
     per_layer = 8 * T * D * D + 4 * T * T * D + 2 * 2 * kernel * T * D * 4 * D
     return B * (2 * T * n_in * D + n_layers * per_layer + 2 * T * D * n_emo)
+
+
+def vocoder_flops(B, T_frames, hp=None):
+    """HiFi-GAN generator forward (fastspeech2.vocoder) over B utterances of T_frames mel frames
+    (plus the 2 x inference_padding replicated frames): conv_pre, the polyphase upsampling
+    GEMMs (3 taps, including their structural zero taps), 3 ResBlock1 x 3 x 2 convs per stage,
+    conv_post."""
+    from .vocoder import HPARAMS
+    hp = hp or HPARAMS
+    L = T_frames + 2 * hp["inference_padding"]
+    c = hp["upsample_initial_channel"]
+    f = 2 * L * 7 * hp["in_channels"] * c
+    for u in hp["upsample_factors"]:
+        f += 2 * L * 3 * c * (u * (c // 2))
+        L *= u
+        c //= 2
+        for k, dils in zip(hp["resblock_kernel_sizes"], hp["resblock_dilation_sizes"]):
+            f += len(dils) * 2 * 2 * L * k * c * c
+    f += 2 * L * 7 * c
+    return B * f

@@ -38,8 +38,9 @@ def round_up(x, m):
 def gemm(M, N_, K, A, lda, B, ldb, C, ldc, *, dt, a_kmajor=1, b_kmajor=1, conv=None, c_fp32=0,
          c_conv_kw=0, bias=None, relu=0, gate=None, ldg=0, row_scale=None, residual=None, ldr=0,
          row_scale_post=None, accumulate=0, split_k=1, split_stride=0, kvalid=0, mvalid=0,
-         nvalid=0, batch=1, batch_div=1, strides=None):
+         nvalid=0, batch=1, batch_div=1, strides=None, conv_dil=1):
     d = N.GemmDesc()
+    d.conv_dil = conv_dil
     d.M, d.N, d.K, d.kvalid, d.mvalid, d.nvalid, d.dtype = M, N_, K, kvalid, mvalid, nvalid, dt
     d.A, d.lda, d.a_kmajor = _p(A), lda, a_kmajor
     d.B, d.ldb, d.b_kmajor = _p(B), ldb, b_kmajor
@@ -272,6 +273,20 @@ def weight_prep_table(entries):
 def weight_prep_batched(table, n, total_tiles, *, dt):
     _chk(N.lib().fs2_weight_prep_batched(_p(table), n, total_tiles, dt, _s()),
          "fs2_weight_prep_batched")
+
+
+def vocoder_input(mel, B, n_mels, T, pad, X, ldx, *, dt):
+    _chk(N.lib().fs2_vocoder_input(_p(mel), B, n_mels, T, pad, _p(X), ldx, dt, _s()),
+         "fs2_vocoder_input")
+
+
+def leaky_relu(x, y, n, slope, *, dt):
+    _chk(N.lib().fs2_leaky_relu(_p(x), _p(y), n, slope, dt, _s()), "fs2_leaky_relu")
+
+
+def mean3_leaky_relu(a, b, c, y, n, slope, *, dt):
+    _chk(N.lib().fs2_mean3_leaky_relu(_p(a), _p(b), _p(c), _p(y), n, slope, dt, _s()),
+         "fs2_mean3_leaky_relu")
 
 
 def fill(X, n, value, *, dt):

@@ -58,7 +58,8 @@ typedef struct fs2_gemm_desc {
   void* C; int64_t ldc; int c_fp32;           /* output; c_fp32: float output else dtype     */
   int c_conv_kw;        /* >0: output column n=(j,c) is stored at c*c_conv_kw + j            */
   const float* bias;    /* [N]       v += bias[n]                                             */
-  int relu;             /* 1: v = max(v, 0); 2: v = GELU(v) = v/2 (1 + erf(v/sqrt 2))        */
+  int relu;             /* 1: v = max(v, 0); 2: v = GELU(v) = v/2 (1 + erf(v/sqrt 2));
+                           3: leaky ReLU slope 0.1; 4: tanh                                    */
   const void* gate; int64_t ldg;              /* dtype [M][ldg]: v *= (gate > 0)             */
   const float* row_scale;                     /* [M]: v *= row_scale[m]                      */
   const void* residual; int64_t ldr;          /* dtype [M][ldr]: v += residual               */
@@ -71,6 +72,7 @@ typedef struct fs2_gemm_desc {
   /* batched: z in [0,batch): offset(z) = (z / batch_div)*s1 + (z % batch_div)*s2 (elements) */
   int batch, batch_div;
   int64_t sA1, sA2, sB1, sB2, sC1, sC2, sR1, sR2;
+  int conv_dil;         /* dilation of conv modes 1 / 5 (tap j reads row t + (j-P)*dil); 0 = 1 */
 } fs2_gemm_desc;
 
 int fs2_gemm(const fs2_gemm_desc* d, void* stream);
@@ -302,6 +304,20 @@ int fs2_collate_frames(const int32_t* order, const int64_t* frame_offsets, const
                        const float* pitch, const float* energy, int B, int Tm, int n_mels,
                        float* mel_padded, float* pitch_padded, float* energy_padded,
                        float* rank_x, int64_t* output_lengths, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * HiFi-GAN generator forward (speechbrain HIFIGAN.decode_batch,
+ * fastspeech2/inference.py:60-63,85).  Convs on fs2_gemm (conv_mode 1 + conv_dil, transposed
+ * convs as 3-tap polyphase conv_mode 5, act 3 / 4 epilogues, residual epilogue).
+ * ------------------------------------------------------------------------------------------ */
+/* mel (B, n_mels, T) fp32 -> X[B*(T+2 pad)][ldx] (dtype), pad replicated frames each side   */
+int fs2_vocoder_input(const float* mel, int B, int n_mels, int T, int pad, void* X, int ldx,
+                      int dtype, void* stream);
+/* y = leaky_relu(x, slope); n % (16 / sizeof(dtype)) == 0, 16-byte aligned                  */
+int fs2_leaky_relu(const void* x, void* y, int64_t n, float slope, int dtype, void* stream);
+/* y = leaky_relu(((a + b) + c) / 3, slope)                                                  */
+int fs2_mean3_leaky_relu(const void* a, const void* b, const void* c, void* y, int64_t n,
+                         float slope, int dtype, void* stream);
 
 /* utilities */
 int fs2_fill(void* X, int64_t n, float value, int dtype, void* stream);

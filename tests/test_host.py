@@ -140,3 +140,20 @@ def test_get_intensity_rep_prototype_lookup():
     r = get_intensity_rep(2, 3, 1, 7, bank)
     assert r.shape == (1, 7, 5)
     assert torch.equal(r[0, 4], torch.from_numpy(bank[2, 3, 1]))
+
+
+@pytest.mark.parametrize("u", [8, 2])
+def test_vocoder_polyphase_transposed_conv(u):
+    """fastspeech2.vocoder.polyphase_weights: ConvTranspose1d(k=2u, stride u, padding u/2) ==
+    a 3-tap zero-padded conv whose u output phases are stacked along the channel axis (the
+    form the GEMM runs, conv_mode 5)."""
+    import torch.nn.functional as F
+    from fastspeech2.vocoder import polyphase_weights
+    torch.manual_seed(u)
+    C, O, L = 6, 5, 9
+    W, b, x = torch.randn(C, O, 2 * u), torch.randn(O), torch.randn(2, C, L)
+    ref = F.conv_transpose1d(x, W, b, stride=u, padding=u // 2)
+    W3 = polyphase_weights(W, u).reshape(u * O, 3, C).permute(0, 2, 1)
+    y = F.conv1d(x, W3, b.repeat(u), padding=1)
+    y = y.reshape(2, u, O, L).permute(0, 2, 3, 1).reshape(2, O, L * u)
+    torch.testing.assert_close(y, ref, rtol=1e-5, atol=1e-5)

@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--sentences", type=int, default=256)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--vocoder", action="store_true",
+                    help="also decode the mels with the HiFi-GAN generator (fastspeech2.vocoder)")
     a = ap.parse_args()
     from fastspeech2 import load_config
     from fastspeech2.model import FastSpeech2
@@ -56,12 +58,34 @@ def main():
     frames = sum(lens)
     Tp, Tm = max(p.numel() for p in phs), max(lens)
     fl = forward_flops(m.cfg, a.sentences, Tp, Tm)
+    voc = None
+    if a.vocoder:
+        from fastspeech2.vocoder import HifiganGenerator
+        from fastspeech2.flops import vocoder_flops
+        gen = HifiganGenerator(act_dtype=torch.bfloat16).cuda()
+        # mels padded to T_mel_max as (B, 80, T) (decode_batch's input layout)
+        melb = torch.zeros(a.sentences, 80, Tm, device="cuda")
+        for i, x in enumerate(mels):
+            melb[i, :, :x.shape[0]] = x.float().t()
+        wav = gen.decode_batch(melb)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            wav = gen.decode_batch(melb)
+        torch.cuda.synchronize()
+        tv = (time.perf_counter() - t0) / a.steps
+        vf = vocoder_flops(a.sentences, Tm)
+        voc = {"ms_per_batch": tv * 1e3, "samples_per_s": wav.numel() / tv,
+               "padded_samples": wav.numel(), "tflops_padded": vf / tv / 1e12,
+               "end_to_end_mel_frames_per_s": frames / (dt + tv),
+               "note": "HiFi-GAN generator (LibriTTS-16k architecture), random weights, bf16"}
     print(json.dumps({"metric": "inference mel-frames/sec (mel generation, predicted durations)",
                       "value": frames / dt, "unit": "mel-frames/s", "ms_per_batch": dt * 1e3,
                       "sentences": a.sentences, "T_phon_max": Tp, "T_mel_max": Tm,
                       "frames": frames, "dtype": "bf16", "tflops_padded": fl / dt / 1e12,
                       "note": "includes host padding of the sentence list and the mel-length "
-                              "D2H the reference also performs (mel_lens on CPU)"}))
+                              "D2H the reference also performs (mel_lens on CPU)",
+                      "vocoder": voc}))
 
 
 if __name__ == "__main__":
