@@ -473,6 +473,16 @@ __global__ void conv_fold_kernel(const float* Xp, int nsplit, long sstride, int 
   }
 }
 
+// out[i] (+)= sum_s ws[s * stride + i]: split-K weight-gradient slices (fixed order)
+__global__ void __launch_bounds__(256) sum_slices_kernel(const float* ws, int ns, long stride,
+                                                         long n4, float* out, int accumulate) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n4) return;
+  f32x4 a = accumulate ? ((const f32x4*)out)[i] : f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int s = 0; s < ns; ++s) a += *(const f32x4*)(ws + s * stride + i * 4);
+  ((f32x4*)out)[i] = a;
+}
+
 int ln_blocks(int M) { return min(4096, max(1, (M + 31) / 32)); }
 int colsum_blocks(int M) { return min(512, max(1, (M + 63) / 64)); }
 bool a16(const void* p) { return ((uintptr_t)p & 15) == 0; }
@@ -595,6 +605,18 @@ extern "C" int fs2_colsum(const void* X, int64_t ldx, int M, int N, int dtype, f
   }
   hipLaunchKernelGGL(reduce_parts_kernel, dim3((N + 15) / 16), dim3(256), 0, st, workspace, nb, N,
                      1, out, nullptr, nullptr, accumulate);
+  FS2_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int fs2_sum_slices(const float* ws, int nslices, int64_t stride, int64_t n,
+                              float* out, int accumulate, void* stream) {
+  if (n == 0) return 0;
+  if (!ws || !out || nslices < 1 || (n % 4) || (stride % 4) || !a16(ws) || !a16(out))
+    return FS2_EINVAL;
+  const long n4 = n / 4;
+  hipLaunchKernelGGL(sum_slices_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, ws, nslices, (long)stride, n4, out, accumulate);
   FS2_CHECK_LAUNCH();
   return 0;
 }

@@ -58,6 +58,27 @@ def dgrad_split(Mp, C, K, dt, n_cu=256, max_split=8):
     return best
 
 
+_NO_SLICES = os.environ.get("FS2_NO_WGRAD_SLICES", "0") not in ("", "0")
+
+
+def wgrad_slices(O, Ncols, ldc, K, dt, n_cu=256):
+    """Split-K slice count for a weight gradient with a small output: enough 256x128 tiles x
+    slices to fill the 256 CUs once, each slice >= 8 K-tiles; slices are fp32 planes summed in
+    a fixed order instead of tens of fp32 atomics landing on every output element.  Applied
+    where it measured faster (bench.py --detail, FS2_NO_WGRAD_SLICES=1 for the A/B): outputs of
+    >= 256 rows and <= 256 K elements (out-projection 62 -> 55 us, PostNet conv_pre 73 -> 57 us),
+    or <= 600 K elements over encoder-length K (conv2 58 -> 42 us, out-projection 47 -> 31 us).
+    1 = the atomic split-K path (decoder conv2 91 vs 144 us, PostNet 150 vs 231 us)."""
+    if dt != 1 or ldc % 8 or Ncols != ldc or O < 256:
+        return 1
+    n = O * ldc
+    if not (n <= (1 << 18) or (n <= 600_000 and K <= 8192)):
+        return 1
+    tiles = -(-O // 256) * -(-Ncols // 128)
+    ns = min(-(-n_cu // tiles), max(1, (K // 64) // 8))
+    return ns if ns >= 2 else 1
+
+
 class FS2Engine:
     def __init__(self, model, act_dtype=torch.float32):
         self.m = model
@@ -216,8 +237,19 @@ class FS2Engine:
         if tiles < 256:
             split = max(1, min(-(-512 // tiles), K // (_BK[self.dt] * 4)))
         conv = (3, T, KW, C) if KW > 1 else None
+        ldc = C * KW
+        ns = wgrad_slices(O, Ncols, ldc, K, self.dt) if not _NO_SLICES else 1
+        if ns > 1:
+            # small outputs: split-K slices into fp32 planes, summed in a fixed order -- instead
+            # of tens of fp32 atomics landing on every output element
+            stride = O * ldc
+            ws = self.ws(ns * stride)
+            ops.gemm(O, Ncols, K, dY, lddy, X, ldx, ws, ldc, dt=self.dt, a_kmajor=0, b_kmajor=0,
+                     conv=conv, c_fp32=1, kvalid=M, nvalid=ldc, split_k=ns, split_stride=stride)
+            ops.sum_slices(ws, ns, stride, stride, self.grads[wname], accumulate=1)
+            return
         # conv weight gradients land contiguous in the [O][KW][C] flat layout (model._kw_major)
-        ops.gemm(O, Ncols, K, dY, lddy, X, ldx, self.grads[wname], C * KW, dt=self.dt, a_kmajor=0,
+        ops.gemm(O, Ncols, K, dY, lddy, X, ldx, self.grads[wname], ldc, dt=self.dt, a_kmajor=0,
                  b_kmajor=0, conv=conv, c_fp32=1, kvalid=M, nvalid=KW * C, accumulate=1,
                  split_k=split)
 

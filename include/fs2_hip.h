@@ -85,6 +85,12 @@ int fs2_conv_fold(const float* Xpad, int nsplit, int64_t split_stride, int B, in
                   int C, void* out, int64_t ldo, const void* residual, int64_t ldr,
                   const float* row_scale, const float* row_scale_post, int dtype, void* stream);
 
+/* out[i] (+)= sum_{s < nslices} ws[s*stride + i], i < n (fp32; n, stride multiples of 4,
+ * 16-byte aligned): the sum of split-K weight-gradient slices written by fs2_gemm with
+ * split_stride (no atomics; fixed summation order)                                         */
+int fs2_sum_slices(const float* ws, int nslices, int64_t stride, int64_t n, float* out,
+                   int accumulate, void* stream);
+
 /* column sums: out[n] (+)= sum_m X[m][n]   (bias gradients; SB Linear/Conv1d bias, K16) */
 int fs2_colsum(const void* X, int64_t ldx, int M, int N, int dtype, float* out, int accumulate,
                float* workspace, void* stream);
