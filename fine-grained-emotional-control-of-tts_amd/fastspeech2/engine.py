@@ -59,6 +59,7 @@ def dgrad_split(Mp, C, K, dt, n_cu=256, max_split=8):
 
 
 _NO_SLICES = os.environ.get("FS2_NO_WGRAD_SLICES", "0") not in ("", "0")
+_NO_SIDE = os.environ.get("FS2_NO_SIDE_STREAM", "0") not in ("", "0")
 
 
 def wgrad_slices(O, Ncols, ldc, K, dt, n_cu=256):
@@ -94,6 +95,9 @@ class FS2Engine:
         self.pe_enc = model.sinusoidal_positional_embed_encoder.pe[0].float().contiguous()
         self.pe_dec = model.sinusoidal_positional_embed_decoder.pe[0].float().contiguous()
         self._ws = torch.empty(1 << 20, dtype=torch.float32, device=self.dev)
+        self._ws_key = torch.cuda.current_stream(self.dev).cuda_stream
+        self._ws_other = {}
+        self._side = torch.cuda.Stream(self.dev) if (self.dt == N.BF16 and not _NO_SIDE) else None
         self.w = {}
         self._wspecs = self._weight_specs()
         self._prepared_version = None
@@ -116,10 +120,44 @@ class FS2Engine:
         return self.dt == 1 and not _NO_FLASH and ops.attn_supported(T, dh, self.dt)
 
     def ws(self, n):
+        """scratch buffer of the CURRENT stream (the weight-gradient side stream has its own)"""
         n = int(n)
-        if self._ws.numel() < n:
-            self._ws = torch.empty(int(n * 1.25) + 1024, dtype=torch.float32, device=self.dev)
-        return self._ws
+        key = torch.cuda.current_stream(self.dev).cuda_stream
+        buf = self._ws if key == self._ws_key else self._ws_other.get(key)
+        if buf is None or buf.numel() < n:
+            buf = torch.empty(max(int(n * 1.25) + 1024, 1 << 20), dtype=torch.float32,
+                              device=self.dev)
+            if key == self._ws_key:
+                self._ws = buf
+            else:
+                self._ws_other[key] = buf
+        return buf
+
+    # ------------------------------------------------------------------ side stream
+    # Weight and bias gradients depend only on tensors the data-gradient chain has already
+    # produced, so they run on a second stream: the encoder's GEMMs (M = 6400) and the tail
+    # rounds of the decoder's leave CUs idle that the other chain fills.
+    def _side_enter(self, *tensors):
+        if self._side is None:
+            return None
+        main = torch.cuda.current_stream(self.dev)
+        self._side.wait_stream(main)
+        ctx = torch.cuda.stream(self._side)
+        ctx.__enter__()
+        return ctx, tensors
+
+    def _side_exit(self, h):
+        if h is None:
+            return
+        ctx, tensors = h
+        ctx.__exit__(None, None, None)
+        for t in tensors:
+            if t is not None:
+                t.record_stream(self._side)
+
+    def side_join(self):
+        if self._side is not None:
+            torch.cuda.current_stream(self.dev).wait_stream(self._side)
 
     def empty(self, *shape, dtype=None):
         return torch.empty(*shape, dtype=dtype or self.adt, device=self.dev)
@@ -220,12 +258,14 @@ class FS2Engine:
                       split_stride=Mp * C)
 
     def _wgrad(self, dY, lddy, X, ldx, M, T, wname, n_cols=None):
+        h = self._side_enter(dY, X)
         tag = self._dtag("wgrad", wname, T)
         if tag:
             self._tic(tag)
         self._wgrad_impl(dY, lddy, X, ldx, M, T, wname, n_cols)
         if tag:
             self._toc(tag)
+        self._side_exit(h)
 
     def _wgrad_impl(self, dY, lddy, X, ldx, M, T, wname, n_cols=None):
         """grad[O][KW][C] += sum_m dY[m][o] * X[reflect(t+j-P)][c]   (fp32, accumulate)."""
@@ -254,7 +294,9 @@ class FS2Engine:
                  split_k=split)
 
     def _bias_grad(self, dY, lddy, M, n, gname):
+        h = self._side_enter(dY)
         ops.colsum(dY, lddy, M, n, self.grads[gname], dt=self.dt, ws=self.ws(ops.colsum_ws(M, n)))
+        self._side_exit(h)
 
     # ------------------------------------------------------------------ FFT block
     def _fft_fwd(self, X, B, T, key_pad, prefix, H, p_drop, seed, salt):
@@ -704,7 +746,11 @@ class FS2Engine:
         Mp, Mm = B * Tp, B * Tm
         P, G = self.params, self.grads
         keep_p, keep_m = ctx["keep_p"], ctx["keep_m"]
-        notify = self.on_grads_ready or (lambda tag: None)
+        def notify(tag):
+            # a bucket's all-reduce must see this group's side-stream weight gradients
+            if self.on_grads_ready is not None:
+                self.side_join()
+                self.on_grads_ready(tag)
         d_mel = d_mel.reshape(Mm, NM).to(self.adt).contiguous()
         d_post = d_post.reshape(Mm, NM).to(self.adt).contiguous()
         # mel receives the loss gradient and the PostNet residual (model.py:431)
@@ -767,4 +813,5 @@ class FS2Engine:
             notify(f"encoder.layers.{i}")
         ops.embed_bwd(ctx["tokens"], dX, keep_p, Mp, D, c.n_char,
                       G["encPreNet.token_embedding.Embedding.weight"], dt=self.dt)
+        self.side_join()
         notify("prenet")
