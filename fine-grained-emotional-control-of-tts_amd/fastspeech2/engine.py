@@ -60,6 +60,7 @@ def dgrad_split(Mp, C, K, dt, n_cu=256, max_split=8):
 
 _NO_SLICES = os.environ.get("FS2_NO_WGRAD_SLICES", "0") not in ("", "0")
 _NO_SIDE = os.environ.get("FS2_NO_SIDE_STREAM", "0") not in ("", "0")
+_NO_AUX = os.environ.get("FS2_NO_AUX_STREAM", "0") not in ("", "0")
 
 
 def wgrad_slices(O, Ncols, ldc, K, dt, n_cu=256):
@@ -98,6 +99,9 @@ class FS2Engine:
         self._ws_key = torch.cuda.current_stream(self.dev).cuda_stream
         self._ws_other = {}
         self._side = torch.cuda.Stream(self.dev) if (self.dt == N.BF16 and not _NO_SIDE) else None
+        # duration / pitch predictor chains (independent of the rest of the step when the
+        # pitch target is given) run on a third stream; their weight gradients stay on it
+        self._aux = torch.cuda.Stream(self.dev) if (self._side is not None and not _NO_AUX) else None
         self.w = {}
         self._wspecs = self._weight_specs()
         self._prepared_version = None
@@ -141,6 +145,8 @@ class FS2Engine:
         if self._side is None:
             return None
         main = torch.cuda.current_stream(self.dev)
+        if self._aux is not None and main.cuda_stream == self._aux.cuda_stream:
+            return None          # the aux chain is already off the critical path
         self._side.wait_stream(main)
         ctx = torch.cuda.stream(self._side)
         ctx.__enter__()
@@ -154,6 +160,27 @@ class FS2Engine:
         for t in tensors:
             if t is not None:
                 t.record_stream(self._side)
+
+    def _aux_fork(self, *tensors):
+        """enter the aux stream after everything queued so far on the current stream"""
+        main = torch.cuda.current_stream(self.dev)
+        self._aux.wait_stream(main)
+        for t in tensors:
+            if t is not None:
+                t.record_stream(self._aux)
+        ctx = torch.cuda.stream(self._aux)
+        ctx.__enter__()
+        return ctx, main
+
+    def _aux_exit(self, h):
+        h[0].__exit__(None, None, None)
+
+    def _aux_join(self, main, *tensors):
+        """the main stream waits for the aux chain; its outputs are now used on main"""
+        main.wait_stream(self._aux)
+        for t in tensors:
+            if t is not None:
+                t.record_stream(main)
 
     def side_join(self):
         if self._side is not None:
@@ -657,8 +684,14 @@ class FS2Engine:
         Z = self.empty(Mp, D)
         self._fwd(cat, ldc, Mp, Tp, "concat_proj.w.weight", Z, D, row_scale=keep_p)
         # variance adaptor (model.py:365-403)
+        # with the duration and pitch targets given (training), nothing downstream but the loss
+        # reads durPred / pitchPred, so they run on the aux stream (same salt order as sequential)
+        aux_h = (self._aux_fork(Z, keep_p) if (self._aux is not None and pitch is not None
+                                                and durations is not None) else None)
         pd, dctx = self._pred_fwd(Z, keep_p, B, Tp, "durPred", 1.0, pv, seed, salt)
         pp, pctx = self._pred_fwd(Z, keep_p, B, Tp, "pitchPred", pitch_rate, pv, seed, salt)
+        if aux_h is not None:
+            self._aux_exit(aux_h)
         kwp = c.pitch_pred_kernel_size
         if pitch is not None:
             pitch = pitch.to(torch.float32).contiguous()
@@ -725,6 +758,9 @@ class FS2Engine:
         self._fwd(Xo, D, Mm, Tm, "linear.w.weight", mel, NM, bias=P["linear.w.bias"],
                   row_scale=keep_m)                                                # :430
         post, pn_ctx = self._postnet_fwd(mel, B, Tm, pp_, seed, salt)            # :431
+        if aux_h is not None:
+            self._aux_join(aux_h[1], pd, pp, *[t for cc in (dctx, pctx) for t in cc.values()
+                                               if isinstance(t, torch.Tensor)])
         ctx.update(keep_p=keep_p, enc_ctx=enc_ctx, Xenc_last=X, me=me, re=re_, cat=cat, ldc=ldc,
                    Z=Z, dctx=dctx, pctx=pctx, ectx=ectx, a_p=a_p, a_e=a_e, Z2m=Z2m, Tm=Tm,
                    cum=cum, keep_m=keep_m, dec_ctx=dec_ctx, Xdec_last=Xd, md=md, rd=rd, Xo=Xo,
@@ -753,6 +789,17 @@ class FS2Engine:
                 self.on_grads_ready(tag)
         d_mel = d_mel.reshape(Mm, NM).to(self.adt).contiguous()
         d_post = d_post.reshape(Mm, NM).to(self.adt).contiguous()
+        d_pitch = d_pitch.reshape(Mp).to(self.adt).contiguous()
+        d_dur = d_dur.reshape(Mp).to(self.adt).contiguous()
+        aux_h, dZd, dZp = None, None, None
+        if self._aux is not None:
+            # duration and pitch predictor backward chains depend only on the loss gradients
+            # and the forward context: run them beside the PostNet / decoder backward
+            aux_h = self._aux_fork(d_pitch, d_dur, keep_p)
+            dZp = self._pred_bwd(d_pitch, ctx["pctx"], keep_p, B, Tp, "pitchPred", ctx["p_var"],
+                                 seed)
+            dZd = self._pred_bwd(d_dur, ctx["dctx"], keep_p, B, Tp, "durPred", ctx["p_var"], seed)
+            self._aux_exit(aux_h)
         # mel receives the loss gradient and the PostNet residual (model.py:431)
         d_mel_total = d_mel.clone()
         ops.add(d_mel_total, d_post, Mm * NM, 1.0, dt=self.dt)
@@ -786,12 +833,18 @@ class FS2Engine:
         kwp = c.pitch_pred_kernel_size
         ops.embed1d_bwd(dZ2, ctx["a_p"], B, Tp, D, kwp, G["pitchEmbed.conv.weight"],
                         G["pitchEmbed.conv.bias"], dt=self.dt, ws=self.ws(128 * (kwp + 1) * D))
-        d_pitch = d_pitch.reshape(Mp).to(self.adt).contiguous()
-        dZa = self._pred_bwd(d_pitch, ctx["pctx"], keep_p, B, Tp, "pitchPred", ctx["p_var"], seed,
-                             residual=dZ2)
-        d_dur = d_dur.reshape(Mp).to(self.adt).contiguous()
-        dZ = self._pred_bwd(d_dur, ctx["dctx"], keep_p, B, Tp, "durPred", ctx["p_var"], seed,
-                            residual=dZa, post_mask=True)
+        if aux_h is not None:
+            self._aux_join(aux_h[1], dZp, dZd)
+            # dZ = keep * (dZd + dZp + dZ2), as the sequential chain's residual epilogues
+            dZ = dZ2
+            ops.add(dZ, dZp, Mp * D, 1.0, dt=self.dt)
+            ops.add(dZ, dZd, Mp * D, 1.0, dt=self.dt)
+            ops.mask_rows(dZ, D, keep_p, Mp, D, dt=self.dt)
+        else:
+            dZa = self._pred_bwd(d_pitch, ctx["pctx"], keep_p, B, Tp, "pitchPred", ctx["p_var"],
+                                 seed, residual=dZ2)
+            dZ = self._pred_bwd(d_dur, ctx["dctx"], keep_p, B, Tp, "durPred", ctx["p_var"], seed,
+                                residual=dZa, post_mask=True)
         notify("variance")
         # concat projection (Z = proj(cat) * keep) -- dZ is already masked
         ldc = ctx["ldc"]
