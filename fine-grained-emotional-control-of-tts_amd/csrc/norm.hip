@@ -1,3 +1,4 @@
+#include <cstdlib>
 // LayerNorm forward/backward with fused residual-add, dropout, tanh, row-mask, post-add,
 // plus column-sum reductions for bias / gamma / beta gradients.
 //
@@ -200,6 +201,20 @@ __global__ void __launch_bounds__(256) ln_fwd_vec_kernel(LnFwdP p) {
   const float inv_r = p.p_r > 0.f ? 1.f / (1.f - p.p_r) : 1.f;
   float v[NCH][V];
   float sum = 0.f;
+  // the epilogue operands are loaded up front, so their latency overlaps the two row sums
+  float g[NCH][V], b[NCH][V], a[NCH][V];
+  const T* pa = p.post_add ? (const T*)p.post_add + (long)row * p.ldp : nullptr;
+  const float rm = p.row_mask ? p.row_mask[row] : 1.f;
+#pragma unroll
+  for (int ch = 0; ch < NCH; ++ch) {
+    const int d0 = (lane + 64 * ch) * V;
+    if (d0 < p.D) {
+      vload<float>(g[ch], p.gamma + d0);
+      vload<float>(b[ch], p.beta + d0);
+      if constexpr (V == 8) { vload<float>(g[ch] + 4, p.gamma + d0 + 4); vload<float>(b[ch] + 4, p.beta + d0 + 4); }
+      if (pa) vload<T>(a[ch], pa + d0);
+    }
+  }
 #pragma unroll
   for (int ch = 0; ch < NCH; ++ch) {
     const int d0 = (lane + 64 * ch) * V;
@@ -241,26 +256,20 @@ __global__ void __launch_bounds__(256) ln_fwd_vec_kernel(LnFwdP p) {
   const float rstd = 1.f / sqrtf(var + p.eps);
   if (lane == 0) { p.mean[row] = mean; p.rstd[row] = rstd; }
   const float inv_o = p.p_o > 0.f ? 1.f / (1.f - p.p_o) : 1.f;
-  const float rm = p.row_mask ? p.row_mask[row] : 1.f;
   T* y = (T*)p.y + (long)row * p.ldy;
-  const T* pa = p.post_add ? (const T*)p.post_add + (long)row * p.ldp : nullptr;
 #pragma unroll
   for (int ch = 0; ch < NCH; ++ch) {
     const int d0 = (lane + 64 * ch) * V;
     if (d0 < p.D) {
-      float g[V], b[V], o[V], a[V];
-      vload<float>(g, p.gamma + d0);
-      vload<float>(b, p.beta + d0);
-      if constexpr (V == 8) { vload<float>(g + 4, p.gamma + d0 + 4); vload<float>(b + 4, p.beta + d0 + 4); }
-      if (pa) vload<T>(a, pa + d0);
+      float o[V];
 #pragma unroll
       for (int e = 0; e < V; ++e) {
-        float q = (v[ch][e] - mean) * rstd * g[e] + b[e];
+        float q = (v[ch][e] - mean) * rstd * g[ch][e] + b[ch][e];
         if (p.do_tanh) q = tanhf(q);
         if (p.p_o > 0.f)
           q = fs2_keep(p.seed, p.salt_o, (uint64_t)row * p.D + d0 + e, p.p_o) ? q * inv_o : 0.f;
         q *= rm;
-        if (pa) q += a[e];
+        if (pa) q += a[ch][e];
         o[e] = q;
       }
       vstore<T>(y + d0, o);
@@ -366,6 +375,110 @@ __global__ void __launch_bounds__(256) ln_bwd_vec_kernel(LnBwdP p, float* part, 
         for (int e = 0; e < V; ++e)
           red[wave][d0 + e] = kind == 0 ? pg[ch][e] : (kind == 1 ? pb[ch][e] : pc[ch][e]);
       }
+    }
+    __syncthreads();
+    for (int d = threadIdx.x; d < p.D; d += 256)
+      part[((long)blockIdx.x * npart + k) * p.D + d] =
+          (red[0][d] + red[1][d]) + (red[2][d] + red[3][d]);
+    __syncthreads();
+  }
+}
+
+// bf16, D <= 512 (one 16-byte chunk per lane): the same per-row arithmetic and the same
+// per-wave accumulation order as ln_bwd_vec_kernel<bf16, 1> (so identical results), but each
+// wave loads R rows (r, r+4, ..., r+4(R-1)) before computing any of them.  No tanh gate (that
+// case keeps the one-row kernel).  The one-row loop
+// keeps ~1.5 KB per wave in flight and ran at 1-2 TB/s (latency bound: 15 waves per CU).
+template <int R>
+__global__ void __launch_bounds__(256) ln_bwd_rows_kernel(LnBwdP p, float* part, int npart,
+                                                          int kind0) {
+  constexpr int V = 8;
+  __shared__ float red[4][512];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int d0 = lane * V;
+  const bool act = d0 < p.D;
+  float pg[V], pb[V], pc[V], gm[V];
+#pragma unroll
+  for (int e = 0; e < V; ++e) { pg[e] = 0.f; pb[e] = 0.f; pc[e] = 0.f; gm[e] = 0.f; }
+  if (act) {
+    vload<float>(gm, p.gamma + d0);
+    vload<float>(gm + 4, p.gamma + d0 + 4);
+    
+  }
+  const float inv_o = p.p_o > 0.f ? 1.f / (1.f - p.p_o) : 1.f;
+  const float inv_r = p.p_r > 0.f ? 1.f / (1.f - p.p_r) : 1.f;
+  const int rbeg = blockIdx.x * p.rows_per_block;
+  const int rend = min(p.M, rbeg + p.rows_per_block);
+  for (int row0 = rbeg + wave; row0 < rend; row0 += 4 * R) {
+    u32x4 us[R], ud[R];
+    float mean[R], rstd[R], rm[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const int row = row0 + 4 * j;
+      const bool ok = row < rend;
+      const int rr = ok ? row : row0;
+      us[j] = act ? *(const u32x4*)((const bf16*)p.s + (long)rr * p.lds + d0) : u32x4{0, 0, 0, 0};
+      ud[j] = act ? *(const u32x4*)((const bf16*)p.dy + (long)rr * p.lddy + d0) : u32x4{0, 0, 0, 0};
+      mean[j] = p.mean[rr];
+      rstd[j] = p.rstd[rr];
+      rm[j] = p.row_mask ? p.row_mask[rr] : 1.f;
+    }
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const int row = row0 + 4 * j;
+      if (row >= rend) break;
+      float sv[V], g[V], xh[V];
+      float a1 = 0.f, a2 = 0.f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        sv[2 * w] = __builtin_bit_cast(float, us[j][w] << 16);
+        sv[2 * w + 1] = __builtin_bit_cast(float, us[j][w] & 0xffff0000u);
+      }
+      if (act) {
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+          const float dv = __builtin_bit_cast(float, (e & 1) ? (ud[j][e >> 1] & 0xffff0000u)
+                                                             : (ud[j][e >> 1] << 16));
+          xh[e] = (sv[e] - mean[j]) * rstd[j];
+          float gg = dv * rm[j];
+          if (p.p_o > 0.f)
+            gg = fs2_keep(p.seed, p.salt_o, (uint64_t)row * p.D + d0 + e, p.p_o) ? gg * inv_o : 0.f;
+          pg[e] += gg * xh[e];
+          pb[e] += gg;
+          g[e] = gg * gm[e];
+          a1 += g[e];
+          a2 += g[e] * xh[e];
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < V; ++e) { g[e] = 0.f; xh[e] = 0.f; }
+      }
+      a1 = wave_sum(a1) / (float)p.D;
+      a2 = wave_sum(a2) / (float)p.D;
+      if (act) {
+        float o[V], w[V];
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+          float q = rstd[j] * (g[e] - a1 - xh[e] * a2);
+          if (p.relu_gate_in && !(sv[e] > 0.f)) q = 0.f;
+          o[e] = q;
+          w[e] = q;
+          if (p.dr && p.p_r > 0.f)
+            w[e] = fs2_keep(p.seed, p.salt_r, (uint64_t)row * p.D + d0 + e, p.p_r) ? q * inv_r : 0.f;
+        }
+        vstore<bf16>((bf16*)p.ds + (long)row * p.ldds + d0, o);
+        if (p.dr) vstore<bf16>((bf16*)p.dr + (long)row * p.D + d0, w);
+#pragma unroll
+        for (int e = 0; e < V; ++e) pc[e] += p.dr ? w[e] : o[e];
+      }
+    }
+  }
+  if (!part) return;
+  for (int k = 0; k < npart; ++k) {
+    const int kind = kind0 + k;  // 0 gamma, 1 beta, 2 column sum
+    if (act) {
+#pragma unroll
+      for (int e = 0; e < V; ++e) red[wave][d0 + e] = kind == 0 ? pg[e] : (kind == 1 ? pb[e] : pc[e]);
     }
     __syncthreads();
     for (int d = threadIdx.x; d < p.D; d += 256)
@@ -484,6 +597,12 @@ __global__ void __launch_bounds__(256) sum_slices_kernel(const float* ws, int ns
 }
 
 int ln_blocks(int M) { return min(4096, max(1, (M + 31) / 32)); }
+// rows in flight per wave in the bf16 LayerNorm backward (FS2_LN_ROWS=1 selects the one-row
+// kernel for A/B runs)
+int ln_rows_r() {
+  static const int r = [] { const char* v = std::getenv("FS2_LN_ROWS"); return v ? std::atoi(v) : 4; }();
+  return r;
+}
 int colsum_blocks(int M) { return min(512, max(1, (M + 63) / 64)); }
 bool a16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
@@ -558,6 +677,8 @@ extern "C" int fs2_ln_bwd(const void* dy, int64_t lddy, const void* s, int64_t l
   const int kind0 = dgamma ? 0 : 2;
   if (dtype == FS2_BF16) {
     if (!vec) hipLaunchKernelGGL(ln_bwd_kernel<bf16>, dim3(nb), dim3(256), 0, st, p);
+    else if (nch == 1 && !do_tanh && ln_rows_r() == 4) hipLaunchKernelGGL((ln_bwd_rows_kernel<4>), dim3(nb), dim3(256), 0, st, p, part, npart, kind0);
+    else if (nch == 1 && !do_tanh && ln_rows_r() == 2) hipLaunchKernelGGL((ln_bwd_rows_kernel<2>), dim3(nb), dim3(256), 0, st, p, part, npart, kind0);
     else if (nch == 1) hipLaunchKernelGGL((ln_bwd_vec_kernel<bf16, 1>), dim3(nb), dim3(256), 0, st, p, part, npart, kind0);
     else if (nch == 2) hipLaunchKernelGGL((ln_bwd_vec_kernel<bf16, 2>), dim3(nb), dim3(256), 0, st, p, part, npart, kind0);
     else hipLaunchKernelGGL((ln_bwd_vec_kernel<bf16, 4>), dim3(nb), dim3(256), 0, st, p, part, npart, kind0);

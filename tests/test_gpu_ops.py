@@ -150,6 +150,71 @@ def test_layernorm_fwd_bwd(cuda, dt, code, tol, D):
         assert rel(dc2, sr.grad.sum(0)) < tol * 3
 
 
+def _keep_ln_np(seed, salt, idx, p):
+    """numpy restatement of fs2_keep (fs2_common.h): the per-element LayerNorm dropout mask."""
+    M32 = np.uint64(0xffffffff)
+
+    def mix(h):
+        h = h & M32
+        h ^= h >> np.uint64(16)
+        h = (h * np.uint64(0x85ebca6b)) & M32
+        h ^= h >> np.uint64(13)
+        h = (h * np.uint64(0xc2b2ae35)) & M32
+        h ^= h >> np.uint64(16)
+        return h
+
+    k = mix(np.uint64((seed ^ ((salt * 0x9E3779B9) & 0xffffffff)) & 0xffffffff))
+    idx = idx.astype(np.uint64)
+    h = mix((idx & M32) ^ k)
+    h = mix(h ^ (idx >> np.uint64(32)) ^ np.uint64(0x68bc21eb))
+    u = (h >> np.uint64(8)).astype(np.float64) / 16777216.0
+    return u >= np.float32(p)
+
+
+@pytest.mark.parametrize("M,D", [(300, 384), (1001, 384), (203, 256)])
+def test_layernorm_bwd_dropout_gate(cuda, M, D):
+    """bf16 LayerNorm backward with output dropout, the relu gate on the input, the
+    dropout-masked residual-branch copy dr and all three partial sums (the multi-row kernel's
+    cases: ragged row counts per wave, D below a full wave) against torch fp32 on the same
+    masks (fs2_keep restated in numpy).  Tolerance rel 2e-2 (bf16 outputs)."""
+    from fastspeech2 import ops
+    torch.manual_seed(M + D)
+    x = torch.randn(M, D, device=cuda).to(torch.bfloat16)
+    g = torch.randn(D, device=cuda)
+    b = torch.randn(D, device=cuda)
+    keep = (torch.rand(M, device=cuda) > 0.2).float()
+    y = torch.empty(M, D, device=cuda, dtype=torch.bfloat16)
+    mean = torch.empty(M, device=cuda)
+    rstd = torch.empty(M, device=cuda)
+    ops.ln_fwd(x, D, g, b, 1e-5, y, D, mean, rstd, M, D, dt=1)
+    dy = torch.randn(M, D, device=cuda).to(torch.bfloat16)
+    seed, so, sr, po, pr = 7, 3, 11, 0.1, 0.2
+    idx = np.arange(M * D, dtype=np.uint64)
+    ko = torch.from_numpy(_keep_ln_np(seed, so, idx, po).reshape(M, D)).to(cuda).float()
+    kr = torch.from_numpy(_keep_ln_np(seed, sr, idx, pr).reshape(M, D)).to(cuda).float()
+    xs = x.float().requires_grad_(True)
+    gr, br = g.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    o = F.layer_norm(xs, (D,), gr, br, 1e-5)
+    gg = dy.float() * keep[:, None] * ko / (1 - po)
+    o.backward(gg)
+    ds_ref = xs.grad * (x.float() > 0).float()
+    dr_ref = ds_ref * kr / (1 - pr)
+    ds = torch.empty(M, D, device=cuda, dtype=torch.bfloat16)
+    dr = torch.empty(M, D, device=cuda, dtype=torch.bfloat16)
+    dg = torch.zeros(D, device=cuda)
+    db = torch.zeros(D, device=cuda)
+    dc = torch.zeros(D, device=cuda)
+    ws = torch.empty(int(ops.ln_ws(M, D)), device=cuda)
+    ops.ln_bwd(dy, D, x, D, mean, rstd, g, b, ds, D, M, D, dt=1, ws=ws, seed=seed, p_o=po,
+               salt_o=so, row_mask=keep, relu_gate_in=1, dr=dr, p_r=pr, salt_r=sr,
+               dgamma=dg, dbeta=db, dcol=dc)
+    assert rel(ds, ds_ref) < 2e-2
+    assert rel(dr, dr_ref) < 2e-2
+    assert rel(dg, gr.grad) < 2e-2
+    assert rel(db, br.grad) < 2e-2
+    assert rel(dc, dr_ref.sum(0)) < 2e-2
+
+
 def test_attention_mask_quirk_against_torch_mha(cuda, golden_dir):
     """The golden torch-MHA output (reference mask expression) through our kernels, fp32."""
     from fastspeech2 import ops
