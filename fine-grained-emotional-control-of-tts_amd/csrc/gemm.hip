@@ -1367,8 +1367,12 @@ int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
       FS2_CHECK_LAUNCH();
       return 0;
     }
+    // 256x128 tiles down to 60 of them (M = 6400 encoder / predictor GEMMs: 75 tiles beat the
+    // 150 tiles of the 128x128 kernel, e.g. predictor conv fwd 45 -> 31 us); FS2_GEMM_BIG_MIN
+    // overrides for A/B runs
+    static const int big_min = [] { const char* v = std::getenv("FS2_GEMM_BIG_MIN"); return v ? std::atoi(v) : 60; }();
     const bool use_big = !no_big && p.conv_mode != 2 &&
-                         ((p.vec_ok && p.split_k <= 1 && tiles_big * batch >= 240) ||
+                         ((p.vec_ok && p.split_k <= 1 && tiles_big * batch >= big_min) ||
                           (slices && p.vec_ok && tiles_big * p.split_k >= 160) ||
                           (wgrad && tiles_big * split_big >= 160));
     if (use_big) {

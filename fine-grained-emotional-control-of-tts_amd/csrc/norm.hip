@@ -389,7 +389,7 @@ __global__ void __launch_bounds__(256) ln_bwd_vec_kernel(LnBwdP p, float* part, 
 // wave loads R rows (r, r+4, ..., r+4(R-1)) before computing any of them.  No tanh gate (that
 // case keeps the one-row kernel).  The one-row loop
 // keeps ~1.5 KB per wave in flight and ran at 1-2 TB/s (latency bound: 15 waves per CU).
-template <int R>
+template <int R, bool TANH>
 __global__ void __launch_bounds__(256) ln_bwd_rows_kernel(LnBwdP p, float* part, int npart,
                                                           int kind0) {
   constexpr int V = 8;
@@ -397,12 +397,13 @@ __global__ void __launch_bounds__(256) ln_bwd_rows_kernel(LnBwdP p, float* part,
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int d0 = lane * V;
   const bool act = d0 < p.D;
-  float pg[V], pb[V], pc[V], gm[V];
+  float pg[V], pb[V], pc[V], gm[V], bt[V];
 #pragma unroll
-  for (int e = 0; e < V; ++e) { pg[e] = 0.f; pb[e] = 0.f; pc[e] = 0.f; gm[e] = 0.f; }
+  for (int e = 0; e < V; ++e) { pg[e] = 0.f; pb[e] = 0.f; pc[e] = 0.f; gm[e] = 0.f; bt[e] = 0.f; }
   if (act) {
     vload<float>(gm, p.gamma + d0);
     vload<float>(gm + 4, p.gamma + d0 + 4);
+    if constexpr (TANH) { vload<float>(bt, p.beta + d0); vload<float>(bt + 4, p.beta + d0 + 4); }
     
   }
   const float inv_o = p.p_o > 0.f ? 1.f / (1.f - p.p_o) : 1.f;
@@ -443,6 +444,10 @@ __global__ void __launch_bounds__(256) ln_bwd_rows_kernel(LnBwdP p, float* part,
           float gg = dv * rm[j];
           if (p.p_o > 0.f)
             gg = fs2_keep(p.seed, p.salt_o, (uint64_t)row * p.D + d0 + e, p.p_o) ? gg * inv_o : 0.f;
+          if constexpr (TANH) {
+            const float t = tanhf(xh[e] * gm[e] + bt[e]);
+            gg *= (1.f - t * t);
+          }
           pg[e] += gg * xh[e];
           pb[e] += gg;
           g[e] = gg * gm[e];
@@ -677,8 +682,9 @@ extern "C" int fs2_ln_bwd(const void* dy, int64_t lddy, const void* s, int64_t l
   const int kind0 = dgamma ? 0 : 2;
   if (dtype == FS2_BF16) {
     if (!vec) hipLaunchKernelGGL(ln_bwd_kernel<bf16>, dim3(nb), dim3(256), 0, st, p);
-    else if (nch == 1 && !do_tanh && ln_rows_r() == 4) hipLaunchKernelGGL((ln_bwd_rows_kernel<4>), dim3(nb), dim3(256), 0, st, p, part, npart, kind0);
-    else if (nch == 1 && !do_tanh && ln_rows_r() == 2) hipLaunchKernelGGL((ln_bwd_rows_kernel<2>), dim3(nb), dim3(256), 0, st, p, part, npart, kind0);
+    else if (nch == 1 && ln_rows_r() == 4 && !do_tanh) hipLaunchKernelGGL((ln_bwd_rows_kernel<4, false>), dim3(nb), dim3(256), 0, st, p, part, npart, kind0);
+    else if (nch == 1 && ln_rows_r() == 4) hipLaunchKernelGGL((ln_bwd_rows_kernel<4, true>), dim3(nb), dim3(256), 0, st, p, part, npart, kind0);
+    else if (nch == 1 && ln_rows_r() == 2 && !do_tanh) hipLaunchKernelGGL((ln_bwd_rows_kernel<2, false>), dim3(nb), dim3(256), 0, st, p, part, npart, kind0);
     else if (nch == 1) hipLaunchKernelGGL((ln_bwd_vec_kernel<bf16, 1>), dim3(nb), dim3(256), 0, st, p, part, npart, kind0);
     else if (nch == 2) hipLaunchKernelGGL((ln_bwd_vec_kernel<bf16, 2>), dim3(nb), dim3(256), 0, st, p, part, npart, kind0);
     else hipLaunchKernelGGL((ln_bwd_vec_kernel<bf16, 4>), dim3(nb), dim3(256), 0, st, p, part, npart, kind0);

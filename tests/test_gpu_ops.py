@@ -104,7 +104,7 @@ def test_gemm_batched_attention_shapes(cuda, dt, code, tol):
 
 
 @pytest.mark.parametrize("dt,code,tol", DT)
-@pytest.mark.parametrize("D", [384, 90])
+@pytest.mark.parametrize("D", [384, 90, 80, 512])
 def test_layernorm_fwd_bwd(cuda, dt, code, tol, D):
     """D=384: 16-byte vector kernels; D=90: scalar kernels.  dcol = fused column sum of the
     emitted gradient (the bias gradient of the layer that produced s)."""
