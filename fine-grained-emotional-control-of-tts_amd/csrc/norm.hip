@@ -386,7 +386,8 @@ __global__ void __launch_bounds__(256) ln_bwd_vec_kernel(LnBwdP p, float* part, 
 
 // bf16, D <= 512 (one 16-byte chunk per lane): the same per-row arithmetic and the same
 // per-wave accumulation order as ln_bwd_vec_kernel<bf16, 1> (so identical results), but each
-// wave loads R rows (r, r+4, ..., r+4(R-1)) before computing any of them.  No tanh gate (that
+// wave loads R rows (r, r+4, ..., r+4(R-1)) before computing any of them.  The tanh-gated case
+// (PostNet, D = 512) measured no faster this way (94 vs 103 us) and keeps the one-row kernel.  No tanh gate (that
 // case keeps the one-row kernel).  The one-row loop
 // keeps ~1.5 KB per wave in flight and ran at 1-2 TB/s (latency bound: 15 waves per CU).
 template <int R, bool TANH>
@@ -683,7 +684,6 @@ extern "C" int fs2_ln_bwd(const void* dy, int64_t lddy, const void* s, int64_t l
   if (dtype == FS2_BF16) {
     if (!vec) hipLaunchKernelGGL(ln_bwd_kernel<bf16>, dim3(nb), dim3(256), 0, st, p);
     else if (nch == 1 && ln_rows_r() == 4 && !do_tanh) hipLaunchKernelGGL((ln_bwd_rows_kernel<4, false>), dim3(nb), dim3(256), 0, st, p, part, npart, kind0);
-    else if (nch == 1 && ln_rows_r() == 4) hipLaunchKernelGGL((ln_bwd_rows_kernel<4, true>), dim3(nb), dim3(256), 0, st, p, part, npart, kind0);
     else if (nch == 1 && ln_rows_r() == 2 && !do_tanh) hipLaunchKernelGGL((ln_bwd_rows_kernel<2, false>), dim3(nb), dim3(256), 0, st, p, part, npart, kind0);
     else if (nch == 1) hipLaunchKernelGGL((ln_bwd_vec_kernel<bf16, 1>), dim3(nb), dim3(256), 0, st, p, part, npart, kind0);
     else if (nch == 2) hipLaunchKernelGGL((ln_bwd_vec_kernel<bf16, 2>), dim3(nb), dim3(256), 0, st, p, part, npart, kind0);

@@ -241,3 +241,44 @@ def test_scaled_config4_fp32_matches_oracle(cuda, cfg_all):
     with torch.no_grad():
         pb = mb(g[0], g[1], g[6], g[4], g[5], intensity=inten.cuda())
     assert rel(pb[0], po[0]) <= 5e-2
+
+
+def test_bf16_stream_overlap_matches_single_stream(cuda, cfg_all):
+    """The bf16 step runs weight gradients on a side stream and the duration / pitch predictor
+    chains on an aux stream.  Same model, batch and (dropout-off) inputs with both extra streams
+    disabled must give the same outputs (bit-exact: the forward arithmetic is unchanged) and the
+    same parameter gradients up to the summation order of the predictor input gradient and the
+    split-K atomics (max rel 2e-2 per tensor, cosine >= 0.999): a missing stream dependency shows
+    up as stale or garbage gradients here."""
+    from fastspeech2.loss import Loss
+    from fastspeech2.synthetic import make_batch, as_tuple
+    _, m = _pair(cfg_all, dt=torch.bfloat16)
+    b = make_batch(B=4, tp_min=60, tp_max=90, seed=3)
+    bt, inten = as_tuple(b)
+    g = [t.cuda() for t in bt]
+
+    def run():
+        for p in m.parameters():
+            p.grad = None
+        pm = m(g[0], g[1], g[6], g[4], g[5], intensity=inten.cuda())
+        lm = Loss(**cfg_all["loss"])(pm, (g[3], g[6], g[4], g[5], g[7], g[2]), 0)
+        lm["total_loss"].backward()
+        torch.cuda.synchronize()
+        return [t.detach().clone() for t in pm[:7]], {n: p.grad.detach().clone()
+                                                       for n, p in m.named_parameters()}
+    eng = m.engine()
+    assert eng._side is not None and eng._aux is not None
+    out_a, grad_a = run()
+    side, aux = eng._side, eng._aux
+    eng._side, eng._aux = None, None
+    try:
+        out_b, grad_b = run()
+    finally:
+        eng._side, eng._aux = side, aux
+    for x, y in zip(out_a, out_b):
+        assert torch.equal(x, y)
+    for n in grad_a:
+        a, r = grad_a[n].float(), grad_b[n].float()
+        assert rel(a, r) <= 2e-2, n
+        cos = torch.nn.functional.cosine_similarity(a.flatten(), r.flatten(), dim=0).item()
+        assert cos >= 0.999, (n, cos)
