@@ -31,6 +31,42 @@ __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
   p[i] = pi; m[i] = mi; v[i] = vi;
 }
 
+// 4 elements per lane through 16-byte loads / stores (same per-element arithmetic as
+// adamw_kernel, so identical results): the scalar kernel ran at ~5.3 TB/s
+__device__ __forceinline__ void adamw_elem(float& pi, float& mi, float& vi, float gi,
+                                           float decay_mul, float w1, float beta2, float omb2,
+                                           float step_size, float bc2_sqrt, float eps,
+                                           float gscale) {
+  const float gr = gi * gscale;
+  pi = pi * decay_mul;
+  mi = (w1 < 0.5f) ? mi + w1 * (gr - mi) : gr - (gr - mi) * (1.f - w1);
+  vi = vi * beta2 + omb2 * gr * gr;
+  const float denom = sqrtf(vi) / bc2_sqrt + eps;
+  pi = pi + (-step_size) * (mi / denom);
+}
+
+__global__ void __launch_bounds__(256) adamw_vec_kernel(float* __restrict__ p,
+                                                        const float* __restrict__ g,
+                                                        float* __restrict__ m,
+                                                        float* __restrict__ v, long n4,
+                                                        float decay_mul, float w1, float beta2,
+                                                        float omb2, float step_size,
+                                                        float bc2_sqrt, float eps, float gscale) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n4) return;
+  f32x4 pp = ((const f32x4*)p)[i], gg = ((const f32x4*)g)[i];
+  f32x4 mm = ((const f32x4*)m)[i], vv = ((const f32x4*)v)[i];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    float pi = pp[e], mi = mm[e], vi = vv[e];
+    adamw_elem(pi, mi, vi, gg[e], decay_mul, w1, beta2, omb2, step_size, bc2_sqrt, eps, gscale);
+    pp[e] = pi; mm[e] = mi; vv[e] = vi;
+  }
+  ((f32x4*)p)[i] = pp;
+  ((f32x4*)m)[i] = mm;
+  ((f32x4*)v)[i] = vv;
+}
+
 template <typename T>
 __global__ void weight_prep_kernel(const float* W, int O, int C, int KW, int okc, T* Wf, int ldf,
                                    T* Wb, int ldb) {
@@ -129,11 +165,26 @@ extern "C" int fs2_adamw(float* param, const float* grad, float* exp_avg, float*
                          float grad_scale, void* stream) {
   if (n == 0) return 0;
   if (!param || !grad || !exp_avg || !exp_avg_sq) return FS2_EINVAL;
-  hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, param, grad, exp_avg, exp_avg_sq, (long)n, decay_mul,
-                     one_minus_beta1, beta2, one_minus_beta2, step_size, bc2_sqrt, eps,
-                     grad_scale);
-  FS2_CHECK_LAUNCH();
+  hipStream_t st = (hipStream_t)stream;
+  const bool al = (((uintptr_t)param | (uintptr_t)grad | (uintptr_t)exp_avg |
+                    (uintptr_t)exp_avg_sq) & 15) == 0;
+  long done = 0;
+  if (al && n >= 4) {
+    const long n4 = n / 4;
+    hipLaunchKernelGGL(adamw_vec_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st,
+                       param, grad, exp_avg, exp_avg_sq, n4, decay_mul, one_minus_beta1, beta2,
+                       one_minus_beta2, step_size, bc2_sqrt, eps, grad_scale);
+    FS2_CHECK_LAUNCH();
+    done = n4 * 4;
+  }
+  if (done < n) {
+    const long r = n - done;
+    hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)((r + 255) / 256)), dim3(256), 0, st,
+                       param + done, grad + done, exp_avg + done, exp_avg_sq + done, r,
+                       decay_mul, one_minus_beta1, beta2, one_minus_beta2, step_size, bc2_sqrt,
+                       eps, grad_scale);
+    FS2_CHECK_LAUNCH();
+  }
   return 0;
 }
 

@@ -349,10 +349,11 @@ def test_fused_loss_vs_oracle(cuda, dt):
         assert rel(gg.cpu().reshape(leaf.shape), leaf.grad) < gtol
 
 
-def test_adamw_matches_torch(cuda):
+@pytest.mark.parametrize("n", [10000, 10003])
+def test_adamw_matches_torch(cuda, n):
+    """16-byte vector kernel over n // 4 groups + scalar tail (n = 10003)."""
     from fastspeech2 import ops
     torch.manual_seed(5)
-    n = 10000
     p0 = torch.randn(n, device=cuda)
     ref = p0.clone().requires_grad_(True)
     opt = torch.optim.AdamW([ref], lr=1e-3, foreach=False)
