@@ -53,6 +53,7 @@ struct AttnP {
   float scale, scale_log2, p_drop, inv_keep;
   uint32_t seed, salt;
   uint32_t thr16;                // dropout threshold (fs2_thr16)
+  int dsum_in;                   // backward: dsum already computed (attn_dsum_kernel)
 };
 
 __device__ __forceinline__ bf16x8 ld_frag(const bf16* g) { return *(const bf16x8*)g; }
@@ -364,17 +365,23 @@ __global__ void __launch_bounds__(W8 * 64 / QG, 1) attn_bwd_dq_kernel(AttnP p) {
         qf[qg][s] = ld_frag(Qb + (long)qi[qg] * p.ldq + 32 * s + 8 * g);
         const long ro = (long)b * p.T + qi[qg];
         dof[qg][s] = ld_frag(p.dout + ro * p.lddo + h * DH + 32 * s + 8 * g);
-        const bf16x8 of = ld_frag(p.o + ro * p.ldo + h * DH + 32 * s + 8 * g);
+        if (!p.dsum_in) {
+          const bf16x8 of = ld_frag(p.o + ro * p.ldo + h * DH + 32 * s + 8 * g);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) dot += (float)dof[qg][s][e] * (float)of[e];
+          for (int e = 0; e < 8; ++e) dot += (float)dof[qg][s][e] * (float)of[e];
+        }
       } else {
         qf[qg][s] = bf16x8{};
         dof[qg][s] = bf16x8{};
       }
     }
-    dsum[qg] = xg_sum(dot);
     lse[qg] = in ? p.lse[(long)z * p.T + qi[qg]] : 0.f;
-    if (in && g == 0) p.dsum[(long)z * p.T + qi[qg]] = dsum[qg];
+    if (p.dsum_in) {
+      dsum[qg] = in ? p.dsum[(long)z * p.T + qi[qg]] : 0.f;
+    } else {
+      dsum[qg] = xg_sum(dot);
+      if (in && g == 0) p.dsum[(long)z * p.T + qi[qg]] = dsum[qg];
+    }
   }
   f32x4 qacc[ND][QG];
 #pragma unroll
@@ -473,6 +480,33 @@ __global__ void __launch_bounds__(W8 * 64 / QG, 1) attn_bwd_dq_kernel(AttnP p) {
       *(u32x2*)(row + 16 * d + 4 * g) = w;
     }
   }
+}
+
+// ------------------------------------------------------------------------------ backward D
+// D[z][q] = rowsum(dO * O) over head h's dh features, with the lane mapping and summation order
+// of the dQ kernel's own computation (lane = 16 g + row: features 32 s + 8 g + e summed over
+// s then e, then across g by xg_sum), so the values are bit-identical.  Lets the dQ and dK/dV
+// kernels run concurrently (the dK/dV kernel reads D).  One wave = 16 query rows of one z.
+template <int DH>
+__global__ void __launch_bounds__(256) attn_dsum_kernel(AttnP p) {
+  constexpr int NS = DH / 32;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
+  const int z = blockIdx.y, b = z / p.H, h = z - b * p.H;
+  const int q = (blockIdx.x * 4 + wave) * 16 + (lane & 15);
+  const bool in = q < p.T;
+  float dot = 0.f;
+  if (in) {
+    const long ro = (long)b * p.T + q;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const bf16x8 df = ld_frag(p.dout + ro * p.lddo + h * DH + 32 * s + 8 * g);
+      const bf16x8 of = ld_frag(p.o + ro * p.ldo + h * DH + 32 * s + 8 * g);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dot += (float)df[e] * (float)of[e];
+    }
+  }
+  const float d = xg_sum(dot);
+  if (in && g == 0) p.dsum[(long)z * p.T + q] = d;
 }
 
 // ------------------------------------------------------------------------------ backward dK dV
@@ -607,6 +641,20 @@ void launch_fwd(const AttnP& p, hipStream_t s) {
   if (attn_qg_fwd(DH) == 2) hipLaunchKernelGGL((attn_fwd_kernel<DH, 2>), grid, dim3(256), 0, s, p);
   else hipLaunchKernelGGL((attn_fwd_kernel<DH, 1>), grid, dim3(512), 0, s, p);
 }
+// staged backward: 0 = D only, 1 = dQ (D precomputed), 2 = dK/dV (D precomputed)
+template <int DH>
+void launch_bwd_stage(const AttnP& p, int stage, hipStream_t s) {
+  dim3 g1((p.T + 127) / 128, p.B * p.H);
+  if (stage == 0) {
+    hipLaunchKernelGGL(attn_dsum_kernel<DH>, dim3((p.T + 63) / 64, p.B * p.H), dim3(256), 0, s, p);
+  } else if (stage == 1) {
+    if (DH <= 64) hipLaunchKernelGGL((attn_bwd_dq_kernel<DH, 2>), g1, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((attn_bwd_dq_kernel<DH, 1>), g1, dim3(512), 0, s, p);
+  } else {
+    hipLaunchKernelGGL(attn_bwd_dkv_kernel<DH>, g1, dim3(512), 0, s, p);
+  }
+}
+
 template <int DH>
 void launch_bwd(const AttnP& p, hipStream_t s) {
   // measured neutral for the backward at T = 200 (67.5 vs 68.4 us): only on explicit request
@@ -666,11 +714,12 @@ extern "C" int fs2_attn_fwd(const void* qkv, int64_t ldq, const uint8_t* key_pad
   return 0;
 }
 
-extern "C" int fs2_attn_bwd(const void* qkv, int64_t ldq, const uint8_t* key_pad, int mask_mode,
-                            const void* out, int64_t ldo, const void* dout, int64_t lddo,
-                            const float* lse, int B, int H, int T, int dh, float scale,
-                            float p_drop, uint32_t seed, uint32_t salt, void* dqkv,
-                            int64_t lddq, float* workspace, int dtype, void* stream) {
+namespace {
+int attn_bwd_impl(const void* qkv, int64_t ldq, const uint8_t* key_pad, int mask_mode,
+                  const void* out, int64_t ldo, const void* dout, int64_t lddo, const float* lse,
+                  int B, int H, int T, int dh, float scale, float p_drop, uint32_t seed,
+                  uint32_t salt, void* dqkv, int64_t lddq, float* workspace, int dtype,
+                  void* stream, int stage) {
   if (int rc = check(B, H, T, dh, ldq, qkv, dtype)) return rc;
   if (!key_pad || !out || !dout || !lse || !dqkv || !workspace) return FS2_EINVAL;
   if (!a16(out) || !a16(dout) || !a16(dqkv) || (ldo % 8) || (lddo % 8) || (lddq % 8))
@@ -687,14 +736,46 @@ extern "C" int fs2_attn_bwd(const void* qkv, int64_t ldq, const uint8_t* key_pad
   p.seed = seed; p.salt = salt;
   p.thr16 = (uint32_t)(p_drop * 65536.f + 0.5f);
   hipStream_t s = (hipStream_t)stream;
-  switch (dh) {
-    case 64: launch_bwd<64>(p, s); break;
-    case 128: launch_bwd<128>(p, s); break;
-    case 192: launch_bwd<192>(p, s); break;
-    default: launch_bwd<256>(p, s); break;
+  if (stage < 0) {
+    switch (dh) {
+      case 64: launch_bwd<64>(p, s); break;
+      case 128: launch_bwd<128>(p, s); break;
+      case 192: launch_bwd<192>(p, s); break;
+      default: launch_bwd<256>(p, s); break;
+    }
+  } else {
+    p.dsum_in = 1;
+    switch (dh) {
+      case 64: launch_bwd_stage<64>(p, stage, s); break;
+      case 128: launch_bwd_stage<128>(p, stage, s); break;
+      case 192: launch_bwd_stage<192>(p, stage, s); break;
+      default: launch_bwd_stage<256>(p, stage, s); break;
+    }
   }
   FS2_CHECK_LAUNCH();
   return 0;
+}
+
+}  // namespace
+
+extern "C" int fs2_attn_bwd(const void* qkv, int64_t ldq, const uint8_t* key_pad, int mask_mode,
+                            const void* out, int64_t ldo, const void* dout, int64_t lddo,
+                            const float* lse, int B, int H, int T, int dh, float scale,
+                            float p_drop, uint32_t seed, uint32_t salt, void* dqkv,
+                            int64_t lddq, float* workspace, int dtype, void* stream) {
+  return attn_bwd_impl(qkv, ldq, key_pad, mask_mode, out, ldo, dout, lddo, lse, B, H, T, dh,
+                       scale, p_drop, seed, salt, dqkv, lddq, workspace, dtype, stream, -1);
+}
+
+extern "C" int fs2_attn_bwd_stage(const void* qkv, int64_t ldq, const uint8_t* key_pad,
+                                  int mask_mode, const void* out, int64_t ldo, const void* dout,
+                                  int64_t lddo, const float* lse, int B, int H, int T, int dh,
+                                  float scale, float p_drop, uint32_t seed, uint32_t salt,
+                                  void* dqkv, int64_t lddq, float* workspace, int dtype,
+                                  int stage, void* stream) {
+  if (stage < 0 || stage > 2) return FS2_EINVAL;
+  return attn_bwd_impl(qkv, ldq, key_pad, mask_mode, out, ldo, dout, lddo, lse, B, H, T, dh,
+                       scale, p_drop, seed, salt, dqkv, lddq, workspace, dtype, stream, stage);
 }
 
 extern "C" int64_t fs2_attn_workspace_floats(int B, int H, int T) { return (int64_t)B * H * T; }

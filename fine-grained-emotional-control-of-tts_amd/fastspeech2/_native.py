@@ -97,6 +97,8 @@ SIGNATURES = {
     "fs2_attn_bwd": (I, [P, I64, P, I, P, I64, P, I64, P, I, I, I, I, Fl, Fl, U32, U32, P, I64,
                          P, I, P]),
     "fs2_attn_workspace_floats": (I64, [I, I, I]),
+    "fs2_attn_bwd_stage": (I, [P, I64, P, I, P, I64, P, I64, P, I, I, I, I, Fl, Fl, U32, U32, P,
+                               I64, P, I, I, P]),
     "fs2_softmax_fwd": (I, [P, P, I, I, I, I, I, I, Fl, Fl, U32, U32, P, P, I, P]),
     "fs2_softmax_bwd": (I, [P, P, I, I, I, I, I, Fl, Fl, U32, U32, P, I, P]),
     "fs2_embed_fwd": (I, [P, P, P, I, I, I, I, P, P, I, P]),

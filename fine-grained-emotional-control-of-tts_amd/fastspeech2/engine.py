@@ -61,6 +61,9 @@ def dgrad_split(Mp, C, K, dt, n_cu=256, max_split=8):
 _NO_SLICES = os.environ.get("FS2_NO_WGRAD_SLICES", "0") not in ("", "0")
 _NO_SIDE = os.environ.get("FS2_NO_SIDE_STREAM", "0") not in ("", "0")
 _NO_AUX = os.environ.get("FS2_NO_AUX_STREAM", "0") not in ("", "0")
+# dQ and dK/dV of the encoder attention on two streams: opt-in, measured no faster (the side
+# stream's weight gradients already fill those CUs: A/B 22.49-22.54 off vs 22.56-22.59 on)
+_ATTN_SPLIT = os.environ.get("FS2_ATTN_SPLIT", "0") not in ("", "0")
 
 
 def wgrad_slices(O, Ncols, ldc, K, dt, n_cu=256):
@@ -439,9 +442,20 @@ class FS2Engine:
             tag = self._dtag("attn_bwd", "", T)
             if tag:
                 self._tic(tag)
-            ops.attn_bwd(QKV, 3 * D, ctx["key_pad"], ctx["Att"], D, dAtt, D, ctx["lse"], B, H, T,
-                         dh, 1.0 / math.sqrt(dh), p_drop, seed, ctx["s_att"], dQKV, 3 * D,
-                         dt=self.dt, ws=self.ws(ops.attn_ws(B, H, T)))
+            args = (QKV, 3 * D, ctx["key_pad"], ctx["Att"], D, dAtt, D, ctx["lse"], B, H, T, dh,
+                    1.0 / math.sqrt(dh), p_drop, seed, ctx["s_att"], dQKV, 3 * D)
+            ws = self.ws(ops.attn_ws(B, H, T))
+            if self._aux is not None and _ATTN_SPLIT and -(-T // 128) * B * H < 256:
+                # dQ and dK/dV blocks each fill < 1 round of the 256 CUs (the encoder): run
+                # them on two streams after the shared D = rowsum(dO*O) pass
+                ops.attn_bwd_stage(0, *args, dt=self.dt, ws=ws)
+                h = self._aux_fork(QKV, ctx["key_pad"], dAtt, ctx["lse"], dQKV, ws)
+                ops.attn_bwd_stage(2, *args, dt=self.dt, ws=ws)
+                self._aux_exit(h)
+                ops.attn_bwd_stage(1, *args, dt=self.dt, ws=ws)
+                self._aux_join(h[1])
+            else:
+                ops.attn_bwd(*args, dt=self.dt, ws=ws)
             if tag:
                 self._toc(tag)
             return self._qkv_bwd(dQKV, ctx, M, T, D, prefix, ds1)

@@ -113,6 +113,16 @@ def attn_fwd(qkv, ldq, key_pad, B, H, T, dh, scale, p_drop, seed, salt, out, ldo
          "fs2_attn_fwd")
 
 
+def attn_bwd_stage(stage, qkv, ldq, key_pad, out, ldo, dout, lddo, lse, B, H, T, dh, scale,
+                   p_drop, seed, salt, dqkv, lddq, *, dt, ws, mask_mode=1):
+    """one stage of ``attn_bwd``: 0 = D = rowsum(dO*O) into ws, 1 = dQ, 2 = dK/dV (1 and 2
+    read D, in either order or concurrently)."""
+    _chk(N.lib().fs2_attn_bwd_stage(_p(qkv), ldq, _p(key_pad), mask_mode, _p(out), ldo, _p(dout),
+                                    lddo, _p(lse), B, H, T, dh, scale, p_drop, seed & 0xffffffff,
+                                    salt, _p(dqkv), lddq, _p(ws), dt, stage, _s()),
+         "fs2_attn_bwd_stage")
+
+
 def attn_bwd(qkv, ldq, key_pad, out, ldo, dout, lddo, lse, B, H, T, dh, scale, p_drop, seed, salt,
              dqkv, lddq, *, dt, ws, mask_mode=1):
     _chk(N.lib().fs2_attn_bwd(_p(qkv), ldq, _p(key_pad), mask_mode, _p(out), ldo, _p(dout), lddo,

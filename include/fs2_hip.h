@@ -156,6 +156,15 @@ int fs2_attn_bwd(const void* qkv, int64_t ldq, const uint8_t* key_pad, int mask_
                  int T, int dh, float scale, float p_drop, uint32_t seed, uint32_t salt,
                  void* dqkv, int64_t lddq, float* workspace, int dtype, void* stream);
 int64_t fs2_attn_workspace_floats(int B, int H, int T);
+/* fs2_attn_bwd in three stream-ordered stages, so dQ and dK/dV can run on two streams when one
+ * alone underfills the chip: stage 0 writes D = rowsum(dO*O) into workspace, then stage 1 (dQ)
+ * and stage 2 (dK, dV) both read it (each after stage 0; no order between 1 and 2).  Results
+ * are bit-identical to fs2_attn_bwd.                                                       */
+int fs2_attn_bwd_stage(const void* qkv, int64_t ldq, const uint8_t* key_pad, int mask_mode,
+                       const void* out, int64_t ldo, const void* dout, int64_t lddo,
+                       const float* lse, int B, int H, int T, int dh, float scale, float p_drop,
+                       uint32_t seed, uint32_t salt, void* dqkv, int64_t lddq, float* workspace,
+                       int dtype, int stage, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Token embedding + positional encoding + pad mask (K1, K2; model.py:331-337)

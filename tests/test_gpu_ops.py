@@ -533,3 +533,38 @@ def test_fused_attention_vs_torch(cuda, dh, T, p_drop):
     for i, t in enumerate((q, k, v)):
         r = t.grad.permute(0, 2, 1, 3).reshape(B * T, D)
         assert rel(dqkv[:, i * D:(i + 1) * D], r) < 3e-2, i
+
+
+@pytest.mark.parametrize("dh,T,p_drop", [(192, 200, 0.1), (64, 70, 0.0)])
+def test_attention_backward_stages_equal_fused(cuda, dh, T, p_drop):
+    """fs2_attn_bwd_stage: D pass, then dQ and dK/dV on two streams, bit-identical to the
+    one-call fs2_attn_bwd (the engine splits the encoder's backward this way)."""
+    from fastspeech2 import ops
+    torch.manual_seed(dh * T)
+    B, H = 4, 2
+    D = H * dh
+    qkv = (torch.randn(B * T, 3 * D, device=cuda) * 0.5).to(torch.bfloat16)
+    kp = torch.zeros(B, T, dtype=torch.uint8, device=cuda)
+    for b, L in enumerate([T, T - 11, T - 40, 5]):
+        kp[b, L:] = 1
+    scale = 1.0 / math.sqrt(dh)
+    out = torch.empty(B * T, D, device=cuda, dtype=torch.bfloat16)
+    lse = torch.empty(B * H, T, device=cuda)
+    ops.attn_fwd(qkv, 3 * D, kp, B, H, T, dh, scale, p_drop, 9, 4, out, D, lse, dt=1)
+    dout = torch.randn(B * T, D, device=cuda).to(torch.bfloat16)
+    args = (qkv, 3 * D, kp, out, D, dout, D, lse, B, H, T, dh, scale, p_drop, 9, 4)
+    ref = torch.full((B * T, 3 * D), float("nan"), device=cuda, dtype=torch.bfloat16)
+    ws = torch.empty(int(ops.attn_ws(B, H, T)), device=cuda)
+    ops.attn_bwd(*args, ref, 3 * D, dt=1, ws=ws)
+    got = torch.full_like(ref, float("nan"))
+    ws2 = torch.empty_like(ws)
+    ops.attn_bwd_stage(0, *args, got, 3 * D, dt=1, ws=ws2)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        ops.attn_bwd_stage(2, *args, got, 3 * D, dt=1, ws=ws2)
+    ops.attn_bwd_stage(1, *args, got, 3 * D, dt=1, ws=ws2)
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    assert torch.equal(ws, ws2)
+    assert torch.equal(got, ref)
