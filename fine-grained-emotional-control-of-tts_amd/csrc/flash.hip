@@ -109,6 +109,12 @@ __device__ __forceinline__ void blds16(i32x4 rsrc, int voff, int soff, char* lds
                            voff, soff, 0, 0);
 }
 
+// 4-byte variant: 64 lanes x 4 B land contiguously (one float per lane, e.g. a row statistic)
+__device__ __forceinline__ void blds4(i32x4 rsrc, int voff, int soff, char* lds_wave_base) {
+  llvm_raw_buffer_load_lds(rsrc, (__attribute__((address_space(3))) uint32_t*)lds_wave_base, 4,
+                           voff, soff, 0, 0);
+}
+
 // A 64-row x DH tile image (16-byte chunk c of row r stored at c ^ (r & 7)) filled by LDS-DMA:
 // 1 KiB instruction i covers image bytes [1024 i, 1024 i + 1024) and each lane fetches the
 // logical chunk that lands at its slot.  NW waves issue NI / NW instructions each.
@@ -510,15 +516,19 @@ __global__ void __launch_bounds__(256) attn_dsum_kernel(AttnP p) {
 }
 
 // ------------------------------------------------------------------------------ backward dK dV
-// block: W8 waves x 16 keys; query tiles of 64 (Q, dO, lse, D staged in LDS)
+// block: W8 waves x 16 keys; query tiles of 64 (Q, dO, lse, D staged in LDS).  Q / dO tiles are
+// double-buffered through LDS-DMA (tile t+1 streams in while tile t computes; the one-buffer
+// version exposed each tile's load); wave 0 streams tile t+1's lse / D rows the same way.
 template <int DH, int W8 = 8>
 __global__ void __launch_bounds__(W8 * 64, 1) attn_bwd_dkv_kernel(AttnP p) {
   constexpr int NS = DH / 32, ND = DH / 16;
-  __shared__ __attribute__((aligned(16))) char Qs[64 * DH * 2];
-  __shared__ __attribute__((aligned(16))) char Os[64 * DH * 2];  // dO tile
-  __shared__ float ls_s[64], ds_s[64];
-  __shared__ uint8_t kval[TMAX];
-  __shared__ int kend_s;
+  constexpr int TB = 64 * DH * 2;
+  // one LDS array (a second __shared__ object can make hipcc drain the DMA ring early):
+  // [Q 0 | dO 0 | Q 1 | dO 1 | (lse, D) 0 | (lse, D) 1 | kval | kend]
+  __shared__ __attribute__((aligned(16))) char smem[4 * TB + 1024 + TMAX + 16];
+  float* lsd = (float*)(smem + 4 * TB);
+  uint8_t* kval = (uint8_t*)(smem + 4 * TB + 1024);
+  int& kend_s = *(int*)(smem + 4 * TB + 1024 + TMAX);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
   const int z = blockIdx.y, b = z / p.H, h = z - b * p.H;
   const uint32_t dkey = fs2_drop_key(p.seed, p.salt);
@@ -544,16 +554,44 @@ __global__ void __launch_bounds__(W8 * 64, 1) attn_bwd_dkv_kernel(AttnP p) {
   // a block whose keys are all masked contributes nothing: skip the query loop
   const int anyk = __syncthreads_or(kok);
 
-  for (int q0 = 0; anyk && q0 < p.T; q0 += 64) {
-    __syncthreads();
-    load_tile<DH, 64>(Qs, Qb, p.ldq, q0, p.T, threadIdx.x, W8 * 64);
-    load_tile<DH, 64>(Os, dOb, p.lddo, q0, p.T, threadIdx.x, W8 * 64);
-    if (threadIdx.x < 64) {
-      const int q = q0 + threadIdx.x;
-      ls_s[threadIdx.x] = q < p.T ? p.lse[(long)z * p.T + q] : 0.f;
-      ds_s[threadIdx.x] = q < p.T ? p.dsum[(long)z * p.T + q] : 0.f;
+  TileDma<DH, W8> dma;
+  dma.init(wave, lane, 0);
+  const i32x4 rsQ = make_rsrc(Qb), rsO = make_rsrc(dOb);
+  const int ntile = anyk ? (p.T + 63) / 64 : 0;
+  // lse / D rows of a tile: wave 0 streams them in by 4-byte LDS-DMA (no registers held)
+  const i32x4 rsL = make_rsrc(p.lse + (long)z * p.T), rsD = make_rsrc(p.dsum + (long)z * p.T);
+  auto issue_stats = [&](int q0, int buf) {
+    if (wave == 0) {
+      const int vo = q0 + lane < p.T ? lane * 4 : BUF_OOB;
+      blds4(rsL, vo, q0 * 4, (char*)(lsd + buf * 128));
+      blds4(rsD, vo, q0 * 4, (char*)(lsd + buf * 128 + 64));
     }
-    __syncthreads();
+  };
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // K/V fragments resident before the ring
+  if (ntile > 0) {
+    issue_stats(0, 0);
+    dma.issue(smem, rsQ, p.ldq, 0, p.T, wave);
+    dma.issue(smem + TB, rsO, p.lddo, 0, p.T, wave);
+  }
+  for (int t = 0; t < ntile; ++t) {
+    const int q0 = t * 64;
+    const char* Qs = smem + (t & 1) * 2 * TB;
+    const char* Os = Qs + TB;
+    const float* ls_s = lsd + (t & 1) * 128;
+    const float* ds_s = ls_s + 64;
+    if (t + 1 < ntile) {
+      issue_stats(q0 + 64, (t + 1) & 1);
+      char* nx = smem + ((t + 1) & 1) * 2 * TB;
+      dma.issue(nx, rsQ, p.ldq, q0 + 64, p.T, wave);
+      dma.issue(nx + TB, rsO, p.lddo, q0 + 64, p.T, wave);
+      // tile t's pieces landed (wave 0 also has its two lse / D loads behind them)
+      if (wave == 0) wait_vmcnt<2 * TileDma<DH, W8>::PER + 2>();
+      else wait_vmcnt<2 * TileDma<DH, W8>::PER>();
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
     // S = Q K^T, dP = dO V^T for 64 queries x this wave's 16 keys (C: col key, rows queries)
     f32x4 sacc[4], pacc[4];
 #pragma unroll
@@ -598,6 +636,7 @@ __global__ void __launch_bounds__(W8 * 64, 1) attn_bwd_dkv_kernel(AttnP p) {
         dk[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sa, qb, dk[d], 0, 0, 0);
       }
     }
+    __builtin_amdgcn_s_barrier();   // every wave is done with buffer t & 1 before t+2 lands
   }
   // C layout: col = feature (lane & 15), rows = keys 4g + r of this wave's 16
 #pragma unroll
