@@ -696,9 +696,9 @@ void launch_bwd_stage(const AttnP& p, int stage, hipStream_t s) {
 
 template <int DH>
 void launch_bwd(const AttnP& p, hipStream_t s) {
-  // measured neutral for the backward at T = 200 (67.5 vs 68.4 us): only on explicit request
-  static const bool small_bwd = [] { const char* v = std::getenv("FS2_ATTN_W8"); return v && std::atoi(v) == 4; }();
-  if (small_bwd) {
+  // 64-key / 64-query blocks when 128-row blocks underfill the chip, as the forward (encoder
+  // T = 200 with the LDS-DMA dK/dV kernel: 60.2 -> 56.7 us; FS2_ATTN_W8=4 / 8 forces either)
+  if (attn_small_blocks(p)) {
     dim3 g1((p.T + 63) / 64, p.B * p.H);
     if (DH <= 64) hipLaunchKernelGGL((attn_bwd_dq_kernel<DH, 2, 4>), g1, dim3(128), 0, s, p);
     else hipLaunchKernelGGL((attn_bwd_dq_kernel<DH, 1, 4>), g1, dim3(256), 0, s, p);
