@@ -1315,7 +1315,10 @@ int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
     int split_big = 1;
     if (wgrad) {
       const int nk = (p.K + 63) / 64;
-      split_big = max(1, min((480 + tiles_big - 1) / tiles_big, nk / 8));
+      // ~one round of blocks: fewer K slices halve the fp32 atomics (decoder QKV weight
+      // gradient 95 -> 75 us vs two rounds); FS2_WGRAD_BIG_TARGET overrides for A/B runs
+      static const int tgt = [] { const char* v = std::getenv("FS2_WGRAD_BIG_TARGET"); return v ? std::atoi(v) : 240; }();
+      split_big = max(1, min((tgt + tiles_big - 1) / tiles_big, nk / 8));
     }
     const bool slices = p.split_stride > 0 && p.split_k > 1;  // caller-chosen split, plain stores
     // 256x256 phased kernel: wide outputs (< 10 % column padding; the QKV projection's
