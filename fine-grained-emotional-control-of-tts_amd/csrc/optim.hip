@@ -117,13 +117,21 @@ __global__ void __launch_bounds__(256) weight_prep_batched_kernel(const fs2_wpre
   const int o0 = to * 64, k0 = tk * 64;
   const int KC = d.KW * d.C;
   T* Wf = (T*)d.Wf;
+  // (tap j, channel c) of the tile's 64 k columns, one division each instead of one per element
+  __shared__ int jcs[64];
+  if (threadIdx.x < 64) {
+    const int k = k0 + threadIdx.x;
+    const int j = k / d.C;
+    jcs[threadIdx.x] = (j << 16) | (k - j * d.C);
+  }
+  __syncthreads();
   // read (coalesced along k for the [O][KW][C] layout) -> Wf, and stage for the transpose
   for (int i = threadIdx.x; i < 64 * 64; i += blockDim.x) {
     const int ol = i >> 6, kl = i & 63, o = o0 + ol, k = k0 + kl;
     if (o >= d.O || k >= d.ldf) continue;
     float v = 0.f;
     if (k < KC) {
-      const int j = k / d.C, c = k - j * d.C;
+      const int j = jcs[kl] >> 16, c = jcs[kl] & 0xffff;
       v = d.w_okc ? d.W[(long)o * KC + k] : d.W[((long)o * d.C + c) * d.KW + j];
     }
     Wf[(long)o * d.ldf + k] = from_f<T>(v);
@@ -136,7 +144,7 @@ __global__ void __launch_bounds__(256) weight_prep_batched_kernel(const fs2_wpre
   for (int i = threadIdx.x; i < 64 * 64; i += blockDim.x) {
     const int kl = i >> 6, ol = i & 63, o = o0 + ol, k = k0 + kl;
     if (o >= d.O || k >= KC) continue;
-    const int j = k / d.C, c = k - j * d.C;
+    const int j = jcs[kl] >> 16, c = jcs[kl] & 0xffff;
     Wb[(long)c * d.ldb + (long)j * d.O + o] = from_f<T>(tile[ol][kl]);
   }
 }

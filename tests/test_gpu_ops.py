@@ -568,3 +568,30 @@ def test_attention_backward_stages_equal_fused(cuda, dh, T, p_drop):
     torch.cuda.synchronize()
     assert torch.equal(ws, ws2)
     assert torch.equal(got, ref)
+
+
+def test_weight_prep_batched_layouts(cuda):
+    """fs2_weight_prep_batched: fp32 masters ([O][KW][C] conv weights, [O][C] linear weights,
+    shapes not multiples of the 64x64 tile) -> bf16 Wf[O][ldf] (zero column padding) and
+    Wb[C][KW*O], exactly the bf16 rounding of the expected images."""
+    from fastspeech2 import ops
+    torch.manual_seed(12)
+    shapes = [(384, 384, 9), (80, 384, 1), (130, 72, 5), (1152, 384, 1)]
+    entries, refs = [], []
+    for O, C, KW in shapes:
+        W = torch.randn(O, KW, C, device=cuda) if KW > 1 else torch.randn(O, C, device=cuda)
+        ldf = ops.round_up(KW * C, 8)
+        Wf = torch.full((O, ldf), float("nan"), device=cuda).to(torch.bfloat16)
+        Wb = torch.full((C, KW * O), float("nan"), device=cuda).to(torch.bfloat16)
+        entries.append((W, O, C, KW, int(KW > 1), Wf, ldf, Wb, KW * O))
+        W3 = W.view(O, KW, C)
+        ref_f = torch.zeros(O, ldf, device=cuda)
+        ref_f[:, :KW * C] = W3.reshape(O, KW * C)
+        ref_b = W3.permute(2, 1, 0).reshape(C, KW * O)      # [c][j*O + o]
+        refs.append((Wf, Wb, ref_f.to(torch.bfloat16), ref_b.to(torch.bfloat16)))
+    table = ops.weight_prep_table(entries)
+    ops.weight_prep_batched(*table, dt=1)
+    torch.cuda.synchronize()
+    for Wf, Wb, rf, rb in refs:
+        assert torch.equal(Wf, rf)
+        assert torch.equal(Wb, rb)
