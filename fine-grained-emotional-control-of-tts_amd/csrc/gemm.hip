@@ -1332,8 +1332,11 @@ int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
       const int nk = (p.K + 63) / 64;
       split256 = max(1, min((240 + tiles256 - 1) / tiles256, nk / 8));
     }
+    // from 150 tiles: the encoder FFN conv1 forward (M = 6400, N = 1536: 150 tiles of 256^2 in
+    // one round vs 300 of 256x128 in 1.2 rounds) 122 -> 112 us; FS2_G4_MIN_TILES overrides
+    static const int g4_min = [] { const char* v = std::getenv("FS2_G4_MIN_TILES"); return v ? std::atoi(v) : 150; }();
     const bool use256 = !no256 && wide && p.conv_mode != 2 &&
-                        ((p.vec_ok && p.split_k <= 1 && tiles256 * batch >= 200) ||
+                        ((p.vec_ok && p.split_k <= 1 && tiles256 * batch >= g4_min) ||
                          (slices && p.vec_ok && tiles256 * p.split_k >= 160) ||
                          (wgrad && tiles256 * split256 >= 160));
     if (use256) {
