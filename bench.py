@@ -33,7 +33,13 @@ def parse():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--max-shape", action="store_true", help="all T_phon=200, d=5 (T_mel=1000)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-utts", type=int, default=2)
+    ap.add_argument("--cpu-utts", type=int, default=0,
+                    help="CPU baseline batch size (default: the bench batch itself)")
+    ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--single-speaker", action="store_true",
+                    help="every utterance speaker 0 (BASELINE config 2 with --batch 16)")
+    ap.add_argument("--no-fp32-leg", action="store_true")
+    ap.add_argument("--no-config2-leg", action="store_true")
     ap.add_argument("--scaled", action="store_true",
                     help="BASELINE config 4: scaled FastSpeech2, hidden 512, FFN 2048, 6+6 layers")
     ap.add_argument("--detail", action="store_true",
@@ -54,31 +60,101 @@ def scaled_config(cfg_all):
     return c
 
 
+def cpu_threads():
+    """Host threads for the CPU baseline: the cores this process may run on (sched affinity),
+    capped by OMP_NUM_THREADS when the box sets it (the GPU pool gives one GPU's job a 16-core
+    share of a much larger host: os.cpu_count() reports the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
 def cpu_baseline(cfg_all, args):
-    """Oracle (op-for-op PyTorch-CPU fp32 restatement of the reference train step) on a bounded
-    sample of the same workload: ``cpu_utts`` utterances, 1 warm-up + 2 timed steps."""
+    """Oracle (op-for-op PyTorch-CPU fp32 restatement of the reference train step) on
+    the SAME synthetic B-utterance batch as the GPU line (rank 0's, seed 0), 1 warm-up step then
+    the median of ``cpu_steps`` timed steps."""
     from oracle.fs2_oracle import FastSpeech2Oracle, LossOracle, train_step
     from fastspeech2.synthetic import make_batch, as_tuple
-    cores = min(16, os.cpu_count() or 1)
+    cores = cpu_threads()
     torch.set_num_threads(cores)
     torch.manual_seed(0)
     model = FastSpeech2Oracle(**cfg_all["model"]["fastspeech2"], n_speakers=4).train()
     crit = LossOracle(**cfg_all["loss"])
     opt = torch.optim.AdamW(model.parameters(), lr=cfg_all["train"]["learning_rate"])
-    b = make_batch(B=args.cpu_utts, seed=1000, max_shape=args.max_shape)
+    b = make_batch(B=args.cpu_utts or args.batch, seed=0, max_shape=args.max_shape,
+                   single_speaker=args.single_speaker)
     bt, inten = as_tuple(b)
     train_step(model, crit, opt, bt, inten)
     ts = []
-    for _ in range(2):
+    for _ in range(args.cpu_steps):
         t0 = time.perf_counter()
         train_step(model, crit, opt, bt, inten)
         ts.append(time.perf_counter() - t0)
     t = sorted(ts)[len(ts) // 2]
     frames = int(b["mel_len"].sum())
     return {"value": frames / t, "unit": "mel-frames/s", "cores": cores, "kind": "port",
-            "sample": f"{args.cpu_utts} utterances of the same synthetic workload "
-                      f"({frames} valid mel frames, T_mel_max={b['mel'].shape[1]}), fp32, dropout on, "
-                      f"median of 2 steps after 1 warm-up; oracle/fs2_oracle.py"}
+            "host_cpu_count": os.cpu_count(),
+            "sample": f"the bench batch itself: B={b['mel'].shape[0]} utterances ({frames} valid mel "
+                      f"frames, T_mel_max={b['mel'].shape[1]}), fp32, dropout on, {cores} threads "
+                      f"(sched affinity / OMP_NUM_THREADS; os.cpu_count()={os.cpu_count()}), "
+                      f"median of {len(ts)} steps after 1 warm-up ({t:.2f} s/step); "
+                      f"oracle/fs2_oracle.py"}
+
+
+def timed_leg(trainer, bt, inten, Tm, frames_local, steps, warmup, world):
+    """K timed steps of ``trainer`` on one resident batch (barrier + synchronize on both sides,
+    max over ranks); returns (whole-job frames/s, ms per step)."""
+    for _ in range(warmup):
+        trainer.step(bt, inten, mel_len_max=Tm)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        trainer.step(bt, inten, mel_len_max=Tm)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = torch.tensor([time.perf_counter() - t0], device="cuda")
+    fr = torch.tensor([frames_local], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        dist.all_reduce(fr, op=dist.ReduceOp.SUM)
+    el = float(el.item())
+    return float(fr.item()) * steps / el, el / steps * 1e3
+
+
+def secondary_legs(cfg_all, args, rank, world):
+    """Secondary lines beside ``value``: the fp32 train step (the reference trains in fp32, no
+    AMP: train.py:72-81) at the same batch, and BASELINE config 2 (B=16, single speaker 'bea',
+    bf16)."""
+    from fastspeech2.model import FastSpeech2
+    from fastspeech2.train import FusedTrainer
+    from fastspeech2.synthetic import make_batch, as_tuple
+    out = {}
+    legs = []
+    if not args.no_fp32_leg and args.dtype != "fp32":
+        legs.append(("fp32", torch.float32, args.batch, args.single_speaker, 3, 1))
+    if not args.no_config2_leg and not (args.batch == 16 and args.single_speaker):
+        legs.append(("config2_b16_single_speaker_bf16", torch.bfloat16, 16, True, args.steps, 3))
+    for name, dt, B, single, steps, warm in legs:
+        torch.manual_seed(0)
+        model = FastSpeech2(**cfg_all["model"]["fastspeech2"], n_speakers=4, act_dtype=dt).cuda().train()
+        tr = FusedTrainer(model, lr=cfg_all["train"]["learning_rate"])
+        b = make_batch(B=B, seed=rank, max_shape=args.max_shape, device="cuda",
+                       single_speaker=single)
+        bt, inten = as_tuple(b)
+        v, ms = timed_leg(tr, bt, inten, b["mel"].shape[1], int(b["mel_len"].sum()), steps, warm,
+                          world)
+        out[name] = {"value": v, "unit": "mel-frames/s", "ms_per_step": ms, "steps": steps,
+                     "batch_per_gpu": B, "single_speaker": single,
+                     "dtype": "fp32" if dt == torch.float32 else "bf16",
+                     "T_mel_max": int(b["mel"].shape[1])}
+        del tr, model
+        torch.cuda.empty_cache()
+    return out
 
 
 def pmc_traffic():
@@ -188,7 +264,8 @@ def main():
     torch.manual_seed(0)
     model = FastSpeech2(**cfg_all["model"]["fastspeech2"], n_speakers=4, act_dtype=dt).cuda().train()
     trainer = FusedTrainer(model, lr=cfg_all["train"]["learning_rate"])
-    b = make_batch(B=args.batch, seed=rank, max_shape=args.max_shape, device="cuda")
+    b = make_batch(B=args.batch, seed=rank, max_shape=args.max_shape, device="cuda",
+                   single_speaker=args.single_speaker)
     bt, inten = as_tuple(b)
     Tm = b["mel"].shape[1]
     Tp = b["phoneme"].shape[1]
@@ -205,6 +282,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = trainer.step(bt, inten, mel_len_max=Tm)
+    host_enqueue = time.perf_counter() - t0      # host time to issue the K steps' launches
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -224,6 +302,7 @@ def main():
     ext_info = None
     if not args.no_extractor:
         ext_info = extractor_leg(cfg_all, args, trainer, b, bt, Tm, dt, world, frames_local)
+    legs = secondary_legs(cfg_all, args, rank, world)
     if rank == 0:
         c = model.cfg
         D, F, KW = c.dec_d_model, c.dec_ffn_dim, c.ffn_cnn_kernel_size_list[0]
@@ -245,7 +324,8 @@ def main():
                                    f"B={args.batch}/GPU, T_phon_max={Tp}, T_mel_max={Tm}, "
                                    f"D={c.enc_d_model} F={c.enc_ffn_dim} "
                                    f"{c.enc_num_layers}+{c.dec_num_layers} FFT layers, 80 mels"
-                                   + (", max-shape" if args.max_shape else ""),
+                                   + (", max-shape" if args.max_shape else "")
+                                   + (", single speaker" if args.single_speaker else ""),
                        "global_batch": args.batch * world, "seq_len": Tm,
                        "valid_mel_frames_per_step": frames_all, "parallelism": f"dp{world}"},
             "roofline": {"bound": "mfma", "kernel": "decoder FFN conv1 (k=9) implicit-GEMM fwd",
@@ -255,11 +335,13 @@ def main():
                          "launches": n, "avg_ms": ms,
                          "flop_per_launch": kflop},
             "step_mfma_frac": step_tflops / (MFMA_BF16_PEAK_TFLOPS * world),
+            "host_enqueue_ms_per_step": host_enqueue / args.steps * 1e3,
             "kernel_ms": {k: v[1] for k, v in ks.items()},
             "loss_total_last": loss_v[0],
         }
         if ext_info is not None:
             line["with_intensity_extractor"] = ext_info
+        line.update(legs)
         if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(cfg_all, args)
         print(json.dumps(line), flush=True)

@@ -189,6 +189,12 @@ class FS2Engine:
             if t is not None:
                 t.record_stream(main)
 
+    def grad_streams(self):
+        """streams that may hold queued parameter-gradient writes (the aux stream's are joined
+        into the main stream before the variance group completes)"""
+        main = torch.cuda.current_stream(self.dev)
+        return [main] if self._side is None else [main, self._side]
+
     def side_join(self):
         if self._side is not None:
             torch.cuda.current_stream(self.dev).wait_stream(self._side)
@@ -804,10 +810,11 @@ class FS2Engine:
         P, G = self.params, self.grads
         keep_p, keep_m = ctx["keep_p"], ctx["keep_m"]
         def notify(tag):
-            # a bucket's all-reduce must see this group's side-stream weight gradients
+            # a bucket's all-reduce must see this group's gradients on the main stream and on
+            # the weight-gradient side stream: the bucketer makes its communication stream wait
+            # on both (events), so the main stream itself never blocks on the side stream
             if self.on_grads_ready is not None:
-                self.side_join()
-                self.on_grads_ready(tag)
+                self.on_grads_ready(tag, self.grad_streams())
         d_mel = d_mel.reshape(Mm, NM).to(self.adt).contiguous()
         d_post = d_post.reshape(Mm, NM).to(self.adt).contiguous()
         d_pitch = d_pitch.reshape(Mp).to(self.adt).contiguous()

@@ -10,8 +10,12 @@ Reference: emo_rank_tts/fastspeech2/inference.py
   truncation, model.py:372-375,408) and the vocoder.
 
 Differences, each deliberate:
-* neutral intensity is zeros of shape (1, T_phon, n_emotions); the reference builds
-  (1, T_phon, 256) (:14), which the concat projection (model.py:201: 2*D + 5 inputs) rejects;
+* the reference's ``emotion == 'neutral'`` branch (:13-14) compares the STRING 'neutral' with the
+  integer ``emo_id`` its caller passes (:34, :76), so it never fires and every emotion, neutral
+  included, reads ``intensity_bank[spk][emo][lv]``.  ``get_intensity_rep`` does the same for
+  every integer id.  Only when it is given the string 'neutral' (the dead branch) does it return
+  zeros, of width n_emotions: the reference's (1, T_phon, 256) there would be rejected by the
+  concat projection (model.py:201: 2*D + 5 inputs);
 * ``synthesize`` runs many sentences as ONE padded batch on the GPU.  Its outputs equal the
   model's forward on that padded batch (what the reference's model computes for a batch, e.g.
   valid_one_epoch), not B=1 calls: padded rows are live inside the FFT blocks
@@ -28,12 +32,13 @@ import torch
 from .model import FastSpeech2
 
 
-def get_intensity_rep(speaker, emotion, intensity_lv, T_phon, intensity_bank, n_emotions=5,
-                      neutral_id=0):
-    """Per-phoneme intensity input (1, T_phon, n_emotions) for one (speaker, emotion, level).
+def get_intensity_rep(speaker, emotion, intensity_lv, T_phon, intensity_bank, n_emotions=5):
+    """Per-phoneme intensity input (1, T_phon, n_emotions) for one (speaker, emotion, level)
+    (fastspeech2/inference.py:12-21 as called at :76, i.e. with an integer emotion id).
     ``intensity_bank`` is the (n_spk, n_emo, bucket, n_emo) prototype array (or a path to the
-    .npy, loaded without pickle)."""
-    if emotion == neutral_id:
+    .npy, loaded without pickle).  ``emotion == 'neutral'`` (a string, the reference's
+    unreachable branch) gives zeros."""
+    if isinstance(emotion, str) and emotion == "neutral":
         return torch.zeros(1, T_phon, n_emotions, dtype=torch.float32)
     if isinstance(intensity_bank, str):
         intensity_bank = np.load(intensity_bank, allow_pickle=False)
@@ -81,8 +86,7 @@ def synthesize(model, phonemes, speakers, intensities, pace=1.0, batched=True):
     return [mel[i, :lens[i]] for i in range(B)], lens
 
 
-def intensity_sweep_batch(phoneme, n_speakers, emotions, levels, intensity_bank, n_emotions=5,
-                          neutral_id=0):
+def intensity_sweep_batch(phoneme, n_speakers, emotions, levels, intensity_bank, n_emotions=5):
     """The reference sweep's inputs (inference.py:55-89) for one sentence as batch lists:
     every (speaker, emotion, level) combination, in the reference's loop order."""
     T = int(phoneme.numel())
@@ -92,7 +96,6 @@ def intensity_sweep_batch(phoneme, n_speakers, emotions, levels, intensity_bank,
             for lv in levels:
                 ph.append(phoneme)
                 spk.append(s)
-                inten.append(get_intensity_rep(s, e, lv, T, intensity_bank, n_emotions,
-                                               neutral_id)[0])
+                inten.append(get_intensity_rep(s, e, lv, T, intensity_bank, n_emotions)[0])
                 keys.append((s, e, lv))
     return ph, spk, inten, keys

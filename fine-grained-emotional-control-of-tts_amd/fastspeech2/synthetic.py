@@ -9,7 +9,8 @@ durations summing exactly to each mel length (MFA alignments).  ``intensity`` is
 Draws: tokens ~ U{1..n_char-1} (0 = pad), T_phon ~ U{tp_min..tp_max}, durations ~ U{1..9}
 rescaled so that sum <= t_mel_cap, mel ~ N(-4, 2) clipped to [-11.5, 2.5] (log-mel range),
 pitch / energy ~ N(0, 1) with 15 % unvoiced (exact zero) pitch frames, speakers ~ U{0..n_spk-1},
-intensity ~ N(0, 1) (zeros if ``emotion=False``), emotion ids ~ U{0..4}; ``rank_x`` is the collate's
+intensity ~ N(0, 1) (zeros if ``emotion=False``), emotion ids ~ U{0..4} (``single_speaker``: every
+speaker id 0, BASELINE config 2's 'bea', other draws unchanged); ``rank_x`` is the collate's
 (B, n_mels + 2, T_mel) extractor input built from mel / pitch / energy.
 """
 
@@ -27,7 +28,8 @@ def _durations(g, tp, cap):
 
 
 def make_batch(B=32, tp_min=100, tp_max=200, t_mel_cap=1000, n_mels=80, n_char=95, n_spk=4,
-               seed=0, emotion=True, max_shape=False, device="cpu", fixed_tp=None):
+               seed=0, emotion=True, max_shape=False, device="cpu", fixed_tp=None,
+               single_speaker=False):
     g = torch.Generator().manual_seed(seed)
     if max_shape:
         tps = [tp_max] * B
@@ -63,6 +65,8 @@ def make_batch(B=32, tp_min=100, tp_max=200, t_mel_cap=1000, n_mels=80, n_char=9
         energy[b, :L] = torch.randn(L, generator=g)
     speakers = torch.randint(0, n_spk, (B,), generator=g)
     emotions = torch.randint(0, 5, (B,), generator=g)     # drawn last: earlier fields unchanged
+    if single_speaker:           # BASELINE config 2: EmoV-DB speaker 'bea' (id 0) only
+        speakers = torch.zeros_like(speakers)
     # rank_X as the collate builds it: cat(mel^T, pitch, energy) -> (B, n_mels + 2, T_mel)
     # (dataset.py:94,116-117), the frozen IntensityExtractor's input (train.py:27)
     rank_x = torch.cat([mel.transpose(1, 2), pitch[:, None], energy[:, None]], dim=1)

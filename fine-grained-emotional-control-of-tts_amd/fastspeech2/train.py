@@ -32,13 +32,18 @@ class GradBucketer:
     """Bucketed all-reduce of a flat gradient buffer, overlapped with the backward.
 
     ``ranges`` are the model's (tag, start, end) backward groups in completion order; they
-    are merged into contiguous buckets of at least ``bucket_bytes``.  ``ready(tag)`` is called
-    by the backward when a group's gradients are final; a bucket is reduced (async, SUM) once
-    its last group is ready.  ``finish()`` waits for every outstanding reduction.
+    are merged into contiguous buckets of at least ``bucket_bytes``.  ``ready(tag, streams)``
+    is called by the backward when a group's gradients are queued; a bucket is reduced (async,
+    SUM) once its last group is ready.  The reduction is issued from a communication stream
+    that first waits (stream-ordered events, no host sync) on every stream in ``streams`` that
+    may still be writing gradients -- the main stream and the weight-gradient side stream --
+    so neither the host nor the main stream waits for it.  ``finish()`` makes the current
+    stream wait for every outstanding reduction.
     """
 
     def __init__(self, flat, ranges, bucket_bytes=32 << 20, group=None):
         self.flat, self.group = flat, group
+        self.comm = torch.cuda.Stream(flat.device) if flat.is_cuda else None
         self.buckets = []          # [(start, end, last_tag)]
         cur = None
         for tag, s, e in ranges:
@@ -57,22 +62,32 @@ class GradBucketer:
         self.handles = []
         self.launched = set()
 
-    def ready(self, tag):
-        for i in self.by_tag.get(tag, []):
-            if i in self.launched:
-                continue
-            s, e, _ = self.buckets[i]
+    def _reduce(self, i, streams):
+        s, e, _ = self.buckets[i]
+        if self.comm is None:
             self.handles.append(dist.all_reduce(self.flat[s:e], op=dist.ReduceOp.SUM,
                                                 group=self.group, async_op=True))
-            self.launched.add(i)
-
-    def finish(self):
-        for i, (s, e, _) in enumerate(self.buckets):
-            if i not in self.launched:   # groups that never reported (defensive)
+        else:
+            for st in streams or [torch.cuda.current_stream(self.flat.device)]:
+                self.comm.wait_stream(st)
+            with torch.cuda.stream(self.comm):
                 self.handles.append(dist.all_reduce(self.flat[s:e], op=dist.ReduceOp.SUM,
                                                     group=self.group, async_op=True))
+        self.launched.add(i)
+
+    def ready(self, tag, streams=None):
+        for i in self.by_tag.get(tag, []):
+            if i not in self.launched:
+                self._reduce(i, streams)
+
+    def finish(self, streams=None):
+        for i in range(len(self.buckets)):
+            if i not in self.launched:   # groups that never reported (defensive)
+                self._reduce(i, streams)
         for h in self.handles:
             h.wait()
+        if self.comm is not None:
+            torch.cuda.current_stream(self.flat.device).wait_stream(self.comm)
         self.handles, self.launched = [], set()
 
 
@@ -92,13 +107,16 @@ class FusedTrainer:
             self.eng.on_grads_ready = self.bucketer.ready
         self.seed = 0
 
-    def step(self, batch, intensity, mel_len_max=None):
+    def forward_backward(self, batch, intensity, mel_len_max=None, seed=None):
+        """Forward + fused loss + backward of this rank's shard; the gradients are left in the
+        model's flat buffer (with DP on, their bucket all-reduces are queued as the backward
+        produces them).  Returns the loss vector."""
         (phoneme, spk_ids, phon_len, mel_tgt, pitch_tgt, energy_tgt, duration_tgt, mel_len) = batch[:8]
         m = self.model
-        self.seed += 1
         m._gflat.zero_()
         out, ctx = self.eng.forward(phoneme, spk_ids, duration_tgt, pitch_tgt, energy_tgt,
-                                    intensity=intensity, training=True, seed=self.seed,
+                                    intensity=intensity, training=True,
+                                    seed=self.seed if seed is None else seed,
                                     mel_len_max=mel_len_max if mel_len_max is not None
                                     else mel_tgt.shape[1])
         mel, post, pd, pp, avg_p, pe, avg_e, _ = out
@@ -106,7 +124,16 @@ class FusedTrainer:
                                  duration_tgt, avg_p.view(pd.shape), avg_e.view(pd.shape), mel_len,
                                  phon_len, self.weights)
         self.eng.backward(ctx, *grads)
+        return loss
+
+    def apply(self):
+        """Wait for the gradient all-reduce (stream-ordered) and run AdamW with the 1/N mean."""
         if self.bucketer is not None:
-            self.bucketer.finish()
+            self.bucketer.finish(self.eng.grad_streams())
         self.opt.step(grad_scale=1.0 / self.world)
+
+    def step(self, batch, intensity, mel_len_max=None):
+        self.seed += 1
+        loss = self.forward_backward(batch, intensity, mel_len_max)
+        self.apply()
         return loss

@@ -400,13 +400,14 @@ def test_conv_dgrad_shift_plus_fold(cuda, dt, code, tol, KW, T, split):
     assert rel(dX, ref) < tol
 
 
-@pytest.mark.parametrize("Bn,T", [(32, 640), (1, 640), (32, 200)])
+@pytest.mark.parametrize("Bn,T", [(32, 640), (1, 640), (32, 200), (32, 977)])
 def test_gemm_big_tile_paths_bf16(cuda, Bn, T):
     """BASELINE-sized GEMMs that take the 256x128 LDS-DMA kernel (gemm_big_kernel): implicit
     reflect conv k=9 forward with bias+ReLU, zero-padded shift-conv data gradient + fold, and
     the weight gradient into the [O][KW][C] layout -- split-K with atomics at Bn=32, the
     single-split vector accumulate epilogue at Bn=1; T=200 (encoder) takes the split-slice
-    data gradient.  bf16 inputs, fp32 reference on the same
+    data gradient; T=977 is the bench's decoder shape (M = 31264: a partial last 256-row tile,
+    utterance boundaries inside tiles).  bf16 inputs, fp32 reference on the same
     bf16 values, rel 2e-2."""
     from fastspeech2 import ops
     torch.manual_seed(Bn)
@@ -485,17 +486,25 @@ def _keep_np(seed, salt, idx, p):
     return bits >= np.uint64(int(p * 65536 + 0.5))
 
 
-@pytest.mark.parametrize("dh,T,p_drop", [(192, 150, 0.0), (192, 150, 0.1), (64, 70, 0.1),
-                                          (256, 130, 0.0)])
-def test_fused_attention_vs_torch(cuda, dh, T, p_drop):
+@pytest.mark.parametrize("dh,T,p_drop,B", [(192, 150, 0.0, 3), (192, 150, 0.1, 3), (64, 70, 0.1, 3),
+                                            (256, 130, 0.0, 3), (192, 977, 0.0, 32),
+                                            (192, 200, 0.0, 32)])
+def test_fused_attention_vs_torch(cuda, dh, T, p_drop, B):
     """fs2_attn_fwd/bwd (bf16) against torch fp32 on the same bf16 Q/K/V: the head-major mask
     tiling rule, ragged lengths, and (p > 0) the counter-hash dropout masks restated in numpy.
+    B=32 with T=977 / 200 are the bench's decoder / encoder shapes: 128-row (W8 = 8) blocks for
+    the decoder, 64-row blocks for the encoder, descending ragged lengths as the collate sorts.
     Tolerance rel 2e-2 (O) / 3e-2 (dQ, dK, dV): bf16 operands and probabilities."""
     from fastspeech2 import ops
     torch.manual_seed(dh + T)
-    B, H = 3, 2
+    H = 2
     D = H * dh
-    lens = [T, T - 37, T - 90]
+    if B == 3:
+        lens = [T, T - 37, T - 90]
+    else:
+        g = torch.Generator().manual_seed(T)
+        lens = sorted([T] + torch.randint(T // 2, T + 1, (B - 1,), generator=g).tolist(),
+                      reverse=True)
     qkv = (torch.randn(B * T, 3 * D, device=cuda) * 0.5).to(torch.bfloat16)
     kp = torch.zeros(B, T, dtype=torch.uint8, device=cuda)
     for b, L in enumerate(lens):

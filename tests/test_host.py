@@ -130,12 +130,17 @@ def test_flop_count_matches_survey(cfg_all):
 
 
 def test_get_intensity_rep_prototype_lookup():
-    """fastspeech2/inference.py:12-21: prototype bank lookup expanded over the phonemes;
-    neutral -> zeros with n_emotions (=5) channels (the reference's 256 is the App. fix)."""
+    """fastspeech2/inference.py:12-21 as called at :76 (integer emo_id): the prototype bank
+    lookup expanded over the phonemes for EVERY emotion id, neutral (id 0) included -- the
+    reference's `emotion == 'neutral'` string test never matches an int.  Only the string
+    'neutral' (that dead branch) gives zeros, with n_emotions (=5) channels instead of 256."""
     import numpy as np
     from fastspeech2.inference import get_intensity_rep
     bank = np.random.default_rng(0).standard_normal((4, 5, 3, 5)).astype(np.float32)
-    z = get_intensity_rep(1, 0, 2, 7, bank)
+    n = get_intensity_rep(1, 0, 2, 7, bank)
+    assert n.shape == (1, 7, 5)
+    assert torch.equal(n[0, 3], torch.from_numpy(bank[1, 0, 2]))
+    z = get_intensity_rep(1, "neutral", 2, 7, bank)
     assert z.shape == (1, 7, 5) and torch.all(z == 0)
     r = get_intensity_rep(2, 3, 1, 7, bank)
     assert r.shape == (1, 7, 5)

@@ -75,6 +75,87 @@ def kernel(d, name_sub, grid, min_us):
           f"avg {sum(durs) / len(durs):.1f} us, min {min(durs):.1f}, max {max(durs):.1f}")
 
 
+def gaps(d, marker="adamw_vec_kernel", last=10, out=None):
+    """GPU-idle time per train step: steps are delimited by the end of the one AdamW launch per
+    step (``marker``); within a step, idle = wall time - |union of every kernel's busy interval
+    over all streams|.  Reported for the ``last`` steps of the trace (the timed region)."""
+    ev = []
+    for f in _find(d, "kernel_trace.csv"):
+        for r in csv.DictReader(open(f)):
+            ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"],
+                       r.get("Queue_Id", r.get("Stream_Id", ""))))
+    ev.sort()
+    ends = sorted(e for s, e, n, _ in ev if marker in n)
+    if len(ends) < 2:
+        raise SystemExit(f"fewer than 2 {marker} dispatches")
+    rows = []
+    for a, b in list(zip(ends[:-1], ends[1:]))[-last:]:
+        iv = sorted((max(s, a), min(e, b)) for s, e, _, _ in ev if e > a and s < b)
+        busy, cur_s, cur_e, n = 0, None, None, 0
+        for s, e in iv:
+            n += 1
+            if cur_e is None or s > cur_e:
+                if cur_e is not None:
+                    busy += cur_e - cur_s
+                cur_s, cur_e = s, e
+            else:
+                cur_e = max(cur_e, e)
+        if cur_e is not None:
+            busy += cur_e - cur_s
+        rows.append(((b - a) / 1e6, busy / 1e6, n))
+    wall = sorted(r[0] for r in rows)[len(rows) // 2]
+    idle = sorted(r[0] - r[1] for r in rows)[len(rows) // 2]
+    res = {"steps": len(rows), "median_step_ms": wall, "median_gpu_idle_ms": idle,
+           "median_busy_ms": sorted(r[1] for r in rows)[len(rows) // 2],
+           "launches_per_step": rows[-1][2],
+           "per_step": [{"wall_ms": w, "busy_ms": bz, "launches": n} for w, bz, n in rows]}
+    if out:
+        json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps({k: v for k, v in res.items() if k != "per_step"}))
+
+
+def pmc(out, subs, *dirs):
+    """Per (kernel, grid) averages of every counter collected in the --pmc pass directories
+    ``dirs`` (one counter set per pass), for kernels whose name contains one of the
+    comma-separated substrings ``subs``.  Counter values are summed over a dispatch's rows
+    (per-XCD / per-SE instances), then averaged over dispatches; avg_us from the same rows."""
+    import collections
+    acc = collections.defaultdict(lambda: collections.defaultdict(dict))
+    dur = collections.defaultdict(dict)
+    want = [s for s in subs.split(",") if s]
+    for d in dirs:
+        for f in _find(d, "counter_collection.csv"):
+            for r in csv.DictReader(open(f)):
+                name = r["Kernel_Name"]
+                if want and not any(w in name for w in want):
+                    continue
+                key = (name[:90], int(r["Grid_Size"]))
+                disp = (f, r["Dispatch_Id"])
+                c = acc[key][r["Counter_Name"]]
+                c[disp] = c.get(disp, 0.0) + float(r["Counter_Value"])
+                dur[key][disp] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+    res = []
+    for key, cs in acc.items():
+        row = {"kernel": key[0], "grid": key[1],
+               "avg_us": sum(dur[key].values()) / len(dur[key]), "dispatches": len(dur[key])}
+        for cn, v in cs.items():
+            row[cn] = sum(v.values()) / len(v)
+        if "FETCH_SIZE" in row:
+            row["hbm_read_bytes"] = 2.0 * 1024.0 * row["FETCH_SIZE"]
+        if "WRITE_SIZE" in row:
+            row["hbm_write_bytes"] = 1024.0 * row["WRITE_SIZE"]
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in row and "GRBM_GUI_ACTIVE" in row:
+            # MFMA busy cycles summed over every SIMD of the chip (4 per CU x 256 CUs) vs the
+            # kernel's GPU-active cycles (GRBM_GUI_ACTIVE is summed over the 8 XCDs)
+            row["mfma_busy_frac"] = row["SQ_VALU_MFMA_BUSY_CYCLES"] / (
+                1024.0 * row["GRBM_GUI_ACTIVE"] / 8.0)
+        res.append(row)
+    res.sort(key=lambda r: -r["avg_us"] * r["dispatches"])
+    json.dump(res, open(out, "w"), indent=1)
+    for r in res:
+        print(json.dumps({k: (round(v, 4) if isinstance(v, float) else v) for k, v in r.items()}))
+
+
 def _per_dispatch(d, counter, name_sub, grid, min_us):
     vals = {}
     for f in _find(d, "counter_collection.csv"):
@@ -114,6 +195,12 @@ if __name__ == "__main__":
         shapes(sys.argv[2], int(sys.argv[3]), int(sys.argv[4]) if len(sys.argv) > 4 else 40)
     elif sys.argv[1] == "kernel":
         kernel(sys.argv[2], sys.argv[3], int(sys.argv[4]), float(sys.argv[5]))
+    elif sys.argv[1] == "pmc":
+        pmc(sys.argv[2], sys.argv[3], *sys.argv[4:])
+    elif sys.argv[1] == "gaps":
+        gaps(sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else "adamw_vec_kernel",
+             int(sys.argv[4]) if len(sys.argv) > 4 else 10,
+             sys.argv[5] if len(sys.argv) > 5 else None)
     elif sys.argv[1] == "traffic":
         traffic(sys.argv[2], sys.argv[3], sys.argv[4], int(sys.argv[5]), float(sys.argv[6]),
                 sys.argv[7] if len(sys.argv) > 7 else None)
