@@ -39,6 +39,8 @@ def parse():
     ap.add_argument("--single-speaker", action="store_true",
                     help="every utterance speaker 0 (BASELINE config 2 with --batch 16)")
     ap.add_argument("--no-fp32-leg", action="store_true")
+    ap.add_argument("--no-graph", action="store_true",
+                    help="eager launches even if FS2_GRAPH=1 selects the captured HIP graph step")
     ap.add_argument("--no-config2-leg", action="store_true")
     ap.add_argument("--scaled", action="store_true",
                     help="BASELINE config 4: scaled FastSpeech2, hidden 512, FFN 2048, 6+6 layers")
@@ -270,6 +272,8 @@ def main():
     Tm = b["mel"].shape[1]
     Tp = b["phoneme"].shape[1]
     frames_local = int(b["mel_len"].sum())
+    if args.detail or args.no_graph:
+        trainer.use_graph = False
     for _ in range(args.warmup):
         trainer.step(bt, inten, mel_len_max=Tm)
     torch.cuda.synchronize()
@@ -289,6 +293,20 @@ def main():
     elapsed = time.perf_counter() - t0
     trainer.eng.timer = None
     ks = timer.summary()
+    graphed = trainer.use_graph
+    if graphed:
+        # a graph replay runs the captured launches without the host-side HIP-event brackets:
+        # time the roofline kernel in an eager pass of the same step (same kernels, arguments
+        # and inputs), on the stream the kernel is launched on
+        trainer.use_graph = False
+        timer = KernelTimer()
+        trainer.eng.timer = timer
+        for _ in range(args.steps):
+            trainer.step(bt, inten, mel_len_max=Tm)
+        torch.cuda.synchronize()
+        trainer.eng.timer = None
+        ks = timer.summary()
+        trainer.use_graph = True
     if args.detail and rank == 0:
         detail_table(ks, trainer.eng, args.batch, args.steps, elapsed)
     tmax = torch.tensor([elapsed], device="cuda")
@@ -333,7 +351,12 @@ def main():
                          "frac": (achieved / MFMA_BF16_PEAK_TFLOPS) if achieved else None,
                          "traffic": traffic, "traffic_source": traffic_src,
                          "launches": n, "avg_ms": ms,
-                         "flop_per_launch": kflop},
+                         "flop_per_launch": kflop,
+                         "timing": ("HIP events on the engine stream around each launch, in an "
+                                    "eager pass of the same steps after the graph-replayed "
+                                    "timed region" if graphed else
+                                    "HIP events on the engine stream over the timed region")},
+            "hip_graph": graphed,
             "step_mfma_frac": step_tflops / (MFMA_BF16_PEAK_TFLOPS * world),
             "host_enqueue_ms_per_step": host_enqueue / args.steps * 1e3,
             "kernel_ms": {k: v[1] for k, v in ks.items()},

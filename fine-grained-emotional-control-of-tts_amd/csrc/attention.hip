@@ -128,3 +128,6 @@ extern "C" int fs2_softmax_bwd(const float* dPd, const void* P, int B, int H, in
   FS2_CHECK_LAUNCH();
   return 0;
 }
+
+// this translation unit's dropout seed base (fs2_common.h)
+FS2_SEED_SETTER(fs2_seed_base_attention)

@@ -818,3 +818,6 @@ extern "C" int fs2_attn_bwd_stage(const void* qkv, int64_t ldq, const uint8_t* k
 }
 
 extern "C" int64_t fs2_attn_workspace_floats(int B, int H, int T) { return (int64_t)B * H * T; }
+
+// this translation unit's dropout seed base (fs2_common.h)
+FS2_SEED_SETTER(fs2_seed_base_flash)

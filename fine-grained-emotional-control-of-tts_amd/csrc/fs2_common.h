@@ -86,8 +86,26 @@ __device__ __forceinline__ uint32_t fs2_mix32(uint32_t h) {
   h ^= h >> 16; h *= 0x85ebca6bu; h ^= h >> 13; h *= 0xc2b2ae35u; h ^= h >> 16;
   return h;
 }
+//
+// The step's seed is the launch's ``seed`` argument PLUS a device-resident base (one cell per
+// translation unit, written by fs2_set_dropout_seed).  Eager steps pass their seed as the
+// argument with base 0; a captured HIP graph replays launches with their captured arguments,
+// so the graph is captured with seed 0 and each replay first sets the base to the step's seed.
+// Both give identical masks for the same step seed.
+namespace {
+__device__ uint32_t g_fs2_seed_base = 0u;
+__global__ void fs2_seed_base_kernel(uint32_t v) { g_fs2_seed_base = v; }
+}  // namespace
+#define FS2_SEED_SETTER(NAME)                                            \
+  int NAME(uint32_t v, void* stream) {                                    \
+    hipLaunchKernelGGL(fs2_seed_base_kernel, dim3(1), dim3(1), 0,          \
+                       (hipStream_t)stream, v);                           \
+    return (int)hipGetLastError();                                        \
+  }
+
 __device__ __forceinline__ bool fs2_keep(uint32_t seed, uint32_t salt, uint64_t idx, float p) {
   if (p <= 0.f) return true;
+  seed += g_fs2_seed_base;
   uint32_t h = fs2_mix32((uint32_t)idx ^ fs2_mix32(seed ^ (salt * 0x9E3779B9u)));
   h = fs2_mix32(h ^ (uint32_t)(idx >> 32) ^ 0x68bc21ebu);
   // uniform in [0,1) with 24 bits
@@ -100,6 +118,7 @@ __device__ __forceinline__ bool fs2_keep(uint32_t seed, uint32_t salt, uint64_t 
 // per element compared with thr16 = round(p * 65536).  Element indices are row-major over
 // rows padded to an even length, so a lane's consecutive keys share one hash.
 __device__ __forceinline__ uint32_t fs2_drop_key(uint32_t seed, uint32_t salt) {
+  seed += g_fs2_seed_base;
   return fs2_mix32(seed ^ (salt * 0x9E3779B9u)) | 1u;
 }
 __device__ __forceinline__ uint32_t fs2_hash_pair(uint32_t key, uint64_t pair) {

@@ -772,3 +772,6 @@ extern "C" int fs2_conv_fold(const float* Xpad, int nsplit, int64_t split_stride
   FS2_CHECK_LAUNCH();
   return 0;
 }
+
+// this translation unit's dropout seed base (fs2_common.h)
+FS2_SEED_SETTER(fs2_seed_base_norm)

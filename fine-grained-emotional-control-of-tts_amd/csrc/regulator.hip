@@ -619,4 +619,14 @@ extern "C" int fs2_cast(const void* src, int src_dtype, void* dst, int dst_dtype
   return 0;
 }
 
+int fs2_seed_base_norm(uint32_t v, void* stream);
+int fs2_seed_base_attention(uint32_t v, void* stream);
+int fs2_seed_base_flash(uint32_t v, void* stream);
+
+extern "C" int fs2_set_dropout_seed(uint32_t seed_base, void* stream) {
+  if (int rc = fs2_seed_base_norm(seed_base, stream)) return rc;
+  if (int rc = fs2_seed_base_attention(seed_base, stream)) return rc;
+  return fs2_seed_base_flash(seed_base, stream);
+}
+
 extern "C" const char* fs2_version(void) { return "fs2_hip 0.1 gfx950"; }

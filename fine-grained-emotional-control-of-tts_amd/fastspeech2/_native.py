@@ -133,6 +133,7 @@ SIGNATURES = {
     "fs2_fill": (I, [P, I64, Fl, I, P]),
     "fs2_add": (I, [P, P, I64, Fl, I, P]),
     "fs2_cast": (I, [P, I, P, I, I64, P]),
+    "fs2_set_dropout_seed": (I, [U32, P]),
     "fs2_version": (ctypes.c_char_p, []),
 }
 

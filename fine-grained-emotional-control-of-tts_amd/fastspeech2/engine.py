@@ -233,6 +233,8 @@ class FS2Engine:
         """fp32 master weights -> K-major GEMM images in the activation dtype (fwd + dgrad), all
         weights in one fs2_weight_prep_batched launch per parameter update."""
         ver = (self.m._param_version, self.m._flat._version)
+        if torch.cuda.is_current_stream_capturing():
+            force = True     # a captured step must re-prepare on every replay
         if not force and self._prepared_version == ver:
             return
         if self._wtable is None:

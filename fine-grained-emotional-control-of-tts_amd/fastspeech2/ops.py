@@ -314,3 +314,8 @@ def add(X, Y, n, alpha=1.0, *, dt):
 
 def cast(src, src_dt, dst, dst_dt, n):
     _chk(N.lib().fs2_cast(_p(src), src_dt, _p(dst), dst_dt, n, _s()), "fs2_cast")
+
+
+def set_dropout_seed(seed_base):
+    """Device-resident dropout seed base added to every launch's seed (graph replays)."""
+    _chk(N.lib().fs2_set_dropout_seed(int(seed_base) & 0xffffffff, _s()), "fs2_set_dropout_seed")

@@ -9,9 +9,12 @@
   AdamW kernel.  One process per GPU, ``torch.distributed`` with the nccl (= RCCL) backend.
 """
 
+import os
+
 import torch
 import torch.distributed as dist
 
+from . import ops
 from .loss import fused_loss
 from .optim import FusedAdamW
 
@@ -91,11 +94,59 @@ class GradBucketer:
         self.handles, self.launched = [], set()
 
 
+# opt-in: measured slower on ROCm 7 / MI355X (bench A/B, profiles/r02_graph_ab.txt: B=32 21.88 ms
+# eager vs 22.16 ms graph, B=16 14.02 vs 14.46 ms; GPU-idle time per step 0.63 ms eager vs
+# 1.50 ms graph): the replayed multi-stream graph leaves more gaps between kernels than the
+# eager launches, whose host issue time (8-12 ms/step) is already below the GPU time
+_GRAPH = os.environ.get("FS2_GRAPH", "0") not in ("", "0")
+
+
+class _StepGraph:
+    """One captured forward + loss + backward for a fixed batch shape.
+
+    The graph owns static copies of the batch tensors (refreshed by a device copy per step, so
+    a caller may hand in a new batch of the same shape every step), the loss vector it writes,
+    and every intermediate (torch's graph-private memory pool).  Launch arguments are frozen at
+    capture, so the dropout seed is captured as 0 and each replay first writes the step's seed
+    into the kernels' device-resident seed base (``ops.set_dropout_seed``); AdamW, whose bias
+    corrections change every step, runs eagerly after the replay."""
+
+    def __init__(self, trainer, batch, intensity, mel_len_max):
+        self.static = [t.clone() for t in batch[:8]] + [intensity.clone()]
+        self.mel_len_max = mel_len_max
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            # one eager pass on the capture stream: workspaces and lazily built tables exist
+            # before capture, as torch.cuda.graphs recommends
+            trainer.forward_backward(self.static[:8], self.static[8], mel_len_max, seed=0)
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph, stream=s):
+            self.loss = trainer.forward_backward(self.static[:8], self.static[8], mel_len_max,
+                                                 seed=0)
+        torch.cuda.synchronize()
+
+    def replay(self, batch, intensity, seed):
+        for dst, src in zip(self.static, list(batch[:8]) + [intensity]):
+            if dst.data_ptr() != src.data_ptr():
+                dst.copy_(src, non_blocking=True)
+        ops.set_dropout_seed(seed)
+        self.graph.replay()
+        ops.set_dropout_seed(0)
+        return self.loss
+
+
 class FusedTrainer:
-    """One optimiser step of the FastSpeech2 train path on this rank's shard of the batch."""
+    """One optimiser step of the FastSpeech2 train path on this rank's shard of the batch.
+
+    ``graph=True`` (or FS2_GRAPH=1 on one rank) replays forward + loss + backward as a captured
+    HIP graph per batch shape: one host launch instead of ~500 ctypes calls per step.  Off by
+    default: measured slower than the eager launches on this stack (see ``_GRAPH``)."""
 
     def __init__(self, model, loss_weights=(1.0,) * 6, lr=1e-4, betas=(0.9, 0.999), eps=1e-8,
-                 weight_decay=1e-2, bucket_bytes=32 << 20):
+                 weight_decay=1e-2, bucket_bytes=32 << 20, graph=None):
         self.model = model
         self.eng = model.engine()
         self.opt = FusedAdamW(model, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
@@ -106,6 +157,18 @@ class FusedTrainer:
             self.bucketer = GradBucketer(model._gflat, model.group_ranges(), bucket_bytes)
             self.eng.on_grads_ready = self.bucketer.ready
         self.seed = 0
+        # DP steps stay eager: their bucketed all-reduces are issued from the backward hooks
+        self.use_graph = (self.world == 1 and _GRAPH) if graph is None else bool(graph)
+        self._graphs = {}
+
+    def _graph_for(self, batch, intensity, mel_len_max):
+        key = tuple(tuple(t.shape) for t in batch[:8]) + (tuple(intensity.shape), mel_len_max)
+        g = self._graphs.get(key)
+        if g is None:
+            if len(self._graphs) >= 4:          # shape buckets kept resident
+                self._graphs.pop(next(iter(self._graphs)))
+            g = self._graphs[key] = _StepGraph(self, batch, intensity, mel_len_max)
+        return g
 
     def forward_backward(self, batch, intensity, mel_len_max=None, seed=None):
         """Forward + fused loss + backward of this rank's shard; the gradients are left in the
@@ -134,6 +197,10 @@ class FusedTrainer:
 
     def step(self, batch, intensity, mel_len_max=None):
         self.seed += 1
-        loss = self.forward_backward(batch, intensity, mel_len_max)
+        if self.use_graph:
+            mlm = mel_len_max if mel_len_max is not None else batch[3].shape[1]
+            loss = self._graph_for(batch, intensity, mlm).replay(batch, intensity, self.seed)
+        else:
+            loss = self.forward_backward(batch, intensity, mel_len_max)
         self.apply()
         return loss

@@ -339,6 +339,10 @@ int fs2_fill(void* X, int64_t n, float value, int dtype, void* stream);
 /* X[i] += alpha * Y[i] over n elements of dtype                                           */
 int fs2_add(void* X, const void* Y, int64_t n, float alpha, int dtype, void* stream);
 int fs2_cast(const void* src, int src_dtype, void* dst, int dst_dtype, int64_t n, void* stream);
+/* Dropout seed base (device-resident, added to every launch's seed argument): HIP-graph
+ * replays of a step captured with seed 0 set it to the step's seed first; eager steps leave
+ * it 0.  Stream-ordered. */
+int fs2_set_dropout_seed(uint32_t seed_base, void* stream);
 const char* fs2_version(void);
 
 #ifdef __cplusplus

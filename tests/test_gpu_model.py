@@ -282,3 +282,34 @@ def test_bf16_stream_overlap_matches_single_stream(cuda, cfg_all):
         assert rel(a, r) <= 2e-2, n
         cos = torch.nn.functional.cosine_similarity(a.flatten(), r.flatten(), dim=0).item()
         assert cos >= 0.999, (n, cos)
+
+
+def test_graph_replayed_step_equals_eager_step(cuda, cfg_all):
+    """FusedTrainer's captured HIP-graph step (one capture per batch shape, dropout seed in the
+    kernels' device-resident seed base) against the eager step on the same initial weights and
+    batch, dropout on: the first step's loss is bit-identical (same kernels, same masks), later
+    steps within 1e-4 (weight-gradient split-K atomics perturb the weights at fp32 rounding),
+    and the weights after three steps agree except where a gradient is rounding noise."""
+    from fastspeech2.model import FastSpeech2
+    from fastspeech2.train import FusedTrainer
+    from fastspeech2.synthetic import make_batch, as_tuple
+    kw = dict(cfg_all["model"]["fastspeech2"], enc_num_layers=2, dec_num_layers=2)
+    b = make_batch(B=8, tp_min=60, tp_max=90, seed=21, device="cuda")
+    bt, inten = as_tuple(b)
+    res = {}
+    for graph in (False, True):
+        torch.manual_seed(0)
+        m = FastSpeech2(**kw, n_speakers=4, act_dtype=torch.bfloat16).cuda().train()
+        tr = FusedTrainer(m, lr=1e-4, graph=graph)
+        losses = [tr.step(bt, inten).clone() for _ in range(3)]
+        torch.cuda.synchronize()
+        res[graph] = (torch.stack(losses).cpu(), m._flat.cpu())
+        if graph:
+            assert len(tr._graphs) == 1
+    (le, pe), (lg, pg) = res[False], res[True]
+    assert torch.equal(le[0], lg[0])
+    assert torch.allclose(le, lg, rtol=1e-4, atol=0)
+    assert not torch.equal(le[1], le[2])            # masks / weights do change per step
+    dp = (pe - pg).abs()
+    assert dp.max().item() <= 3 * 2.1e-4
+    assert (dp > 1e-6).float().mean().item() <= 1e-3
