@@ -1,0 +1,94 @@
+"""Microbenchmark of the FFT-block GEMM call sites exactly as the engine issues them
+(FS2Engine._fwd / _dgrad / _wgrad on a bf16 default-size model), at the bench's decoder
+(B=32, T=977) and encoder (B=32, T=200) shapes.  Weight gradients run on the calling stream
+(FS2_NO_SIDE_STREAM=1 is set here).  Prints one line per call site: us per call, TFLOP/s.
+
+    python tools/gemm_bench.py [filter-substring ...]
+"""
+import os
+import sys
+
+os.environ.setdefault("FS2_NO_SIDE_STREAM", "1")
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "fine-grained-emotional-control-of-tts_amd"))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+
+
+def main():
+    from fastspeech2 import load_config
+    from fastspeech2.model import FastSpeech2
+    flt = sys.argv[1:]
+    cfg = load_config()["model"]["fastspeech2"]
+    torch.manual_seed(0)
+    m = FastSpeech2(**cfg, n_speakers=4, act_dtype=torch.bfloat16).cuda()
+    eng = m.engine()
+    eng.prepare_weights()
+    D, F = cfg["enc_d_model"], cfg["enc_ffn_dim"]
+    bf = torch.bfloat16
+    rows = []
+    for stack, T in (("decoder", 977), ("encoder", 200)):
+        B = 32
+        M = B * T
+        p = f"{stack}.layers.0."
+        r = lambda n: (torch.randn(M, n, device="cuda") * 0.5).to(bf)
+        X, X1, Att, dAo, dY = r(D), r(D), r(D), r(D), r(D)
+        Hc = torch.relu(r(F))
+        QKV, dQKV = r(3 * D), r(3 * D)
+        dHc, res = r(F), r(D)
+        P = eng.params
+        cases = [
+            ("fwd in_proj", 6 * M * D * D, lambda: eng._fwd(X, D, M, T, p + "self_att.att.in_proj_weight", QKV, 3 * D, bias=P[p + "self_att.att.in_proj_bias"])),
+            ("fwd out_proj", 2 * M * D * D, lambda: eng._fwd(Att, D, M, T, p + "self_att.att.out_proj.weight", dAo, D, bias=P[p + "self_att.att.out_proj.bias"])),
+            ("fwd conv1", 2 * M * F * 9 * D, lambda: eng._fwd(X1, D, M, T, p + "pos_ffn.0.conv.weight", Hc, F, bias=P[p + "pos_ffn.0.conv.bias"], relu=1)),
+            ("fwd conv2", 2 * M * F * D, lambda: eng._fwd(Hc, F, M, T, p + "pos_ffn.2.conv.weight", dY, D, bias=P[p + "pos_ffn.2.conv.bias"])),
+            ("dgrad conv2", 2 * M * F * D, lambda: eng._dgrad(dY, D, M, T, p + "pos_ffn.2.conv.weight", dHc, F, gate=Hc, ldg=F)),
+            ("dgrad conv1", 2 * M * F * 9 * D, lambda: eng._dgrad(dHc, F, M, T, p + "pos_ffn.0.conv.weight", X1, D, residual=res, ldr=D)),
+            ("dgrad out_proj", 2 * M * D * D, lambda: eng._dgrad(dAo, D, M, T, p + "self_att.att.out_proj.weight", Att, D)),
+            ("dgrad in_proj", 6 * M * D * D, lambda: eng._dgrad(dQKV, 3 * D, M, T, p + "self_att.att.in_proj_weight", X, D, residual=res, ldr=D)),
+            ("wgrad conv2", 2 * M * F * D, lambda: eng._wgrad(dY, D, Hc, F, M, T, p + "pos_ffn.2.conv.weight")),
+            ("wgrad conv1", 2 * M * F * 9 * D, lambda: eng._wgrad(dHc, F, X1, D, M, T, p + "pos_ffn.0.conv.weight")),
+            ("wgrad out_proj", 2 * M * D * D, lambda: eng._wgrad(dAo, D, Att, D, M, T, p + "self_att.att.out_proj.weight")),
+            ("wgrad in_proj", 6 * M * D * D, lambda: eng._wgrad(dQKV, 3 * D, X, D, M, T, p + "self_att.att.in_proj_weight")),
+        ]
+        if os.environ.get("FS2_GB_BLAS"):
+            # hipBLASLt (torch.matmul, bf16) on the same shapes as plain GEMMs: a ceiling reference
+            W3 = (torch.randn(3 * D, D, device="cuda") * 0.05).to(bf)
+            W1 = (torch.randn(D, D, device="cuda") * 0.05).to(bf)
+            Wf = (torch.randn(F, D, device="cuda") * 0.05).to(bf)
+            Wc = (torch.randn(F, 9 * D, device="cuda") * 0.05).to(bf)
+            Xc = r(9 * D)
+            cases += [
+                ("blas M.384x384.1152", 6 * M * D * D, lambda: torch.matmul(X, W3.t())),
+                ("blas M.384x384.384", 2 * M * D * D, lambda: torch.matmul(X, W1.t())),
+                ("blas M.1536x1536.384", 2 * M * F * D, lambda: torch.matmul(Hc, Wf)),
+                ("blas M.384x384.1536", 2 * M * F * D, lambda: torch.matmul(X, Wf.t())),
+                ("blas M.3456x3456.1536", 2 * M * F * 9 * D, lambda: torch.matmul(Xc, Wc.t())),
+                ("blas wgrad 384xM.Mx1536", 2 * M * F * D, lambda: torch.matmul(dY.t(), Hc)),
+                ("blas wgrad 1152xM.Mx384", 6 * M * D * D, lambda: torch.matmul(dQKV.t(), X)),
+            ]
+        for name, fl, fn in cases:
+            tag = f"{stack} {name}"
+            if flt and not any(f in tag for f in flt):
+                continue
+            for _ in range(3):
+                fn()
+            torch.cuda.synchronize()
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            n = 20
+            a.record()
+            for _ in range(n):
+                fn()
+            b.record()
+            torch.cuda.synchronize()
+            us = a.elapsed_time(b) / n * 1e3
+            rows.append((tag, us, fl / us / 1e6))
+    tot = 0.0
+    for tag, us, tf in rows:
+        tot += us
+        print(f"{tag:28s} {us:8.1f} us {tf:8.1f} TF/s", flush=True)
+    print(f"{'sum':28s} {tot:8.1f} us")
+
+
+if __name__ == "__main__":
+    main()
