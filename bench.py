@@ -330,6 +330,7 @@ def main():
         traffic, traffic_src = pmc_traffic() if not args.scaled else (None, None)
         step_ms = elapsed / args.steps * 1e3
         step_tflops = train_flops(c, args.batch, Tp, Tm) * world / (step_ms * 1e-3) / 1e12
+        fpf = train_flops(c, 1, 200, 1000) / 1000.0
         line = {
             "metric": "train mel-frames/sec at B=32, 80-bin mel; 1/2/4/8 MI355X",
             "value": frames_all * args.steps / elapsed,
@@ -357,6 +358,16 @@ def main():
                                     "timed region" if graphed else
                                     "HIP events on the engine stream over the timed region")},
             "hip_graph": graphed,
+            # the step-level roofline on VALID frames -- frames/s x the train FLOPs
+            # of one mel frame at T_phon=200, T_mel=1000 (338.8 MFLOP at default dims) / peak
+            "roofline_step": {"bound": "mfma",
+                              "achieved": frames_all * args.steps / elapsed * fpf / 1e12 / world,
+                              "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s per GPU",
+                              "frac": frames_all * args.steps / elapsed * fpf / 1e12 / world
+                              / MFMA_BF16_PEAK_TFLOPS,
+                              "flop_per_valid_frame": fpf,
+                              "definition": "SURVEY 8(d): frames/s x train FLOP per mel frame "
+                                            "(fwd + 2x bwd at T_phon=200, T_mel=1000) / peak"},
             "step_mfma_frac": step_tflops / (MFMA_BF16_PEAK_TFLOPS * world),
             "host_enqueue_ms_per_step": host_enqueue / args.steps * 1e3,
             "kernel_ms": {k: v[1] for k, v in ks.items()},

@@ -1028,7 +1028,7 @@ __global__ void __launch_bounds__(BNT) gemm_big_kernel(GemmP p) {
   char* Cb = p.C + (zb * p.sC1 + zh * p.sC2) * (p.c_fp32 ? 4 : 2);
   if (p.split_stride > 0 && p.split_k > 1) Cb += (long)blockIdx.z * p.split_stride * 4;
   const char* Rb = p.residual ? p.residual + (zb * p.sR1 + zh * p.sR2) * 2 : nullptr;
-  if (p.vec_ok) {
+  if (p.vec_ok && !(p.g4_flags & 64)) {
     epilogue_direct(p, &acc[0][0], m0 + wm * 64, n0 + wn * 64, Cb, Rb, lane);
     return;
   }
@@ -1362,6 +1362,216 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256_kernel(GemmP p) {
   }
 }
 
+// ============================================================================================
+// Persistent 256x128 kernel for the short-K GEMMs (K <= 1536, plain K-major A and B: the
+// attention projections, the FFN conv2 and the data gradients of the 1x1 weights).
+//
+// Why: at K = 384 a 256x128 tile is 6 K-tiles of MFMA work, while the non-persistent kernels
+// pay, per tile and in series, the first LDS-DMA round trip, the epilogue, and the drain of
+// the tile's 64 KiB of stores before the CU takes its next block (one 144 KiB block per CU):
+// a K-sweep at fixed M x N put ~45 of the 82 us of the decoder QKV projection in that fixed
+// part, while the same stores alone stream at ~6 TB/s (tools/micro/store_bw.hip).
+// How: one block per CU walks its tiles through ONE continuous K-tile sequence: the 3-stage
+// LDS-DMA ring runs straight across tile boundaries (tile i+1's first K-tiles land while tile
+// i finishes), and each tile's epilogue stores straight from the MFMA registers (blocks
+// computed transposed: a lane holds 4 consecutive columns of one row) while the next tile's
+// loads are in flight.  Epilogue operands (bias, row scales, gate OR residual) are loaded
+// before the K-tile prefetch of the tile's last iteration, so waiting for them never waits for
+// a younger DMA; epilogue stores and loads go through the buffer resource with out-of-range
+// lanes at BUF_OOB, so every epilogue issues exactly 16 stores and the counted vmcnt waits of
+// the ring stay exact.  Tiles are split into 8 contiguous chunks, one per XCD (blocks b and
+// b + 8 share an XCD), walked row-major so consecutive tiles of a block share the A panel.
+// ============================================================================================
+typedef __attribute__((ext_vector_type(2))) int i32x2;
+__device__ void llvm_raw_buffer_store_v2i32(i32x2 data, i32x4 rsrc, int voffset, int soffset,
+                                            int aux) __asm("llvm.amdgcn.raw.buffer.store.v2i32");
+__device__ void llvm_raw_buffer_store_v4i32(i32x4 data, i32x4 rsrc, int voffset, int soffset,
+                                            int aux) __asm("llvm.amdgcn.raw.buffer.store.v4i32");
+__device__ i32x2 llvm_raw_buffer_load_v2i32(i32x4 rsrc, int voffset, int soffset,
+                                            int aux) __asm("llvm.amdgcn.raw.buffer.load.v2i32");
+
+constexpr int PK_STORES = 16;   // epilogue store instructions per wave per tile (4 x 4 blocks)
+
+template <int N>
+__device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
+__global__ void __launch_bounds__(BNT) gemm_pk_kernel(GemmP p) {
+  __shared__ __attribute__((aligned(16))) char smem[BIG_LDS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int li = lane & 15, lg = lane >> 4;
+  // this block's tiles: chunk [c0, c1) of its XCD, every nbx-th from c0 + local
+  const int ntile = p.tiles_m * p.tiles_n;
+  const int G = gridDim.x;
+  const int xcd = blockIdx.x & 7, local = blockIdx.x >> 3;
+  const int nbx = (G - xcd + 7) >> 3;
+  const int c0 = (int)((long)ntile * xcd / 8), c1 = (int)((long)ntile * (xcd + 1) / 8);
+  const int mine = local < c1 - c0 ? (c1 - c0 - local + nbx - 1) / nbx : 0;
+  const int nk = (p.K + 63) / 64;
+  const int total = mine * nk;
+  const i32x4 rsA = make_rsrc(p.A), rsB = make_rsrc(p.B), rsC = make_rsrc(p.C);
+  const i32x4 rsE = make_rsrc(p.gate ? p.gate : (p.residual ? p.residual : p.C));
+  const long lde = p.gate ? p.ldg : p.ldr;
+  const bool has_e = p.gate || p.residual;
+
+  // per-lane parts of the DMA addressing (as gemm_big_kernel, plain operands)
+  int ar[4], alc[4], br[2], blc[2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    ar[i] = (wave * 4 + i) * 8 + (lane >> 3);
+    alc[i] = (lane & 7) ^ (ar[i] & 7);
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    br[i] = (wave * 2 + i) * 8 + (lane >> 3);
+    blc[i] = (lane & 7) ^ (br[i] & 7);
+  }
+  auto issue = [&](int t, int kt, int stage) {
+    const int tile = c0 + local + t * nbx;
+    const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
+    const int k0 = kt * 64;
+    char* la = smem + stage * BIG_STAGE;
+    char* lb = la + BIG_A;
+    const bool kin = k0 + 64 <= p.K;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = tm * BBM + ar[i];
+      const bool ok = row < p.M && (kin || k0 + alc[i] * 8 < p.K);
+      blds16(rsA, ok ? (int)(((long)row * p.lda + alc[i] * 8) * 2) : BUF_OOB, k0 * 2,
+             la + (wave * 4 + i) * 1024);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = tn * 128 + br[i];
+      const bool ok = row < p.N && (kin || k0 + blc[i] * 8 < p.K);
+      blds16(rsB, ok ? (int)(((long)row * p.ldb + blc[i] * 8) * 2) : BUF_OOB, k0 * 2,
+             lb + (wave * 2 + i) * 1024);
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // epilogue operands of the current tile
+  f32x4 bv[4];
+  float rs[4], rs2[4];
+  i32x2 ev[4][4];
+
+  // (t, kt) of iterations it (current), it + 2 (prefetch)
+  int t = 0, kt = 0, t2 = 0, kt2 = 0;
+  if (total > 0) issue(0, 0, 0);
+  if (total > 1) { t2 = nk > 1 ? 0 : 1; kt2 = nk > 1 ? 1 : 0; issue(t2, kt2, 1); }
+  if (++kt2 == nk) { kt2 = 0; ++t2; }     // (t2, kt2) = iteration 2
+  bool prev_last = false;
+  for (int it = 0; it < total; ++it) {
+    const bool more = it + 1 < total;
+    // stage it landed: younger than its 6 pieces are those of it + 1 and, after a tile's
+    // epilogue, that epilogue's 16 stores
+    if (more) { if (prev_last) vm_wait<6 + PK_STORES>(); else vm_wait<6>(); }
+    else { if (prev_last) vm_wait<PK_STORES>(); else vm_wait<0>(); }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    const bool last = kt == nk - 1;
+    const int tile = c0 + local + t * nbx;
+    const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
+    const int mb = tm * BBM + wm * 64, nb = tn * 128 + wn * 64;
+    // epilogue operands one iteration ahead of the epilogue (nk >= 2): issued before this
+    // iteration's prefetch, they are retired by the NEXT iteration's stage wait, so the
+    // epilogue itself never waits on a load (with nk == 1 they are issued in the same one)
+    if (kt == (nk > 1 ? nk - 2 : 0)) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = nb + 16 * j + 4 * lg;
+        bv[j] = (p.bias && n < p.nvalid) ? *(const f32x4*)(p.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = mb + 16 * i + li;
+        const bool in = m < p.mvalid;
+        rs[i] = (p.row_scale && in) ? p.row_scale[m] : 1.f;
+        rs2[i] = (p.row_scale_post && in) ? p.row_scale_post[m] : 1.f;
+        if (has_e) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int n = nb + 16 * j + 4 * lg;
+            const bool ok = in && n < p.nvalid;
+            ev[i][j] = llvm_raw_buffer_load_v2i32(rsE, ok ? (int)(((long)m * lde + n) * 2) : BUF_OOB, 0, 0);
+          }
+        }
+      }
+    }
+    const bool pre = it + 2 < total;
+    if (pre) {
+      issue(t2, kt2, (it + 2) % 3);
+      if (++kt2 == nk) { kt2 = 0; ++t2; }
+    }
+    const char* la = smem + (it % 3) * BIG_STAGE;
+    const char* lb = la + BIG_A;
+    bf16x8 af[2][4], bfr[2][4];
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        af[s][i] = frag_bf16_kmajor(la, wm * 64 + i * 16, s, lane);
+        bfr[s][i] = frag_bf16_kmajor(lb, wn * 64 + i * 16, s, lane);
+      }
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[s][j], af[s][i], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 32, 0);
+    if (last) {
+      if (nk == 1) {   // operands issued this iteration: retire them, keep the prefetch in flight
+        if (pre) vm_wait<6>(); else vm_wait<0>();
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = mb + 16 * i + li;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int n = nb + 16 * j + 4 * lg;
+          const bool ok = m < p.mvalid && n < p.nvalid;
+          float v[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float x = epi_act(acc[i][j][e] + bv[j][e], p.relu);
+            const unsigned w = (unsigned)ev[i][j][e >> 1];
+            const float ef = __builtin_bit_cast(float, (e & 1) ? (w & 0xffff0000u) : (w << 16));
+            if (p.gate) x = ef > 0.f ? x : 0.f;
+            x *= rs[i];
+            if (p.residual) x += ef;
+            v[e] = x * rs2[i];
+          }
+          if (p.g4_flags & 16) {   // timing experiments only: no stores (wrong results)
+          } else if (p.c_fp32) {
+            const i32x4 d = {__builtin_bit_cast(int, v[0]), __builtin_bit_cast(int, v[1]),
+                             __builtin_bit_cast(int, v[2]), __builtin_bit_cast(int, v[3])};
+            llvm_raw_buffer_store_v4i32(d, rsC, ok ? (int)(((long)m * p.ldc + n) * 4) : BUF_OOB, 0, 0);
+          } else {
+            i32x2 d;
+            d[0] = (int)((unsigned)__builtin_bit_cast(unsigned short, (bf16)v[0]) |
+                         ((unsigned)__builtin_bit_cast(unsigned short, (bf16)v[1]) << 16));
+            d[1] = (int)((unsigned)__builtin_bit_cast(unsigned short, (bf16)v[2]) |
+                         ((unsigned)__builtin_bit_cast(unsigned short, (bf16)v[3]) << 16));
+            llvm_raw_buffer_store_v2i32(d, rsC, ok ? (int)(((long)m * p.ldc + n) * 2) : BUF_OOB, 0, 0);
+          }
+          acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      }
+    }
+    prev_last = last;
+    if (++kt == nk) { kt = 0; ++t; }
+  }
+}
+
 // compile-time A-operand conv variant for the large-tile kernels: 0 plain, 1 / 4 conv with
 // taps aligned to the k-granule, -1 anything else (run-time generic path)
 int conv_variant(const GemmP& q, int granule) {
@@ -1402,6 +1612,26 @@ int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
       split_big = max(1, min((tgt + tiles_big - 1) / tiles_big, nk / 8));
     }
     const bool slices = p.split_stride > 0 && p.split_k > 1;  // caller-chosen split, plain stores
+    // persistent 256x128 kernel: short-K plain GEMMs (FS2_GEMM_NO_PK=1 restores the per-tile
+    // kernels for A/B runs); 32-bit buffer offsets must cover A, B, C and the gate/residual
+    static const bool no_pk = getenv_flag("FS2_GEMM_NO_PK");
+    const long lim = 0x7fffffffL;
+    const bool pk_fits = (long)p.M * p.lda * 2 < lim && (long)p.N * p.ldb * 2 < lim &&
+                         (long)p.mvalid * p.ldc * (p.c_fp32 ? 4 : 2) < lim &&
+                         (long)p.mvalid * (p.gate ? p.ldg : p.ldr) * 2 < lim;
+    if (!no_pk && ak && bk && p.conv_mode == 0 && batch == 1 && p.split_k <= 1 && p.vec_ok &&
+        !p.accumulate && !(p.gate && p.residual) && p.K <= 1536 && pk_fits) {
+      GemmP q = p;
+      static const int pkf = [] { const char* v = std::getenv("FS2_PK_FLAGS"); return v ? std::atoi(v) : 0; }();
+      q.g4_flags = pkf;
+      q.tiles_m = (p.M + BBM - 1) / BBM;
+      const int nt = q.tiles_m * q.tiles_n;
+      // >= 8 blocks: every XCD chunk needs a block (blocks with no tile exit at once)
+      const int g = nt < 256 ? (nt + 7) / 8 * 8 : 256;
+      hipLaunchKernelGGL(gemm_pk_kernel, dim3(g), dim3(BNT), 0, s, q);
+      FS2_CHECK_LAUNCH();
+      return 0;
+    }
     // 256x256 phased kernel: wide outputs (< 10 % column padding; the QKV projection's
     // N = 1152 pads 11 % and measured 100 vs 85 us on the 256x128 kernel at M = 31264)
     static const bool no256 = getenv_flag("FS2_GEMM_NO256");

@@ -149,7 +149,131 @@ __global__ void __launch_bounds__(256) weight_prep_batched_kernel(const fs2_wpre
   }
 }
 
+// ---- AdamW fused with the weight-image preparation ----------------------------------------
+// The optimiser pass is the last reader and writer of every master weight in a step, and the
+// next forward's GEMMs need the bf16 images Wf (forward, [O][ldf]) and Wb (data gradient,
+// [C][KW*O]) of exactly the updated values.  One block per 64x64 tile (o, k = j*C + c) of each
+// GEMM weight runs the AdamW update of the tile (same per-element arithmetic as adamw_elem, so
+// identical parameters and moments) and writes the tile's Wf rows and, through an LDS
+// transpose, its Wb rows: the separate fs2_weight_prep_batched pass re-read all 85 M fp32
+// masters (0.33 GB) after AdamW had just written them.  Every other parameter (biases, norms,
+// embeddings) goes through the element-wise ranges kernel.
+struct AdamScal {
+  float decay_mul, w1, beta2, omb2, step_size, bc2_sqrt, eps, gscale;
+};
+
+template <typename T>
+__global__ void __launch_bounds__(256) adamw_prep_tiles_kernel(const fs2_wprep_desc* descs, int n,
+                                                               float* __restrict__ pb,
+                                                               const float* __restrict__ gb,
+                                                               float* __restrict__ mb,
+                                                               float* __restrict__ vb, AdamScal a) {
+  __shared__ int t0s[256];
+  __shared__ float tile[64][65];
+  __shared__ int jcs[64];
+  for (int i = threadIdx.x; i < n; i += blockDim.x) t0s[i] = descs[i].tile0;
+  __syncthreads();
+  const int blk = blockIdx.x;
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (t0s[mid] <= blk) lo = mid; else hi = mid - 1;
+  }
+  const fs2_wprep_desc d = descs[lo];
+  const int t = blk - d.tile0;
+  const int to = t / d.tiles_k, tk = t - to * d.tiles_k;
+  const int o0 = to * 64, k0 = tk * 64;
+  const int KC = d.KW * d.C;
+  const long base = d.W - pb;          // the weight's offset in the flat buffers ([O][KW][C])
+  if (threadIdx.x < 64) {
+    const int k = k0 + threadIdx.x;
+    const int j = k / d.C;
+    jcs[threadIdx.x] = (j << 16) | (k - j * d.C);
+  }
+  __syncthreads();
+  T* Wf = (T*)d.Wf;
+  for (int i = threadIdx.x; i < 64 * 64; i += blockDim.x) {
+    const int ol = i >> 6, kl = i & 63, o = o0 + ol, k = k0 + kl;
+    if (o >= d.O || k >= d.ldf) continue;
+    float v = 0.f;
+    if (k < KC) {
+      const long e = base + (long)o * KC + k;
+      float pi = pb[e], mi = mb[e], vi = vb[e];
+      adamw_elem(pi, mi, vi, gb[e], a.decay_mul, a.w1, a.beta2, a.omb2, a.step_size, a.bc2_sqrt,
+                 a.eps, a.gscale);
+      pb[e] = pi; mb[e] = mi; vb[e] = vi;
+      v = pi;
+    }
+    Wf[(long)o * d.ldf + k] = from_f<T>(v);
+    tile[ol][kl] = v;
+  }
+  if (!d.Wb) return;
+  __syncthreads();
+  T* Wb = (T*)d.Wb;
+  for (int i = threadIdx.x; i < 64 * 64; i += blockDim.x) {
+    const int kl = i >> 6, ol = i & 63, o = o0 + ol, k = k0 + kl;
+    if (o >= d.O || k >= KC) continue;
+    const int j = jcs[kl] >> 16, c = jcs[kl] & 0xffff;
+    Wb[(long)c * d.ldb + (long)j * d.O + o] = from_f<T>(tile[ol][kl]);
+  }
+}
+
+// ranges: int64 triples (flat start, length, first block); 1024 elements per block
+__global__ void __launch_bounds__(256) adamw_ranges_kernel(const int64_t* ranges, int n,
+                                                           float* __restrict__ pb,
+                                                           const float* __restrict__ gb,
+                                                           float* __restrict__ mb,
+                                                           float* __restrict__ vb, AdamScal a) {
+  const int blk = blockIdx.x;
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (ranges[3 * mid + 2] <= blk) lo = mid; else hi = mid - 1;
+  }
+  const long start = ranges[3 * lo], len = ranges[3 * lo + 1];
+  const long i0 = (long)(blk - ranges[3 * lo + 2]) * 1024 + threadIdx.x * 4;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const long i = i0 + e;
+    if (i >= len) break;
+    const long x = start + i;
+    float pi = pb[x], mi = mb[x], vi = vb[x];
+    adamw_elem(pi, mi, vi, gb[x], a.decay_mul, a.w1, a.beta2, a.omb2, a.step_size, a.bc2_sqrt,
+               a.eps, a.gscale);
+    pb[x] = pi; mb[x] = mi; vb[x] = vi;
+  }
+}
+
 }  // namespace
+
+extern "C" int fs2_adamw_prep(const fs2_wprep_desc* descs, int n, int total_tiles,
+                              const int64_t* ranges, int n_ranges, int range_blocks,
+                              float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                              float decay_mul, float one_minus_beta1, float beta2,
+                              float one_minus_beta2, float step_size, float bc2_sqrt, float eps,
+                              float grad_scale, int dtype, void* stream) {
+  if (!param || !grad || !exp_avg || !exp_avg_sq) return FS2_EINVAL;
+  if (n < 0 || n > 256 || (n > 0 && !descs) || (n_ranges > 0 && !ranges)) return FS2_EINVAL;
+  if (dtype != FS2_BF16 && dtype != FS2_F32) return FS2_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  const AdamScal a{decay_mul, one_minus_beta1, beta2, one_minus_beta2, step_size, bc2_sqrt, eps,
+                   grad_scale};
+  if (n > 0 && total_tiles > 0) {
+    if (dtype == FS2_BF16)
+      hipLaunchKernelGGL(adamw_prep_tiles_kernel<bf16>, dim3(total_tiles), dim3(256), 0, s, descs,
+                         n, param, grad, exp_avg, exp_avg_sq, a);
+    else
+      hipLaunchKernelGGL(adamw_prep_tiles_kernel<float>, dim3(total_tiles), dim3(256), 0, s,
+                         descs, n, param, grad, exp_avg, exp_avg_sq, a);
+    FS2_CHECK_LAUNCH();
+  }
+  if (n_ranges > 0 && range_blocks > 0) {
+    hipLaunchKernelGGL(adamw_ranges_kernel, dim3(range_blocks), dim3(256), 0, s, ranges, n_ranges,
+                       param, grad, exp_avg, exp_avg_sq, a);
+    FS2_CHECK_LAUNCH();
+  }
+  return 0;
+}
 
 extern "C" int fs2_weight_prep_batched(const fs2_wprep_desc* descs, int n, int total_tiles,
                                        int dtype, void* stream) {

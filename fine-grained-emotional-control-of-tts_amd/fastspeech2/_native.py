@@ -122,6 +122,7 @@ SIGNATURES = {
     "fs2_adamw": (I, [P, P, P, P, I64, Fl, Fl, Fl, Fl, Fl, Fl, Fl, Fl, P]),
     "fs2_weight_prep": (I, [P, I, I, I, I, P, I, P, I, I, P]),
     "fs2_weight_prep_batched": (I, [P, I, I, I, P]),
+    "fs2_adamw_prep": (I, [P, I, I, P, I, I, P, P, P, P, Fl, Fl, Fl, Fl, Fl, Fl, Fl, Fl, I, P]),
     "fs2_intensity_input": (I, [P, I, I, I, I, P, I, I, P]),
     "fs2_intensity_head": (I, [P, I64, P, P, P, P, P, I, I, I, I, P, I, P]),
     "fs2_phoneme_average": (I, [P, I, I, P, P, I, I, P, P]),

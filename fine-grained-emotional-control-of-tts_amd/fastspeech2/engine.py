@@ -189,6 +189,10 @@ class FS2Engine:
             if t is not None:
                 t.record_stream(main)
 
+    def _flat_is(self, flat):
+        """the engine's weight-image table was built over this flat parameter buffer"""
+        return self.m._flat is flat and self.dev == flat.device
+
     def grad_streams(self):
         """streams that may hold queued parameter-gradient writes (the aux stream's are joined
         into the main stream before the variance group completes)"""
@@ -251,6 +255,33 @@ class FS2Engine:
             self._wtable = ops.weight_prep_table(entries)
         ops.weight_prep_batched(*self._wtable, dt=self.dt)
         self._prepared_version = ver
+
+    def _adam_ranges(self):
+        """flat (start, length) ranges of every parameter that is not a GEMM weight (the
+        element-wise part of fs2_adamw_prep); neighbours separated only by the 16-float
+        alignment padding (zeros in every flat buffer) are merged"""
+        rng = []
+        for name, off, k, _, _ in self.m._layout:
+            if name in self._wspecs:
+                continue
+            if rng and off - (rng[-1][0] + rng[-1][1]) < 16:
+                rng[-1] = (rng[-1][0], off + k - rng[-1][0])
+            else:
+                rng.append((off, k))
+        return rng
+
+    def adamw_step(self, opt, decay_mul, omb1, beta2, omb2, step_size, bc2_sqrt, eps, gscale):
+        """AdamW over the flat buffers fused with the GEMM weight images (fs2_adamw_prep): the
+        next forward's prepare_weights finds them current and skips its own pass."""
+        m = self.m
+        if self._wtable is None:
+            self.prepare_weights(force=True)      # builds the descriptor table
+        if getattr(self, "_rtable", None) is None:
+            self._rtable = ops.adamw_ranges_table(self._adam_ranges(), self.dev)
+        ops.adamw_prep(self._wtable, self._rtable, m._flat, m._gflat, opt.exp_avg, opt.exp_avg_sq,
+                       decay_mul, omb1, beta2, omb2, step_size, bc2_sqrt, eps, gscale, dt=self.dt)
+        m.mark_params_updated()
+        self._prepared_version = (m._param_version, m._flat._version)
 
     def _dtag(self, kind, wname, T):
         """per-call-site tag for the detailed timer (FS2 layer indices folded)"""

@@ -285,6 +285,24 @@ def weight_prep_table(entries):
     return raw.to(dev), len(entries), t0
 
 
+def adamw_ranges_table(ranges, device):
+    """int64 (start, length, first block) triples for fs2_adamw_prep's element-wise part."""
+    rows, b0 = [], 0
+    for st, ln in ranges:
+        rows.append((st, ln, b0))
+        b0 += (ln + 1023) // 1024
+    t = torch.tensor(rows if rows else [(0, 0, 0)], dtype=torch.int64).reshape(-1)
+    return t.to(device), len(rows), b0
+
+
+def adamw_prep(wtable, rtable, param, grad, m, v, decay_mul, omb1, beta2, omb2, step_size,
+               bc2_sqrt, eps, gscale, *, dt):
+    (wt, n, tiles), (rt, nr, rb) = wtable, rtable
+    _chk(N.lib().fs2_adamw_prep(_p(wt), n, tiles, _p(rt), nr, rb, _p(param), _p(grad), _p(m),
+                                _p(v), decay_mul, omb1, beta2, omb2, step_size, bc2_sqrt, eps,
+                                gscale, dt, _s()), "fs2_adamw_prep")
+
+
 def weight_prep_batched(table, n, total_tiles, *, dt):
     _chk(N.lib().fs2_weight_prep_batched(_p(table), n, total_tiles, dt, _s()),
          "fs2_weight_prep_batched")

@@ -3,12 +3,19 @@
 Same hyper-parameters and update rule as ``torch.optim.AdamW(model.parameters(), lr=lr)``
 used by the reference (fastspeech2/train.py:232): betas (0.9, 0.999), eps 1e-8,
 weight_decay 1e-2.  Scalars are computed in Python double exactly as torch's single-tensor
-AdamW does, then one HBM-bound kernel (``fs2_adamw``) updates all 85.3 M parameters.
+AdamW does, then one HBM-bound pass updates all 85.3 M parameters: ``fs2_adamw_prep`` when the
+model's engine exists (the GEMM weights tile by tile, writing the next forward's bf16 weight
+images from the updated values; the rest element-wise), else ``fs2_adamw``.
 """
+
+import os
 
 import torch
 
 from . import ops
+
+# FS2_NO_FUSED_ADAMW=1: separate AdamW pass + weight-image pass at the next forward (A/B runs)
+_NO_FUSED = os.environ.get("FS2_NO_FUSED_ADAMW", "0") not in ("", "0")
 
 
 class FusedAdamW:
@@ -34,8 +41,13 @@ class FusedAdamW:
         lr, wd, t = self.lr, self.weight_decay, self.step_count
         bc1 = 1 - b1 ** t
         bc2 = 1 - b2 ** t
-        ops.adamw(m._flat, m._gflat, self.exp_avg, self.exp_avg_sq, m._flat.numel(),
-                  1 - lr * wd, 1 - b1, b2, 1 - b2, lr / bc1, bc2 ** 0.5, self.eps, grad_scale)
+        args = (1 - lr * wd, 1 - b1, b2, 1 - b2, lr / bc1, bc2 ** 0.5, self.eps, grad_scale)
+        eng = m._engine
+        if eng is not None and not _NO_FUSED and eng._flat_is(m._flat):
+            # the update also writes the next forward's GEMM weight images
+            eng.adamw_step(self, *args)
+            return
+        ops.adamw(m._flat, m._gflat, self.exp_avg, self.exp_avg_sq, m._flat.numel(), *args)
         m.mark_params_updated()
 
     def state_dict(self):

@@ -281,6 +281,16 @@ typedef struct fs2_wprep_desc {
 } fs2_wprep_desc;
 int fs2_weight_prep_batched(const fs2_wprep_desc* descs, int n, int total_tiles, int dtype,
                             void* stream);
+/* AdamW fused with the weight images (replaces fs2_adamw + fs2_weight_prep_batched after an
+ * optimiser step, K17 of SURVEY §2): the descriptor table's weights are updated tile by tile
+ * and their Wf / Wb images written from the updated values; every other parameter lies in
+ * `ranges` (int64 triples: flat start, length, first block; 1024 elements per block).  All
+ * pointers index the same flat layout: descs[i].W - param is a weight's flat offset. */
+int fs2_adamw_prep(const fs2_wprep_desc* descs, int n, int total_tiles, const int64_t* ranges,
+                   int n_ranges, int range_blocks, float* param, const float* grad,
+                   float* exp_avg, float* exp_avg_sq, float decay_mul, float one_minus_beta1,
+                   float beta2, float one_minus_beta2, float step_size, float bc2_sqrt, float eps,
+                   float grad_scale, int dtype, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Frozen IntensityExtractor forward pieces + phoneme averaging (SURVEY §8f-1;

@@ -313,3 +313,38 @@ def test_graph_replayed_step_equals_eager_step(cuda, cfg_all):
     dp = (pe - pg).abs()
     assert dp.max().item() <= 3 * 2.1e-4
     assert (dp > 1e-6).float().mean().item() <= 1e-3
+
+
+@pytest.mark.parametrize("dtname", ["bfloat16", "float32"])
+def test_fused_adamw_writes_the_weight_images(cuda, cfg_all, dtname, monkeypatch):
+    """fs2_adamw_prep (AdamW fused with the GEMM weight images) == fs2_adamw followed by the
+    separate fs2_weight_prep_batched pass, bit for bit: parameters, both moments and every
+    Wf / Wb image; the next forward then skips its weight-prep pass."""
+    from fastspeech2.model import FastSpeech2
+    from fastspeech2.optim import FusedAdamW
+    from fastspeech2 import optim as optim_mod
+    kw = dict(cfg_all["model"]["fastspeech2"], enc_num_layers=1, dec_num_layers=1)
+    dt = getattr(torch, dtname)
+    res = []
+    for fused in (True, False):
+        monkeypatch.setattr(optim_mod, "_NO_FUSED", not fused)
+        torch.manual_seed(0)
+        m = FastSpeech2(**kw, n_speakers=4, act_dtype=dt).cuda()
+        eng = m.engine()
+        eng.prepare_weights()
+        g = torch.Generator(device="cuda").manual_seed(5)
+        m._gflat.copy_(torch.randn(m._gflat.shape, device="cuda", generator=g) * 1e-3)
+        opt = FusedAdamW(m, lr=1e-3)
+        for _ in range(2):
+            opt.step(grad_scale=0.5)
+        eng.prepare_weights()              # unfused: rebuilds the images; fused: already current
+        torch.cuda.synchronize()
+        res.append((m._flat.clone(), opt.exp_avg.clone(), opt.exp_avg_sq.clone(),
+                    {k: (a.clone(), b.clone()) for k, (a, b) in eng.w.items()},
+                    eng._prepared_version == (m._param_version, m._flat._version)))
+    (p1, m1, v1, w1, ok1), (p2, m2, v2, w2, ok2) = res
+    assert ok1 and ok2
+    assert torch.equal(p1, p2) and torch.equal(m1, m2) and torch.equal(v1, v2)
+    for k in w1:
+        assert torch.equal(w1[k][0], w2[k][0]), k
+        assert torch.equal(w1[k][1], w2[k][1]), k
