@@ -14,35 +14,33 @@
 
 namespace {
 
-__global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
-                             float* __restrict__ m, float* __restrict__ v, long n, float decay_mul,
-                             float w1, float beta2, float omb2, float step_size, float bc2_sqrt,
-                             float eps, float gscale) {
-  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const float gr = g[i] * gscale;
-  float pi = p[i] * decay_mul;
-  float mi = m[i];
-  // torch lerp: weight < 0.5 -> self + w * (end - self)
-  mi = (w1 < 0.5f) ? mi + w1 * (gr - mi) : gr - (gr - mi) * (1.f - w1);
-  float vi = v[i] * beta2 + omb2 * gr * gr;
-  const float denom = sqrtf(vi) / bc2_sqrt + eps;
-  pi = pi + (-step_size) * (mi / denom);
-  p[i] = pi; m[i] = mi; v[i] = vi;
-}
-
 // 4 elements per lane through 16-byte loads / stores (same per-element arithmetic as
 // adamw_kernel, so identical results): the scalar kernel ran at ~5.3 TB/s
 __device__ __forceinline__ void adamw_elem(float& pi, float& mi, float& vi, float gi,
                                            float decay_mul, float w1, float beta2, float omb2,
                                            float step_size, float bc2_sqrt, float eps,
                                            float gscale) {
+  // no FMA contraction: every kernel that inlines this (vector, tile-fused, ranges) must round
+  // identically, whatever the surrounding code lets the compiler fuse
+#pragma clang fp contract(off)
   const float gr = gi * gscale;
   pi = pi * decay_mul;
   mi = (w1 < 0.5f) ? mi + w1 * (gr - mi) : gr - (gr - mi) * (1.f - w1);
   vi = vi * beta2 + omb2 * gr * gr;
   const float denom = sqrtf(vi) / bc2_sqrt + eps;
   pi = pi + (-step_size) * (mi / denom);
+}
+
+__global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
+                             float* __restrict__ m, float* __restrict__ v, long n, float decay_mul,
+                             float w1, float beta2, float omb2, float step_size, float bc2_sqrt,
+                             float eps, float gscale) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  // torch lerp: weight < 0.5 -> self + w * (end - self)  (adamw_elem)
+  float pi = p[i], mi = m[i], vi = v[i];
+  adamw_elem(pi, mi, vi, g[i], decay_mul, w1, beta2, omb2, step_size, bc2_sqrt, eps, gscale);
+  p[i] = pi; m[i] = mi; v[i] = vi;
 }
 
 __global__ void __launch_bounds__(256) adamw_vec_kernel(float* __restrict__ p,
