@@ -103,15 +103,6 @@ __global__ void fs2_seed_base_kernel(uint32_t v) { g_fs2_seed_base = v; }
     return (int)hipGetLastError();                                        \
   }
 
-__device__ __forceinline__ bool fs2_keep(uint32_t seed, uint32_t salt, uint64_t idx, float p) {
-  if (p <= 0.f) return true;
-  seed += g_fs2_seed_base;
-  uint32_t h = fs2_mix32((uint32_t)idx ^ fs2_mix32(seed ^ (salt * 0x9E3779B9u)));
-  h = fs2_mix32(h ^ (uint32_t)(idx >> 32) ^ 0x68bc21ebu);
-  // uniform in [0,1) with 24 bits
-  float u = (float)(h >> 8) * (1.0f / 16777216.0f);
-  return u >= p;
-}
 
 // Attention-probability dropout draws B*H*T^2 masks per layer, so it uses a cheaper form:
 // one murmur-finaliser round per PAIR of elements (idx >> 1) keyed by a per-call key, 16 bits
@@ -133,6 +124,29 @@ __device__ __forceinline__ bool fs2_keep_fast(uint32_t key, uint64_t idx, uint32
   return fs2_keep_pair_bit(fs2_hash_pair(key, idx >> 1), idx, thr16);
 }
 __device__ __forceinline__ uint32_t fs2_thr16(float p) { return (uint32_t)(p * 65536.f + 0.5f); }
+
+// Element dropout (LayerNorm residual / output dropout) uses the same pair hash: element idx of
+// the (seed, salt) stream is kept iff its 16-bit half of hash_pair(key, idx >> 1) >= thr16(p).
+// Kernels that own consecutive elements compute one hash per pair (fs2_keep_pair_bit);
+// fs2_keep is the per-element form with identical results.  (One murmur-style round per two
+// elements instead of two full murmur finalisers per element: the LayerNorm kernels spent
+// more VALU on their masks than on the normalisation.)
+__device__ __forceinline__ bool fs2_keep(uint32_t seed, uint32_t salt, uint64_t idx, float p) {
+  if (p <= 0.f) return true;
+  return fs2_keep_fast(fs2_drop_key(seed, salt), idx, fs2_thr16(p));
+}
+// keep bits of V consecutive elements from an EVEN index ib, one hash per pair (== fs2_keep)
+template <int V>
+__device__ __forceinline__ void fs2_keep_run(uint32_t seed, uint32_t salt, uint64_t ib, float p,
+                                             bool (&k)[V]) {
+  const uint32_t key = fs2_drop_key(seed, salt), thr = fs2_thr16(p);
+#pragma unroll
+  for (int e = 0; e < V; e += 2) {
+    const uint32_t h = fs2_hash_pair(key, (ib + e) >> 1);
+    k[e] = p <= 0.f || fs2_keep_pair_bit(h, ib + e, thr);
+    k[e + 1] = p <= 0.f || fs2_keep_pair_bit(h, ib + e + 1, thr);
+  }
+}
 
 // reflect index into [0, T) (torch F.pad(mode="reflect") semantics, single bounce)
 __device__ __forceinline__ int reflect_idx(int i, int T) {

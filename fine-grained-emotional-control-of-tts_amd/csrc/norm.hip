@@ -223,11 +223,12 @@ __global__ void __launch_bounds__(256) ln_fwd_vec_kernel(LnFwdP p) {
       if (r) {
         float rv[V];
         vload<T>(rv, r + d0);
+        bool kr[V];
+        if (p.p_r > 0.f) fs2_keep_run<V>(p.seed, p.salt_r, (uint64_t)row * p.D + d0, p.p_r, kr);
 #pragma unroll
         for (int e = 0; e < V; ++e) {
           float q = rv[e];
-          if (p.p_r > 0.f)
-            q = fs2_keep(p.seed, p.salt_r, (uint64_t)row * p.D + d0 + e, p.p_r) ? q * inv_r : 0.f;
+          if (p.p_r > 0.f) q = kr[e] ? q * inv_r : 0.f;
           v[ch][e] += q;
         }
       }
@@ -262,12 +263,13 @@ __global__ void __launch_bounds__(256) ln_fwd_vec_kernel(LnFwdP p) {
     const int d0 = (lane + 64 * ch) * V;
     if (d0 < p.D) {
       float o[V];
+      bool ko[V];
+      if (p.p_o > 0.f) fs2_keep_run<V>(p.seed, p.salt_o, (uint64_t)row * p.D + d0, p.p_o, ko);
 #pragma unroll
       for (int e = 0; e < V; ++e) {
         float q = (v[ch][e] - mean) * rstd * g[ch][e] + b[ch][e];
         if (p.do_tanh) q = tanhf(q);
-        if (p.p_o > 0.f)
-          q = fs2_keep(p.seed, p.salt_o, (uint64_t)row * p.D + d0 + e, p.p_o) ? q * inv_o : 0.f;
+        if (p.p_o > 0.f) q = ko[e] ? q * inv_o : 0.f;
         q *= rm;
         if (pa) q += a[ch][e];
         o[e] = q;
@@ -314,12 +316,13 @@ __global__ void __launch_bounds__(256) ln_bwd_vec_kernel(LnBwdP p, float* part, 
           vload<float>(bt, p.beta + d0);
           if constexpr (V == 8) vload<float>(bt + 4, p.beta + d0 + 4);
         }
+        bool ko[V];
+        if (p.p_o > 0.f) fs2_keep_run<V>(p.seed, p.salt_o, (uint64_t)row * p.D + d0, p.p_o, ko);
 #pragma unroll
         for (int e = 0; e < V; ++e) {
           xh[ch][e] = (sv[ch][e] - mean) * rstd;
           float gg = dv[e] * rm;
-          if (p.p_o > 0.f)
-            gg = fs2_keep(p.seed, p.salt_o, (uint64_t)row * p.D + d0 + e, p.p_o) ? gg * inv_o : 0.f;
+          if (p.p_o > 0.f) gg = ko[e] ? gg * inv_o : 0.f;
           if (p.do_tanh) {
             const float t = tanhf(xh[ch][e] * gm[e] + bt[e]);
             gg *= (1.f - t * t);
@@ -344,6 +347,8 @@ __global__ void __launch_bounds__(256) ln_bwd_vec_kernel(LnBwdP p, float* part, 
       const int d0 = (lane + 64 * ch) * V;
       if (d0 < p.D) {
         float o[V], w[V];
+        bool kr[V];
+        if (dr && p.p_r > 0.f) fs2_keep_run<V>(p.seed, p.salt_r, (uint64_t)row * p.D + d0, p.p_r, kr);
 #pragma unroll
         for (int e = 0; e < V; ++e) {
           float q = rstd * (g[ch][e] - a1 - xh[ch][e] * a2);
@@ -351,8 +356,7 @@ __global__ void __launch_bounds__(256) ln_bwd_vec_kernel(LnBwdP p, float* part, 
           o[e] = q;
           if (dr) {
             float t = q;
-            if (p.p_r > 0.f)
-              t = fs2_keep(p.seed, p.salt_r, (uint64_t)row * p.D + d0 + e, p.p_r) ? t * inv_r : 0.f;
+            if (p.p_r > 0.f) t = kr[e] ? t * inv_r : 0.f;
             w[e] = t;
           }
         }
@@ -409,6 +413,8 @@ __global__ void __launch_bounds__(256) ln_bwd_rows_kernel(LnBwdP p, float* part,
   }
   const float inv_o = p.p_o > 0.f ? 1.f / (1.f - p.p_o) : 1.f;
   const float inv_r = p.p_r > 0.f ? 1.f / (1.f - p.p_r) : 1.f;
+  const uint32_t key_o = fs2_drop_key(p.seed, p.salt_o), key_r = fs2_drop_key(p.seed, p.salt_r);
+  const uint32_t thr_o = fs2_thr16(p.p_o), thr_r = fs2_thr16(p.p_r);
   const int rbeg = blockIdx.x * p.rows_per_block;
   const int rend = min(p.M, rbeg + p.rows_per_block);
   for (int row0 = rbeg + wave; row0 < rend; row0 += 4 * R) {
@@ -436,6 +442,14 @@ __global__ void __launch_bounds__(256) ln_bwd_rows_kernel(LnBwdP p, float* part,
         sv[2 * w] = __builtin_bit_cast(float, us[j][w] << 16);
         sv[2 * w + 1] = __builtin_bit_cast(float, us[j][w] & 0xffff0000u);
       }
+      // element (row, d0 + e): pairs (e, e + 1) share one hash (row * D + d0 is even)
+      const uint64_t ib = (uint64_t)row * p.D + d0;
+      uint32_t ho[V / 2], hr[V / 2];
+#pragma unroll
+      for (int e = 0; e < V / 2; ++e) {
+        ho[e] = p.p_o > 0.f ? fs2_hash_pair(key_o, (ib >> 1) + e) : 0u;
+        hr[e] = (p.dr && p.p_r > 0.f) ? fs2_hash_pair(key_r, (ib >> 1) + e) : 0u;
+      }
       if (act) {
 #pragma unroll
         for (int e = 0; e < V; ++e) {
@@ -443,8 +457,7 @@ __global__ void __launch_bounds__(256) ln_bwd_rows_kernel(LnBwdP p, float* part,
                                                              : (ud[j][e >> 1] << 16));
           xh[e] = (sv[e] - mean[j]) * rstd[j];
           float gg = dv * rm[j];
-          if (p.p_o > 0.f)
-            gg = fs2_keep(p.seed, p.salt_o, (uint64_t)row * p.D + d0 + e, p.p_o) ? gg * inv_o : 0.f;
+          if (p.p_o > 0.f) gg = fs2_keep_pair_bit(ho[e >> 1], ib + e, thr_o) ? gg * inv_o : 0.f;
           if constexpr (TANH) {
             const float t = tanhf(xh[e] * gm[e] + bt[e]);
             gg *= (1.f - t * t);
@@ -469,8 +482,7 @@ __global__ void __launch_bounds__(256) ln_bwd_rows_kernel(LnBwdP p, float* part,
           if (p.relu_gate_in && !(sv[e] > 0.f)) q = 0.f;
           o[e] = q;
           w[e] = q;
-          if (p.dr && p.p_r > 0.f)
-            w[e] = fs2_keep(p.seed, p.salt_r, (uint64_t)row * p.D + d0 + e, p.p_r) ? q * inv_r : 0.f;
+          if (p.dr && p.p_r > 0.f) w[e] = fs2_keep_pair_bit(hr[e >> 1], ib + e, thr_r) ? q * inv_r : 0.f;
         }
         vstore<bf16>((bf16*)p.ds + (long)row * p.ldds + d0, o);
         if (p.dr) vstore<bf16>((bf16*)p.dr + (long)row * p.D + d0, w);

@@ -151,24 +151,9 @@ def test_layernorm_fwd_bwd(cuda, dt, code, tol, D):
 
 
 def _keep_ln_np(seed, salt, idx, p):
-    """numpy restatement of fs2_keep (fs2_common.h): the per-element LayerNorm dropout mask."""
-    M32 = np.uint64(0xffffffff)
-
-    def mix(h):
-        h = h & M32
-        h ^= h >> np.uint64(16)
-        h = (h * np.uint64(0x85ebca6b)) & M32
-        h ^= h >> np.uint64(13)
-        h = (h * np.uint64(0xc2b2ae35)) & M32
-        h ^= h >> np.uint64(16)
-        return h
-
-    k = mix(np.uint64((seed ^ ((salt * 0x9E3779B9) & 0xffffffff)) & 0xffffffff))
-    idx = idx.astype(np.uint64)
-    h = mix((idx & M32) ^ k)
-    h = mix(h ^ (idx >> np.uint64(32)) ^ np.uint64(0x68bc21eb))
-    u = (h >> np.uint64(8)).astype(np.float64) / 16777216.0
-    return u >= np.float32(p)
+    """The per-element LayerNorm dropout mask: fs2_keep (fs2_common.h) is the same pair hash as
+    the attention mask (restated by _keep_np below), evaluated per element."""
+    return _keep_np(seed, salt, idx, p)
 
 
 @pytest.mark.parametrize("M,D", [(300, 384), (1001, 384), (203, 256)])
