@@ -17,6 +17,8 @@
 // (col = lane&15, row = 4*(lane>>4) + r), so the epilogue is common.
 // Register-staged double buffering: the next K-tile's global loads are in flight while
 // the current tile's MFMAs run; one barrier per K-tile.
+#include <type_traits>
+
 #include "fs2_common.h"
 
 #include <cstdlib>
@@ -1126,6 +1128,10 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256_kernel(GemmP p) {
       abt[i] = b * p.conv_t;
       at[i] = rr - b * rpu;
       avo[i] = aval[i] ? (int)(((long)rr * p.lda + ac[i] * 8) * 2) : BUF_OOB;
+      if (p.g4_flags & 128) {  // timing experiment: 8 full 128-B rows per piece (wrong results)
+        const int r2 = m0 + piece * 16 + (lane >> 3) + 8 * i;
+        avo[i] = r2 < p.M ? (int)(((long)r2 * p.lda + (lane & 7) * 8) * 2) : BUF_OOB;
+      }
     } else {             // 2 k-rows x 512 B per piece
       const int kr = piece * 2 + (lane >> 5);
       ac[i] = (lane & 31) ^ mn_swz<bf16>(kr);
@@ -1150,6 +1156,10 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256_kernel(GemmP p) {
       const int row = n0 + r;
       bval[i] = row < p.N;
       bvo[i] = bval[i] ? (int)(((long)row * p.ldb + bc[i] * 8) * 2) : BUF_OOB;
+      if (p.g4_flags & 128) {
+        const int r2 = n0 + piece * 16 + (lane >> 3) + 8 * i;
+        bvo[i] = r2 < p.N ? (int)(((long)r2 * p.ldb + (lane & 7) * 8) * 2) : BUF_OOB;
+      }
       bkr[i] = 0; bb[i] = 0; bt[i] = 0;
     } else {
       const int kr = piece * 2 + (lane >> 5);
@@ -1198,7 +1208,7 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256_kernel(GemmP p) {
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
           const int vo = (kin || k0 + ac[i] * 8 < K) ? avo[i] : BUF_OOB;
-          blds16(rsA, vo, k0 * 2, dst + (wave * 2 + i) * 1024);
+          blds16(rsA, vo, ((p.g4_flags & 128) ? (k0 & ~63) : k0) * 2, dst + (wave * 2 + i) * 1024);
         }
       } else {                                  // taps not aligned to 32-wide regions
 #pragma unroll
@@ -1232,7 +1242,7 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256_kernel(GemmP p) {
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int vo = (kin || k0 + bc[i] * 8 < K) ? bvo[i] : BUF_OOB;
-        blds16(rsB, vo, k0 * 2, dst + (wave * 2 + i) * 1024);
+        blds16(rsB, vo, ((p.g4_flags & 128) ? (k0 & ~63) : k0) * 2, dst + (wave * 2 + i) * 1024);
       }
     } else if (!bconv3) {
       const bool kin = k0 + 32 <= kva;
@@ -1293,6 +1303,7 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256_kernel(GemmP p) {
   const bool prio = !(p.g4_flags & 2);
   const bool nowait = p.g4_flags & 4;   // timing experiments only (wrong results)
   const bool noissue = p.g4_flags & 8;
+  const bool dma_mm = p.g4_flags & 256;  // LDS-DMA issued inside the matrix section
   // stagger: waves 4-7 half a phase behind; without it both groups retire DMA like group 1
   const int grp = stag ? wr : 1;
   if (stag && wr == 1) __builtin_amdgcn_s_barrier();
@@ -1317,14 +1328,15 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256_kernel(GemmP p) {
       for (int i = 0; i < 4; ++i)
         af[i] = AK ? g4_frag_k(rA, wr * 128 + mq * 64 + i * 16 + (lane & 15), lane >> 4)
                    : frag_bf16_mnmajor512(rA, wr * 128 + mq * 64 + i * 16, 0, lane);
-      if (!noissue) {
-        if (ph < 2) { if (more) issue(it + 1, 3 - ph); }
-        else if (it + 2 < nk) issue(it + 2, 3 - ph);
-      }
-      // phase 1 retires this tile's k1 regions, phase 3 the next tile's k0 regions
+      const bool iss = !noissue && (ph < 2 ? more : it + 2 < nk);
+      if (iss && !dma_mm) issue(ph < 2 ? it + 1 : it + 2, 3 - ph);
+      // phase 1 retires this tile's k1 regions, phase 3 the next tile's k0 regions (with the
+      // issue in the matrix section, this phase's 2 pieces are not yet counted here)
       if (grp == 1 && (ph & 1) && !nowait && !noissue) {
-        if (ph == 1 ? more : it + 2 < nk) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        else if (ph == 3 && more) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        if (iss) {
+          if (dma_mm) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+          else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        } else if (ph == 3 && more) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       __builtin_amdgcn_s_barrier();
@@ -1333,11 +1345,17 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256_kernel(GemmP p) {
       // ---- matrix section: one 64x64 quadrant x K=32 ----
       if (prio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < 4; ++i) {
+        if (i == 2 && dma_mm) {   // this phase's region issued between the MFMAs
+          __builtin_amdgcn_sched_barrier(0);
+          if (iss) issue(ph < 2 ? it + 1 : it + 2, 3 - ph);
+          __builtin_amdgcn_sched_barrier(0);
+        }
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           acc[mq * 4 + i][j] =
               __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[mq * 4 + i][j], 0, 0, 0);
+      }
       if (prio) __builtin_amdgcn_s_setprio(0);
       if (grp == 0 && (ph & 1) && !nowait && !noissue) {
         if (ph == 1 ? more : it + 2 < nk) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
@@ -1589,6 +1607,334 @@ __global__ void __launch_bounds__(BNT) gemm_pk_kernel(GemmP p) {
   }
 }
 
+// ============================================================================================
+// Persistent 256 x BN kernel (BN = 4 * WN = 256 or 192) for the long-K GEMMs with K-major A and
+// B: the FFN conv1 forward (implicit reflect conv, K = 9 x 384) and its data gradient over the
+// padded domain (K = 9 x 1536, N = 384: 256 x 192 tiles put the decoder's 248 tiles in ONE round
+// of the 256 CUs without a K split).
+//
+// Why not gemm256_kernel: a K-sweep at M = 31264, N = 1536 (tools/gemm256_ksweep.py) split its
+// time into ~25 us per round of tiles (prologue DMA round trip, LDS-staged epilogue and store
+// drain, all in series per tile) and a main loop at 1186 TF/s -- 1583 with the LDS-DMA issue
+// removed, 1300 when each DMA piece covers whole 128-byte rows.  Its regions hold 32-wide K
+// halves, so every global cache line is fetched twice, half at a time, phases apart.
+// How:
+//  * LDS images with 128-byte rows (one 64-wide K-tile): A 256 x 128 B, B BN x 128 B per slot,
+//    2 slots; 16-byte chunk c of row r at c ^ ((r >> 1) & 7) (conflict-free ds_read_b128 of 16
+//    rows x one chunk per lane group; the swizzle is applied to the DMA SOURCE address).
+//  * DMA units of one K-tile: A0 = rows {0-63, 128-191}, A1 = rows {64-127, 192-255} (2 pieces
+//    of 8 rows per wave each), B0 = B rows 0-127 (2 per wave), B1 = B rows 128.. (NB1 per wave).
+//  * 4 phases per K-tile, each 16 MFMAs of one 64-row half of the wave's 128 x WN block x
+//    K = 32 (ph = 2 * mq + kh); the wave's B fragments for both K halves are read in phase 0.
+//    Last reads of a slot: A0 and B in phase 0/1, A1 in phase 3.  Iteration g issues A0(g+1),
+//    A1(g+1), B0(g+2), B1(g+2) in phases 0..3 -- each >= 2 phases after the last read of its
+//    slot region and 4-6 phases before its first read -- and retires them with counted waits
+//    in phase 1 (A1 of g) and phase 3 (A0, B of g+1), never vmcnt(0) inside a tile.
+//  * Waves 4-7 run half a phase behind (one extra barrier) so each SIMD pairs one wave's
+//    MFMA section with its partner's LDS reads and DMA issue (as gemm256_kernel).
+//  * One block per CU walks its tiles (8 contiguous XCD chunks, row-major so consecutive tiles
+//    share the A panel) through ONE continuous K-tile stream: the next tile's first K-tiles
+//    land while the current one finishes; each tile's epilogue stores straight from the MFMA
+//    registers (blocks computed transposed: a lane holds 4 consecutive columns of one row),
+//    exactly 8 x NJ buffer stores per wave (out-of-range lanes at BUF_OOB) so the counted waits
+//    of the ring stay exact.
+// ============================================================================================
+__device__ __forceinline__ int ps_sw(int row) { return (row >> 1) & 7; }
+
+template <int CM, int WN>   // CM: 0 plain, 1 reflect "same" conv, 4 padded-domain conv (dgrad)
+__global__ void __launch_bounds__(BNT, 1) gemm_ps_kernel(GemmP p) {
+  constexpr int BN = 4 * WN, NJ = WN / 16;
+  constexpr int AIMG = 256 * 128;
+  constexpr int SLOT = AIMG + BN * 128;
+  constexpr int NB1 = (BN - 128) / 64;     // B1 pieces per wave
+  constexpr int S = 8 * NJ;                // epilogue stores per wave per tile
+  static_assert(2 * SLOT <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) char smem[2 * SLOT];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int li = lane & 15, lg = lane >> 4;
+  const int ntile = p.tiles_m * p.tiles_n;
+  const int G = gridDim.x;
+  const int xcd = blockIdx.x & 7, local = blockIdx.x >> 3;
+  const int nbx = (G - xcd + 7) >> 3;
+  const int c0 = (int)((long)ntile * xcd / 8), c1 = (int)((long)ntile * (xcd + 1) / 8);
+  const int mine = local < c1 - c0 ? (c1 - c0 - local + nbx - 1) / nbx : 0;
+  const int nk = (p.K + 63) / 64;
+  const int total = mine * nk;
+  if (total == 0) return;
+  const i32x4 rsA = make_rsrc(p.A), rsB = make_rsrc(p.B), rsC = make_rsrc(p.C);
+  const int K = p.K;
+  const int rpu = CM == 4 ? p.conv_t + 2 * p.conv_p : p.conv_t;
+  const int cpt = CM ? p.conv_c / 64 : 1;   // K-tiles per tap
+
+  // ---- per-lane DMA state.  A pieces q = 0..3 (unit q >> 1, piece q & 1), B pieces 0..3.
+  const int prow = lane >> 3;
+  // piece base rows (wave-uniform: the LDS-DMA destination goes through M0) and lane rows
+  int abase[4], arow[4], alc[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int u = wave * 2 + (q & 1);
+    abase[q] = (u < 8 ? u * 8 : 128 + (u - 8) * 8) + (q >> 1) * 64;
+    arow[q] = abase[q] + prow;
+    alc[q] = (lane & 7) ^ ps_sw(arow[q]);
+  }
+  int bbase[2 + NB1], brow[2 + NB1], blc[2 + NB1];
+#pragma unroll
+  for (int q = 0; q < 2 + NB1; ++q) {
+    bbase[q] = q < 2 ? (wave * 2 + q) * 8 : 128 + (NB1 == 2 ? wave * 2 + (q - 2) : wave) * 8;
+    brow[q] = bbase[q] + prow;
+    blc[q] = (lane & 7) ^ ps_sw(brow[q]);
+  }
+  // A stream (units of iteration g + 1): tile ordinal, k-tile, tap, row info, lane offsets
+  int a_t = 0, a_kt = -1, a_tap = 0, a_c = 0;
+  int abt[4], at_[4], aoff[4];
+  bool aval[4];
+  auto a_point = [&]() {   // lane offsets of the current tap (conv) / row (plain)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if constexpr (CM == 0) {
+        aoff[q] = aval[q] ? (int)(((long)at_[q] * p.lda + alc[q] * 8) * 2) : BUF_OOB;
+      } else {
+        int ts;
+        bool ok = aval[q];
+        if constexpr (CM == 1) {
+          ts = reflect_idx(at_[q] + a_tap - p.conv_p, p.conv_t);
+        } else {
+          ts = at_[q] - a_tap;
+          ok = ok && ts >= 0 && ts < p.conv_t;
+        }
+        aoff[q] = ok ? (int)(((long)(abt[q] + ts) * p.lda + alc[q] * 8) * 2) : BUF_OOB;
+      }
+    }
+  };
+  auto a_advance = [&]() {  // to the next iteration of the A stream
+    if (++a_kt == nk) { a_kt = 0; ++a_t; }
+    if (a_kt == 0) {
+      const int tile = c0 + local + a_t * nbx;
+      const int tm = tile / p.tiles_n;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = tm * 256 + arow[q];
+        aval[q] = row < p.M;
+        const int rr = aval[q] ? row : 0;
+        if constexpr (CM == 0) {
+          at_[q] = rr;
+          abt[q] = 0;
+        } else {
+          const int b = rr / rpu;
+          abt[q] = b * p.conv_t;
+          at_[q] = rr - b * rpu;
+        }
+      }
+      a_tap = 0; a_c = 0;
+      a_point();
+    } else if constexpr (CM != 0) {
+      if (++a_c == cpt) { a_c = 0; ++a_tap; a_point(); }
+    }
+  };
+  auto issue_a = [&](int unit, char* slot) {
+    const int k0 = a_kt * 64;
+    const int soff = __builtin_amdgcn_readfirstlane((CM ? a_c * 64 : k0) * 2);   // uniform by construction
+    const bool kin = k0 + 64 <= K;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int q = unit * 2 + j;
+      const int vo = (kin || k0 + alc[q] * 8 < K) ? aoff[q] : BUF_OOB;
+      blds16(rsA, vo, soff, slot + abase[q] * 128);
+    }
+  };
+  // B stream (units of iteration g + 2)
+  int b_t = 0, b_kt = -1;
+  int boff[2 + NB1];
+  auto b_advance = [&]() {
+    if (++b_kt == nk) { b_kt = 0; ++b_t; }
+    if (b_kt == 0) {
+      const int tile = c0 + local + b_t * nbx;
+      const int tn = tile - (tile / p.tiles_n) * p.tiles_n;
+#pragma unroll
+      for (int q = 0; q < 2 + NB1; ++q) {
+        const int row = tn * BN + brow[q];
+        boff[q] = row < p.N ? (int)(((long)row * p.ldb + blc[q] * 8) * 2) : BUF_OOB;
+      }
+    }
+  };
+  auto issue_b = [&](int unit, char* slot) {
+    const int k0 = b_kt * 64;
+    const bool kin = k0 + 64 <= K;
+#pragma unroll
+    for (int q = unit * 2; q < (unit ? 2 + NB1 : 2); ++q) {
+      const int vo = (kin || k0 + blc[q] * 8 < K) ? boff[q] : BUF_OOB;
+      blds16(rsB, vo, __builtin_amdgcn_readfirstlane(k0 * 2), slot + AIMG + bbase[q] * 128);
+    }
+  };
+
+  f32x4 acc[8][NJ];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: B0, B1, A0, A1 of iteration 0, then B0, B1 of iteration 1 (total >= nk >= 2)
+  b_advance();
+  issue_b(0, smem); issue_b(1, smem);
+  a_advance();
+  issue_a(0, smem); issue_a(1, smem);
+  b_advance();
+  issue_b(0, smem + SLOT); issue_b(1, smem + SLOT);
+  vm_wait<4 + NB1>();      // A0, B of iteration 0
+  __builtin_amdgcn_s_barrier();
+  if (wr == 1) __builtin_amdgcn_s_barrier();   // stagger: waves 4-7 half a phase behind
+  __builtin_amdgcn_sched_barrier(0);
+
+  int t = 0, kt = 0;          // tile ordinal / k-tile of iteration g
+  bf16x8 af[4], bfr[2][NJ];
+  for (int g = 0; g < total; ++g) {
+    const bool more1 = g + 1 < total, more2 = g + 2 < total;
+    const bool first = kt == 0 && g > 0;        // previous iteration ended a tile (stores)
+    const bool last = kt == nk - 1;
+    char* cur = smem + (g & 1) * SLOT;
+    char* nxt = smem + ((g + 1) & 1) * SLOT;
+    // the 4 phases as compile-time instances (a run-time phase index would put acc in scratch)
+    auto phase = [&](auto PH) {
+      constexpr int ph = decltype(PH)::value;
+      constexpr int mq = ph >> 1, kh = ph & 1;
+      // ---- memory section ----
+      if (ph == 0) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) {
+            const int r = wc * WN + j * 16 + li;
+            bfr[h][j] = *(const bf16x8*)(cur + AIMG + r * 128 + (((h * 4 + lg) ^ ps_sw(r)) << 4));
+          }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = wr * 128 + mq * 64 + i * 16 + li;
+        af[i] = *(const bf16x8*)(cur + r * 128 + (((kh * 4 + lg) ^ ps_sw(r)) << 4));
+      }
+      if (ph == 0 && more1) { a_advance(); issue_a(0, nxt); }
+      if (ph == 1 && more1) issue_a(1, nxt);
+      if (ph == 2 && more2) { b_advance(); issue_b(0, cur); }
+      if (ph == 3 && more2) issue_b(1, cur);
+      auto dwait = [&]() {
+        if constexpr (ph == 1) {
+          if (more1) { if (first) vm_wait<6 + NB1 + S>(); else vm_wait<6 + NB1>(); }
+          else { if (first) vm_wait<S>(); else vm_wait<0>(); }
+        } else {
+          if (more2) vm_wait<4 + NB1>();
+          else if (more1) vm_wait<2>();
+          else vm_wait<0>();
+        }
+      };
+      if constexpr ((ph & 1) != 0) { if (wr == 1) dwait(); }
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      // ---- matrix section ----
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          acc[mq * 4 + i][j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[kh][j], af[i], acc[mq * 4 + i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      if constexpr ((ph & 1) != 0) { if (wr == 0) dwait(); }
+      if (ph == 3 && last && !(p.g4_flags & 32)) {   // flag 32: timing only, no epilogue
+        // ---- tile epilogue, straight from the accumulators ----
+        if (!(p.g4_flags & 64)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int tile = c0 + local + t * nbx;
+        const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
+        const int mb = tm * 256 + wr * 128, nb = tn * BN + wc * WN;
+        f32x4 bv[NJ];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int n = nb + 16 * j + 4 * lg;
+          bv[j] = (p.bias && n < p.nvalid) ? *(const f32x4*)(p.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        float rs[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int m = mb + 16 * i + li;
+          rs[i] = ((p.row_scale && m < p.mvalid) ? p.row_scale[m] : 1.f) *
+                  ((p.row_scale_post && m < p.mvalid) ? p.row_scale_post[m] : 1.f);
+        }
+        // compact, branch-free body (ReLU as a max against 0 or -inf): the epilogue runs once
+        // per tile, so its code is fetched cold every time -- keep it small
+        const float lo = p.relu ? 0.f : -INFINITY;
+        const bool c32 = p.c_fp32, nost = p.g4_flags & 16;
+        const bool odd = lg & 1;
+        auto fin = [&](int i, int j) {   // epilogue values of fragment (i, j), acc cleared
+          f32x4 v = acc[i][j] + bv[j];
+          v[0] = fmaxf(v[0], lo) * rs[i]; v[1] = fmaxf(v[1], lo) * rs[i];
+          v[2] = fmaxf(v[2], lo) * rs[i]; v[3] = fmaxf(v[3], lo) * rs[i];
+          acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+          return v;
+        };
+        auto pack = [](f32x4 v) {
+          return u32x2{(unsigned)__builtin_bit_cast(unsigned short, (bf16)v[0]) |
+                           ((unsigned)__builtin_bit_cast(unsigned short, (bf16)v[1]) << 16),
+                       (unsigned)__builtin_bit_cast(unsigned short, (bf16)v[2]) |
+                           ((unsigned)__builtin_bit_cast(unsigned short, (bf16)v[3]) << 16)};
+        };
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int m = mb + 16 * i + li;
+          const bool rowok = m < p.mvalid;
+          if (c32) {   // a lane's 4 consecutive fp32 columns: one 16-byte store per fragment
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+              const f32x4 v = fin(i, j);
+              const int n = nb + 16 * j + 4 * lg;
+              const bool ok = rowok && n < p.nvalid && !nost;
+              llvm_raw_buffer_store_v4i32(__builtin_bit_cast(i32x4, v), rsC,
+                                          ok ? (int)(((long)m * p.ldc + n) * 4) : BUF_OOB, 0, 0);
+            }
+            continue;
+          }
+          // bf16: lanes l and l ^ 16 trade halves of a fragment pair so each holds 8
+          // consecutive columns -> 16-byte stores (the store path, not HBM, bounds this part)
+#pragma unroll
+          for (int j = 0; j + 1 < NJ; j += 2) {
+            const u32x2 a = pack(fin(i, j)), b = pack(fin(i, j + 1));
+            const unsigned r0 = (unsigned)__shfl_xor((int)(odd ? a[0] : b[0]), 16, 64);
+            const unsigned r1 = (unsigned)__shfl_xor((int)(odd ? a[1] : b[1]), 16, 64);
+            const u32x4 o = odd ? u32x4{r0, r1, b[0], b[1]} : u32x4{a[0], a[1], r0, r1};
+            const int n0 = nb + 16 * (j + (odd ? 1 : 0)) + 4 * (lg - (odd ? 1 : 0));
+            if (nost) {
+            } else if (!rowok || n0 + 8 <= p.nvalid || n0 >= p.nvalid) {
+              const bool ok = rowok && n0 < p.nvalid;
+              llvm_raw_buffer_store_v4i32(__builtin_bit_cast(i32x4, o), rsC,
+                                          ok ? (int)(((long)m * p.ldc + n0) * 2) : BUF_OOB, 0, 0);
+            } else {   // 4 valid columns at the right edge
+              llvm_raw_buffer_store_v2i32(i32x2{(int)o[0], (int)o[1]}, rsC,
+                                          (int)(((long)m * p.ldc + n0) * 2), 0, 0);
+            }
+          }
+          if constexpr (NJ % 2 == 1) {
+            const u32x2 a = pack(fin(i, NJ - 1));
+            const int n = nb + 16 * (NJ - 1) + 4 * lg;
+            const bool ok = rowok && n < p.nvalid && !nost;
+            llvm_raw_buffer_store_v2i32(i32x2{(int)a[0], (int)a[1]}, rsC,
+                                        ok ? (int)(((long)m * p.ldc + n) * 2) : BUF_OOB, 0, 0);
+          }
+        }
+      }
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    phase(std::integral_constant<int, 0>{});
+    phase(std::integral_constant<int, 1>{});
+    phase(std::integral_constant<int, 2>{});
+    phase(std::integral_constant<int, 3>{});
+    if (++kt == nk) { kt = 0; ++t; }
+  }
+  if (wr == 0) __builtin_amdgcn_s_barrier();   // balance the stagger
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // compile-time A-operand conv variant for the large-tile kernels: 0 plain, 1 / 4 conv with
 // taps aligned to the k-granule, -1 anything else (run-time generic path)
 int conv_variant(const GemmP& q, int granule) {
@@ -1636,6 +1982,41 @@ int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
     const bool pk_fits = (long)p.M * p.lda * 2 < lim && (long)p.N * p.ldb * 2 < lim &&
                          (long)p.mvalid * p.ldc * (p.c_fp32 ? 4 : 2) < lim &&
                          (long)p.mvalid * (p.gate ? p.ldg : p.ldr) * 2 < lim;
+    // persistent 256 x 256 / 256 x 192 kernel: long-K K-major GEMMs without gate / residual
+    // operands (FS2_GEMM_NO_PS=1 restores the per-tile kernels for A/B runs)
+    static const bool no_ps = getenv_flag("FS2_GEMM_NO_PS");
+    // FS2_PS_MODES: bit 0 plain, bit 1 reflect conv (fwd), bit 2 padded-domain conv (dgrad).
+    // Default 5: in the bench step the unsplit decoder conv1 data gradient gains 0.15-0.2 ms,
+    // while the conv1 forward measured 0-0.1 ms slower than gemm256_kernel (A/B runs)
+    static const int ps_modes = [] { const char* v = std::getenv("FS2_PS_MODES"); return v ? std::atoi(v) : 5; }();
+    const int cm_ps = p.conv_mode == 0 ? 0
+                      : ((p.conv_mode == 1 || p.conv_mode == 4) && p.conv_dil == 1 && p.conv_c % 64 == 0
+                             ? p.conv_mode : -1);
+    const bool ps_on = cm_ps >= 0 && (ps_modes >> (cm_ps == 0 ? 0 : (cm_ps == 1 ? 1 : 2))) & 1;
+    if (!no_ps && ak && bk && ps_on && batch == 1 && p.split_k <= 1 && p.vec_ok &&
+        !p.accumulate && !p.gate && !p.residual && p.relu <= 1 && p.K >= 2048 && p.N >= 128 && pk_fits) {
+      GemmP q = p;
+      static const int psf = [] { const char* v = std::getenv("FS2_PS_FLAGS"); return v ? std::atoi(v) : 0; }();
+      q.g4_flags = psf;
+      q.tiles_m = (p.M + 255) / 256;
+      // tile width by rounds x width over the 256 CUs (ties to the wider tile)
+      const int t256 = q.tiles_m * ((p.N + 255) / 256), t192 = q.tiles_m * ((p.N + 191) / 192);
+      const bool w192 = (long)((t192 + 255) / 256) * 192 < (long)((t256 + 255) / 256) * 256;
+      q.tiles_n = w192 ? (p.N + 191) / 192 : (p.N + 255) / 256;
+      const int nt = q.tiles_m * q.tiles_n;
+      const int g = nt < 256 ? (nt + 7) / 8 * 8 : 256;
+      if (w192) {
+        if (cm_ps == 0) hipLaunchKernelGGL((gemm_ps_kernel<0, 48>), dim3(g), dim3(BNT), 0, s, q);
+        else if (cm_ps == 1) hipLaunchKernelGGL((gemm_ps_kernel<1, 48>), dim3(g), dim3(BNT), 0, s, q);
+        else hipLaunchKernelGGL((gemm_ps_kernel<4, 48>), dim3(g), dim3(BNT), 0, s, q);
+      } else {
+        if (cm_ps == 0) hipLaunchKernelGGL((gemm_ps_kernel<0, 64>), dim3(g), dim3(BNT), 0, s, q);
+        else if (cm_ps == 1) hipLaunchKernelGGL((gemm_ps_kernel<1, 64>), dim3(g), dim3(BNT), 0, s, q);
+        else hipLaunchKernelGGL((gemm_ps_kernel<4, 64>), dim3(g), dim3(BNT), 0, s, q);
+      }
+      FS2_CHECK_LAUNCH();
+      return 0;
+    }
     if (!no_pk && ak && bk && p.conv_mode == 0 && batch == 1 && p.split_k <= 1 && p.vec_ok &&
         !p.accumulate && !(p.gate && p.residual) && p.K <= 1536 && pk_fits) {
       GemmP q = p;

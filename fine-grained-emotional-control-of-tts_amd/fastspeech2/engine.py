@@ -46,6 +46,12 @@ def dgrad_split(Mp, C, K, dt, n_cu=256, max_split=8):
     extra plane."""
     if dt != 1:
         return 1
+    if not _NO_PS and _PS_MODES & 4 and K >= 2048 and C >= 128 and C % 4 == 0:
+        # the persistent 256 x 192 / 256 x 256 kernel (gemm_ps_kernel) takes an unsplit data
+        # gradient when its tiles fill most of one round (the decoder: 124 x 2 = 248 tiles)
+        w = 192 if C % 256 and -(-C // 192) * 192 < -(-C // 256) * 256 else 256
+        if -(-Mp // 256) * -(-C // w) >= 200:
+            return 1
     tiles = -(-Mp // 256) * -(-C // 128)
 
     def eff(s):
@@ -59,6 +65,8 @@ def dgrad_split(Mp, C, K, dt, n_cu=256, max_split=8):
 
 
 _NO_SLICES = os.environ.get("FS2_NO_WGRAD_SLICES", "0") not in ("", "0")
+_NO_PS = os.environ.get("FS2_GEMM_NO_PS", "0") not in ("", "0")
+_PS_MODES = int(os.environ.get("FS2_PS_MODES", "5"))
 # large weight gradients (the FFN conv1 weights, 5.3 M floats) as split-K planes + fixed-order
 # sum instead of split-K fp32 atomics: decoder 428 -> 420 us, encoder 128 -> 119 us, and the
 # result no longer depends on atomic ordering.  FS2_NO_WGRAD_BIG_SLICES=1 restores the atomics.

@@ -429,6 +429,32 @@ def test_gemm_big_tile_paths_bf16(cuda, Bn, T):
     assert rel(dW - 0.5, Wr.grad.permute(0, 2, 1)) < 2e-2
 
 
+@pytest.mark.parametrize("M,N,K,c32", [(1000, 1536, 2048, 0), (31264, 1536, 3456, 0),
+                                        (700, 384, 4096, 1), (300, 200, 2056, 1)])
+def test_gemm_persistent_long_k(cuda, M, N, K, c32):
+    """Long-K K-major GEMMs take the persistent 256 x 256 / 256 x 192 kernel (gemm_ps_kernel):
+    both tile widths, partial row / column tiles, a partial last K-tile (K = 2056), bf16 and
+    fp32 outputs, the bias + ReLU + row-scale epilogue; fp32 reference on the same bf16 values."""
+    from fastspeech2 import ops
+    torch.manual_seed(M + N)
+    A = torch.randn(M, K, device=cuda).to(torch.bfloat16)
+    W = (torch.randn(N, K, device=cuda) * 0.05).to(torch.bfloat16)
+    bias = torch.randn(N, device=cuda)
+    rs = (torch.rand(M, device=cuda) > 0.2).float()
+    rs2 = torch.rand(M, device=cuda) + 0.5
+    ref = torch.relu(A.float() @ W.float().t() + bias) * rs[:, None] * rs2[:, None]
+    C = torch.full((M, N), float("nan"), device=cuda, dtype=torch.float32 if c32 else torch.bfloat16)
+    ops.gemm(M, N, K, A, K, W, K, C, N, dt=1, c_fp32=c32, bias=bias, relu=1, row_scale=rs,
+             row_scale_post=rs2)
+    assert torch.isfinite(C.float()).all()
+    assert rel(C, ref) < 1e-2
+    # plain (no epilogue operands), output written with a row pitch > N
+    C2 = torch.zeros(M, N + 8, device=cuda, dtype=torch.bfloat16)
+    ops.gemm(M, N, K, A, K, W, K, C2, N + 8, dt=1)
+    assert rel(C2[:, :N], A.float() @ W.float().t()) < 1e-2
+    assert (C2[:, N:] == 0).all()
+
+
 @pytest.mark.parametrize("dt,code,tol", DT)
 @pytest.mark.parametrize("M,N,ldx", [(31264, 1536, 1536), (6400, 1152, 1152 * 3), (777, 90, 96)])
 def test_colsum_bias_gradient(cuda, dt, code, tol, M, N, ldx):
