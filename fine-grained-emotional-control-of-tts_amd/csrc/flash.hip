@@ -58,6 +58,11 @@ struct AttnP {
 
 __device__ __forceinline__ bf16x8 ld_frag(const bf16* g) { return *(const bf16x8*)g; }
 
+// 2^x as the bare v_exp_f32 (exp2f adds a denormal range fix-up and, under a select, a branch
+// per element; softmax probabilities below 2^-126 are zero either way).  Every kernel of this
+// file uses it, so forward and backward recompute identical probabilities.
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 // row-major fragment: 8 consecutive features (chunk) of one row
 __device__ __forceinline__ bf16x8 lds_row_frag(const char* t, int rowbytes, int row, int chunk) {
   return *(const bf16x8*)(t + row * rowbytes + ((chunk ^ (row & 7)) << 4));
@@ -168,8 +173,9 @@ __device__ __forceinline__ int build_kvalid(uint8_t* kval, int* kend_s, const At
   if (threadIdx.x == 0) *kend_s = 0;
   __syncthreads();
   int last = 0;
-  for (int j = threadIdx.x; j < p.T; j += blockDim.x) {
-    const uint8_t v = !(k1[j] | k2[j]);
+  const int tpad = (p.T + 63) & ~63;   // bytes past T read as masked (word reads of 4 keys)
+  for (int j = threadIdx.x; j < tpad; j += blockDim.x) {
+    const uint8_t v = j < p.T ? !(k1[j] | k2[j]) : 0;
     kval[j] = v;
     if (v) last = j + 1;
   }
@@ -264,17 +270,18 @@ __global__ void __launch_bounds__(W8 * 64 / QG, 1) attn_fwd_kernel(AttnP p) {
       float v[4][4];
       float mt = -INFINITY;
 #pragma unroll
-      for (int kt = 0; kt < 4; ++kt)
+      for (int kt = 0; kt < 4; ++kt) {
+        const uint32_t kw = *(const uint32_t*)(kval + k0 + kt * 16 + 4 * g);   // keys 4g..4g+3
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int key = k0 + kt * 16 + 4 * g + r;
-          const bool ok = key < p.T && kval[key];
+          const bool ok = (kw >> (8 * r)) & 1u;
           v[kt][r] = ok ? sacc[kt][qg][r] * p.scale_log2 : -INFINITY;
           mt = fmaxf(mt, v[kt][r]);
         }
+      }
       mt = xg_max(mt);
       const float mnew = fmaxf(mrow[qg], mt);
-      const float alpha = mnew == -INFINITY ? 1.f : exp2f(mrow[qg] - mnew);
+      const float alpha = mnew == -INFINITY ? 1.f : fexp2(mrow[qg] - mnew);
       mrow[qg] = mnew;
       float ls = 0.f;
       float pd[4][4];
@@ -283,7 +290,7 @@ __global__ void __launch_bounds__(W8 * 64 / QG, 1) attn_fwd_kernel(AttnP p) {
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float e = v[kt][r] == -INFINITY ? 0.f : exp2f(v[kt][r] - mnew);
+          const float e = v[kt][r] == -INFINITY ? 0.f : fexp2(v[kt][r] - mnew);
           ls += e;
           pd[kt][r] = e;
         }
@@ -299,8 +306,10 @@ __global__ void __launch_bounds__(W8 * 64 / QG, 1) attn_fwd_kernel(AttnP p) {
           }
       }
       lrow[qg] = lrow[qg] * alpha + ls;
+      if (__any(alpha != 1.f)) {   // once the row maxima settle most tiles skip the rescale
 #pragma unroll
-      for (int d = 0; d < ND; ++d) oacc[d][qg] *= alpha;
+        for (int d = 0; d < ND; ++d) oacc[d][qg] *= alpha;
+      }
       pf[qg][0] = pack8(pd[0], pd[1]);
       pf[qg][1] = pack8(pd[2], pd[3]);
     }
@@ -442,21 +451,23 @@ __global__ void __launch_bounds__(W8 * 64 / QG, 1) attn_bwd_dq_kernel(AttnP p) {
       float ds[4][4];
       const uint64_t rowi = ((uint64_t)z * p.T + qi[qg]) * T2;
 #pragma unroll
-      for (int kt = 0; kt < 4; ++kt)
+      for (int kt = 0; kt < 4; ++kt) {
+        const uint32_t kw = *(const uint32_t*)(kval + k0 + kt * 16 + 4 * g);   // keys 4g..4g+3
 #pragma unroll
         for (int r = 0; r < 4; r += 2) {
           const int key = k0 + kt * 16 + 4 * g + r;
           const uint32_t h = p.p_drop > 0.f ? fs2_hash_pair(dkey, (rowi + key) >> 1) : 0u;
 #pragma unroll
           for (int e = 0; e < 2; ++e) {
-            const bool ok = key + e < p.T && kval[key + e];
-            const float pr = ok ? exp2f(sacc[kt][qg][r + e] * p.scale_log2 - lse[qg]) : 0.f;
+            const bool ok = (kw >> (8 * (r + e))) & 1u;
+            const float pr = ok ? fexp2(sacc[kt][qg][r + e] * p.scale_log2 - lse[qg]) : 0.f;
             float dp = pacc[kt][qg][r + e];
             if (p.p_drop > 0.f)
               dp = fs2_keep_pair_bit(h, rowi + key + e, p.thr16) ? dp * p.inv_keep : 0.f;
             ds[kt][r + e] = pr * (dp - dsum[qg]);
           }
         }
+      }
       sf[qg][0] = pack8(ds[0], ds[1]);
       sf[qg][1] = pack8(ds[2], ds[3]);
     }
@@ -607,22 +618,46 @@ __global__ void __launch_bounds__(W8 * 64, 1) attn_bwd_dkv_kernel(AttnP p) {
       }
     float pdv[4][4], dsv[4][4];
 #pragma unroll
-    for (int qt = 0; qt < 4; ++qt)
+    for (int qt = 0; qt < 4; ++qt) {
+      const f32x4 l4 = *(const f32x4*)(ls_s + qt * 16 + 4 * g);   // rows 4g..4g+3 of this qt
+      const f32x4 d4 = *(const f32x4*)(ds_s + qt * 16 + 4 * g);
+      // dropout: keys 2m and 2m+1 (lanes 2m, 2m+1) share one pair hash per query row; the even
+      // lane hashes rows r = 0, 1 and the odd lane rows 2, 3, then they swap (DPP quad_perm)
+      uint32_t hx[4];
+      if (p.p_drop > 0.f) {
+        const int odd = lane & 1;
+        uint32_t mine[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int q = q0 + qt * 16 + 4 * g + 2 * odd + e;
+          mine[e] = fs2_hash_pair(dkey, (((uint64_t)z * p.T + q) * T2 + key) >> 1);
+        }
+        uint32_t other[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+          other[e] = (uint32_t)__builtin_amdgcn_mov_dpp((int)mine[e], 0xB1, 0xF, 0xF, false);
+        hx[0] = odd ? other[0] : mine[0];
+        hx[1] = odd ? other[1] : mine[1];
+        hx[2] = odd ? mine[0] : other[0];
+        hx[3] = odd ? mine[1] : other[1];
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int ql = qt * 16 + 4 * g + r, q = q0 + ql;
         const bool ok = kok && q < p.T;
-        const float pr = ok ? exp2f(sacc[qt][r] * p.scale_log2 - ls_s[ql]) : 0.f;
+        float pr = fexp2(sacc[qt][r] * p.scale_log2 - l4[r]);
+        pr = ok ? pr : 0.f;
         float dp = pacc[qt][r];
         float pd = pr;
         if (p.p_drop > 0.f) {
-          const bool keep = fs2_keep_fast(dkey, ((uint64_t)z * p.T + q) * T2 + key, p.thr16);
+          const bool keep = fs2_keep_pair_bit(hx[r], (uint64_t)key, p.thr16);
           dp = keep ? dp * p.inv_keep : 0.f;
           pd = keep ? pr * p.inv_keep : 0.f;
         }
         pdv[qt][r] = pd;
-        dsv[qt][r] = pr * (dp - ds_s[ql]);
+        dsv[qt][r] = pr * (dp - d4[r]);
       }
+    }
     // dV += Pd^T dO, dK += dS^T Q : A = (key x query) from registers, B = tile^T via tr reads
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -819,14 +854,14 @@ __global__ void __launch_bounds__(NW * 64) attn_fwd32_kernel(AttnP p) {
       }
     mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
     const float mnew = fmaxf(mrow, mt);
-    const float alpha = mnew == -INFINITY ? 1.f : exp2f(mrow - mnew);
+    const float alpha = mnew == -INFINITY ? 1.f : fexp2(mrow - mnew);
     mrow = mnew;
     float ls = 0.f;
 #pragma unroll
     for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float e = v[kb][r] == -INFINITY ? 0.f : exp2f(v[kb][r] - mnew);
+        const float e = v[kb][r] == -INFINITY ? 0.f : fexp2(v[kb][r] - mnew);
         ls += e;
         v[kb][r] = e;
       }
@@ -973,7 +1008,7 @@ __global__ void __launch_bounds__(NW * 64, 1) attn_dq32_kernel(AttnP p) {
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
           const bool ok = key + e < p.T && kval[key + e];
-          const float pr = ok ? exp2f(sacc[r + e] * p.scale_log2 - lse) : 0.f;
+          const float pr = ok ? fexp2(sacc[r + e] * p.scale_log2 - lse) : 0.f;
           float dp = pacc[r + e];
           if (p.p_drop > 0.f) dp = fs2_keep_pair_bit(hs, rowi + key + e, p.thr16) ? dp * p.inv_keep : 0.f;
           ds[r + e] = pr * (dp - dsum);
@@ -1091,7 +1126,7 @@ __global__ void __launch_bounds__(NW * 64, 1) attn_dkv32_kernel(AttnP p) {
         for (int r = 0; r < 4; ++r) {
           const int q = q0 + ql + r;
           const bool ok = kok && q < p.T;
-          const float pr = ok ? exp2f(sacc[4 * i + r] * p.scale_log2 - l4[r]) : 0.f;
+          const float pr = ok ? fexp2(sacc[4 * i + r] * p.scale_log2 - l4[r]) : 0.f;
           float dp = pacc[4 * i + r];
           float pdr = pr;
           if (p.p_drop > 0.f) {
@@ -1196,6 +1231,11 @@ void launch_fwd(const AttnP& p, hipStream_t s) {
     dim3 grid((p.T + 63) / 64, p.B * p.H);
     if (attn_qg_fwd(DH) == 2) hipLaunchKernelGGL((attn_fwd_kernel<DH, 2, 4>), grid, dim3(128), 0, s, p);
     else hipLaunchKernelGGL((attn_fwd_kernel<DH, 1, 4>), grid, dim3(256), 0, s, p);
+    return;
+  }
+  static const int fcfg = [] { const char* v = std::getenv("FS2_ATTN_FWD"); return v ? std::atoi(v) : 0; }();
+  if (fcfg == 1) {   // 256-query blocks: 8 waves x 32 queries
+    hipLaunchKernelGGL((attn_fwd_kernel<DH, 2, 16>), dim3((p.T + 255) / 256, p.B * p.H), dim3(512), 0, s, p);
     return;
   }
   dim3 grid((p.T + 127) / 128, p.B * p.H);
