@@ -81,12 +81,20 @@ __device__ __forceinline__ u32x4 add_f32x4(u32x4 a, u32x4 b) {
 // epilogue activation: 1 ReLU (SB pos_ffn, model.py:241-267), 2 GELU with erf
 // (nn.GELU() of the IntensityExtractor FFN, rank_model/model.py:30,42), 3 leaky ReLU 0.1 and
 // 4 tanh (HiFi-GAN generator: LRELU_SLOPE, output tanh)
-__device__ __forceinline__ float epi_act(float v, int act) {
-  if (act == 1) return fmaxf(v, 0.f);
+// GELU / leaky ReLU / tanh (the intensity extractor and the vocoder): out of line, so the
+// unrolled epilogues keep ONE compact body for the train step's none / ReLU.  Inlined, the
+// five-way select put an erf and a tanh expansion behind a branch on every output element and
+// grew the large-tile kernels to 40-80 KiB of code -- an epilogue fetched cold from the
+// instruction cache once per tile.
+__device__ __attribute__((noinline)) float epi_act_rare(float v, int act) {
   if (act == 2) return 0.5f * v * (1.f + erff(v * 0.70710678118654752f));
   if (act == 3) return v >= 0.f ? v : 0.1f * v;
   if (act == 4) return tanhf(v);
   return v;
+}
+__device__ __forceinline__ float epi_act(float v, int act) {
+  if (act > 1) return epi_act_rare(v, act);
+  return fmaxf(v, act ? 0.f : -INFINITY);
 }
 
 template <typename T>

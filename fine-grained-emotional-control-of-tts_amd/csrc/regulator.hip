@@ -128,6 +128,18 @@ __global__ void mask_rows_kernel(T* X, long ldx, const float* keep, int M, int D
   *p = from_f<T>(to_f(*p) * keep[m]);
 }
 
+// X = (X + Y + Z) * keep[row], summed in fp32 and rounded once (the aux-stream join of the
+// three predictor input gradients)
+template <typename T>
+__global__ void add3_mask_rows_kernel(T* X, const T* Y, const T* Z, long ld, const float* keep,
+                                      int M, int D) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)M * D) return;
+  const long m = i / D;
+  const long o = m * ld + (i - m * D);
+  X[o] = from_f<T>(((to_f(X[o]) + to_f(Y[o])) + to_f(Z[o])) * keep[m]);
+}
+
 // ---------------------------------------------------------------- predictor head
 template <typename T>
 __global__ void __launch_bounds__(256) rowdot_fwd_kernel(const T* u, long ldu, const float* w,
@@ -373,6 +385,8 @@ inline unsigned nblk(long n, int bs = 256) { return (unsigned)((n + bs - 1) / bs
 
 }  // namespace
 
+// every entry point dispatching through DISPATCH_T reports its own launch status (the macro
+// ends in FS2_CHECK_LAUNCH), as do the entry points that launch directly
 #define DISPATCH_T(dtype, KERNEL_CALL_BF16, KERNEL_CALL_F32) \
   do {                                                     \
     if ((dtype) == FS2_BF16) { KERNEL_CALL_BF16; }          \
@@ -463,6 +477,18 @@ extern "C" int fs2_mask_rows(void* X, int64_t ldx, const float* keep, int M, int
   DISPATCH_T(dtype,
     hipLaunchKernelGGL(mask_rows_kernel<bf16>, dim3(nblk(n)), dim3(256), 0, s, (bf16*)X, ldx, keep, M, D),
     hipLaunchKernelGGL(mask_rows_kernel<float>, dim3(nblk(n)), dim3(256), 0, s, (float*)X, ldx, keep, M, D));
+  return 0;
+}
+
+extern "C" int fs2_add3_mask_rows(void* X, const void* Y, const void* Z, int64_t ld,
+                                  const float* keep, int M, int D, int dtype, void* stream) {
+  const long n = (long)M * D;
+  if (n == 0) return 0;
+  if (!X || !Y || !Z || !keep) return FS2_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  DISPATCH_T(dtype,
+    hipLaunchKernelGGL(add3_mask_rows_kernel<bf16>, dim3(nblk(n)), dim3(256), 0, s, (bf16*)X, (const bf16*)Y, (const bf16*)Z, ld, keep, M, D),
+    hipLaunchKernelGGL(add3_mask_rows_kernel<float>, dim3(nblk(n)), dim3(256), 0, s, (float*)X, (const float*)Y, (const float*)Z, ld, keep, M, D));
   return 0;
 }
 

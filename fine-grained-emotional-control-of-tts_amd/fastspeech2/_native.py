@@ -108,6 +108,7 @@ SIGNATURES = {
     "fs2_concat_fwd": (I, [P, P, P, P, I, I, I, I, P, I, I, P]),
     "fs2_concat_bwd_spk": (I, [P, I, P, I, I, I, I, P, I, P, P]),
     "fs2_mask_rows": (I, [P, I64, P, I, I, I, P]),
+    "fs2_add3_mask_rows": (I, [P, P, P, I64, P, I, I, I, P]),
     "fs2_rowdot_fwd": (I, [P, I64, P, P, Fl, I, I, P, I, P]),
     "fs2_rowdot_bwd": (I, [P, P, I64, P, Fl, I, I, P, P, P, I, P, P]),
     "fs2_avg_over_durations": (I, [P, I, P, I, I, P, P, P]),

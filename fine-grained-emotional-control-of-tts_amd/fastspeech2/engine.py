@@ -904,11 +904,10 @@ class FS2Engine:
                         G["pitchEmbed.conv.bias"], dt=self.dt, ws=self.ws(128 * (kwp + 1) * D))
         if aux_h is not None:
             self._aux_join(aux_h[1], dZp, dZd)
-            # dZ = keep * (dZd + dZp + dZ2), as the sequential chain's residual epilogues
+            # dZ = keep * (dZ2 + dZp + dZd), as the sequential chain's residual epilogues, summed
+            # in fp32 with one rounding
             dZ = dZ2
-            ops.add(dZ, dZp, Mp * D, 1.0, dt=self.dt)
-            ops.add(dZ, dZd, Mp * D, 1.0, dt=self.dt)
-            ops.mask_rows(dZ, D, keep_p, Mp, D, dt=self.dt)
+            ops.add3_mask_rows(dZ, dZp, dZd, D, keep_p, Mp, D, dt=self.dt)
         else:
             dZa = self._pred_bwd(d_pitch, ctx["pctx"], keep_p, B, Tp, "pitchPred", ctx["p_var"],
                                  seed, residual=dZ2)

@@ -180,6 +180,12 @@ def mask_rows(X, ldx, keep, M, D, *, dt):
     _chk(N.lib().fs2_mask_rows(_p(X), ldx, _p(keep), M, D, dt, _s()), "fs2_mask_rows")
 
 
+def add3_mask_rows(X, Y, Z, ld, keep, M, D, *, dt):
+    """X = (X + Y + Z) * keep[row], fp32 sum, one rounding."""
+    _chk(N.lib().fs2_add3_mask_rows(_p(X), _p(Y), _p(Z), ld, _p(keep), M, D, dt, _s()),
+         "fs2_add3_mask_rows")
+
+
 def rowdot_fwd(u, ldu, w, b, scale, M, D, y, *, dt):
     _chk(N.lib().fs2_rowdot_fwd(_p(u), ldu, _p(w), _p(b), scale, M, D, _p(y), dt, _s()),
          "fs2_rowdot_fwd")

@@ -193,6 +193,11 @@ int fs2_concat_bwd_spk(const void* dcat, int ldc, const int64_t* spk, int B, int
 
 /* rows: X[m][:] *= keep[m]   (in place)                                                   */
 int fs2_mask_rows(void* X, int64_t ldx, const float* keep, int M, int D, int dtype, void* stream);
+/* X = (X + Y + Z) * keep[row] over M x D (row pitch ld for all three), summed in fp32 and
+ * rounded once: the join of the predictor input gradients when the duration / pitch predictor
+ * backward runs on its own stream (model.py:365-403 variance adaptor backward). */
+int fs2_add3_mask_rows(void* X, const void* Y, const void* Z, int64_t ld, const float* keep,
+                       int M, int D, int dtype, void* stream);
 
 /* predictor head: y[m] = (dot(u[m], w) + b) * scale (SB DurationPredictor.linear, App. A.7) */
 int fs2_rowdot_fwd(const void* u, int64_t ldu, const float* w, const float* b, float scale, int M,

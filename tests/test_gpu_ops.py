@@ -429,6 +429,21 @@ def test_gemm_big_tile_paths_bf16(cuda, Bn, T):
     assert rel(dW - 0.5, Wr.grad.permute(0, 2, 1)) < 2e-2
 
 
+@pytest.mark.parametrize("dt,code", [(torch.float32, 0), (torch.bfloat16, 1)])
+def test_add3_mask_rows(cuda, dt, code):
+    """fs2_add3_mask_rows: X = (X + Y + Z) * keep[row] in fp32 with one rounding, row pitch > D."""
+    from fastspeech2 import ops
+    torch.manual_seed(5)
+    M, D, ld = 301, 384, 392
+    X, Y, Z = (torch.randn(M, ld, device=cuda).to(dt) for _ in range(3))
+    keep = (torch.rand(M, device=cuda) > 0.3).float()
+    ref = ((X.float() + Y.float()) + Z.float()) * keep[:, None]
+    X0 = X.clone()
+    ops.add3_mask_rows(X, Y, Z, ld, keep, M, D, dt=code)
+    assert torch.equal(X[:, :D], ref[:, :D].to(dt))
+    assert torch.equal(X[:, D:], X0[:, D:])
+
+
 @pytest.mark.parametrize("M,N,K,c32", [(1000, 1536, 2048, 0), (31264, 1536, 3456, 0),
                                         (700, 384, 4096, 1), (300, 200, 2056, 1)])
 def test_gemm_persistent_long_k(cuda, M, N, K, c32):
