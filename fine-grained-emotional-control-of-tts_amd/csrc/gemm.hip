@@ -1433,7 +1433,9 @@ __device__ void llvm_raw_buffer_store_v4i32(i32x4 data, i32x4 rsrc, int voffset,
 __device__ i32x2 llvm_raw_buffer_load_v2i32(i32x4 rsrc, int voffset, int soffset,
                                             int aux) __asm("llvm.amdgcn.raw.buffer.load.v2i32");
 
-constexpr int PK_STORES = 16;   // epilogue store instructions per wave per tile (4 x 4 blocks)
+// epilogue store instructions per wave per tile: fp32 one 16-byte store per 16x16 block (16);
+// bf16 one 16-byte store per block PAIR (8: lanes l and l ^ 16 trade halves)
+constexpr int PK_STORES32 = 16, PK_STORES16 = 8;
 
 template <int N>
 __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
@@ -1513,8 +1515,15 @@ __global__ void __launch_bounds__(BNT) gemm_pk_kernel(GemmP p) {
     const bool more = it + 1 < total;
     // stage it landed: younger than its 6 pieces are those of it + 1 and, after a tile's
     // epilogue, that epilogue's 16 stores
-    if (more) { if (prev_last) vm_wait<6 + PK_STORES>(); else vm_wait<6>(); }
-    else { if (prev_last) vm_wait<PK_STORES>(); else vm_wait<0>(); }
+    if (more) {
+      if (!prev_last) vm_wait<6>();
+      else if (p.c_fp32) vm_wait<6 + PK_STORES32>();
+      else vm_wait<6 + PK_STORES16>();
+    } else {
+      if (!prev_last) vm_wait<0>();
+      else if (p.c_fp32) vm_wait<PK_STORES32>();
+      else vm_wait<PK_STORES16>();
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
@@ -1575,38 +1584,61 @@ __global__ void __launch_bounds__(BNT) gemm_pk_kernel(GemmP p) {
       if (nk == 1) {   // operands issued this iteration: retire them, keep the prefetch in flight
         if (pre) vm_wait<6>(); else vm_wait<0>();
       }
+      const bool nost = p.g4_flags & 16;   // timing experiments only: no stores (wrong results)
+      const bool odd = lg & 1;
+      auto fin = [&](int i, int j) {         // epilogue values of block (i, j); acc cleared
+        f32x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float x = epi_act(acc[i][j][e] + bv[j][e], p.relu);
+          const unsigned w = (unsigned)ev[i][j][e >> 1];
+          const float ef = __builtin_bit_cast(float, (e & 1) ? (w & 0xffff0000u) : (w << 16));
+          if (p.gate) x = ef > 0.f ? x : 0.f;
+          x *= rs[i];
+          if (p.residual) x += ef;
+          v[e] = x * rs2[i];
+        }
+        acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        return v;
+      };
+      auto pack = [](f32x4 v) {
+        return u32x2{(unsigned)__builtin_bit_cast(unsigned short, (bf16)v[0]) |
+                         ((unsigned)__builtin_bit_cast(unsigned short, (bf16)v[1]) << 16),
+                     (unsigned)__builtin_bit_cast(unsigned short, (bf16)v[2]) |
+                         ((unsigned)__builtin_bit_cast(unsigned short, (bf16)v[3]) << 16)};
+      };
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int m = mb + 16 * i + li;
+        const bool rowok = m < p.mvalid;
+        if (p.c_fp32) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int n = nb + 16 * j + 4 * lg;
-          const bool ok = m < p.mvalid && n < p.nvalid;
-          float v[4];
+          for (int j = 0; j < 4; ++j) {
+            const int n = nb + 16 * j + 4 * lg;
+            const f32x4 v = fin(i, j);
+            if (nost) continue;
+            llvm_raw_buffer_store_v4i32(__builtin_bit_cast(i32x4, v), rsC,
+                                        rowok && n < p.nvalid ? (int)(((long)m * p.ldc + n) * 4) : BUF_OOB, 0, 0);
+          }
+          continue;
+        }
+        // bf16: lanes l and l ^ 16 trade halves of a block pair -> 8 consecutive columns each,
+        // one 16-byte store (the CU's store path, not HBM, bounds the 8-byte form)
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            float x = epi_act(acc[i][j][e] + bv[j][e], p.relu);
-            const unsigned w = (unsigned)ev[i][j][e >> 1];
-            const float ef = __builtin_bit_cast(float, (e & 1) ? (w & 0xffff0000u) : (w << 16));
-            if (p.gate) x = ef > 0.f ? x : 0.f;
-            x *= rs[i];
-            if (p.residual) x += ef;
-            v[e] = x * rs2[i];
+        for (int j = 0; j < 4; j += 2) {
+          const u32x2 a = pack(fin(i, j)), b = pack(fin(i, j + 1));
+          const unsigned r0 = (unsigned)__shfl_xor((int)(odd ? a[0] : b[0]), 16, 64);
+          const unsigned r1 = (unsigned)__shfl_xor((int)(odd ? a[1] : b[1]), 16, 64);
+          const u32x4 o = odd ? u32x4{r0, r1, b[0], b[1]} : u32x4{a[0], a[1], r0, r1};
+          const int n0 = nb + 16 * (j + (odd ? 1 : 0)) + 4 * (lg - (odd ? 1 : 0));
+          if (nost) continue;
+          if (!rowok || n0 + 8 <= p.nvalid || n0 >= p.nvalid) {
+            llvm_raw_buffer_store_v4i32(__builtin_bit_cast(i32x4, o), rsC,
+                                        rowok && n0 < p.nvalid ? (int)(((long)m * p.ldc + n0) * 2) : BUF_OOB, 0, 0);
+          } else {   // 4 valid columns at the right edge: still ONE store (the count is exact)
+            llvm_raw_buffer_store_v2i32(i32x2{(int)o[0], (int)o[1]}, rsC,
+                                        (int)(((long)m * p.ldc + n0) * 2), 0, 0);
           }
-          if (p.g4_flags & 16) {   // timing experiments only: no stores (wrong results)
-          } else if (p.c_fp32) {
-            const i32x4 d = {__builtin_bit_cast(int, v[0]), __builtin_bit_cast(int, v[1]),
-                             __builtin_bit_cast(int, v[2]), __builtin_bit_cast(int, v[3])};
-            llvm_raw_buffer_store_v4i32(d, rsC, ok ? (int)(((long)m * p.ldc + n) * 4) : BUF_OOB, 0, 0);
-          } else {
-            i32x2 d;
-            d[0] = (int)((unsigned)__builtin_bit_cast(unsigned short, (bf16)v[0]) |
-                         ((unsigned)__builtin_bit_cast(unsigned short, (bf16)v[1]) << 16));
-            d[1] = (int)((unsigned)__builtin_bit_cast(unsigned short, (bf16)v[2]) |
-                         ((unsigned)__builtin_bit_cast(unsigned short, (bf16)v[3]) << 16));
-            llvm_raw_buffer_store_v2i32(d, rsC, ok ? (int)(((long)m * p.ldc + n) * 2) : BUF_OOB, 0, 0);
-          }
-          acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
       }
     }
