@@ -301,8 +301,9 @@ __global__ void __launch_bounds__(W8 * 64 / QG, 1) attn_fwd_kernel(AttnP p) {
           for (int r = 0; r < 4; r += 2) {
             const uint64_t idx = rowi + k0 + kt * 16 + 4 * g + r;   // even
             const uint32_t h = fs2_hash_pair(dkey, idx >> 1);
-            pd[kt][r] = fs2_keep_pair_bit(h, idx, p.thr16) ? pd[kt][r] * p.inv_keep : 0.f;
-            pd[kt][r + 1] = fs2_keep_pair_bit(h, idx + 1, p.thr16) ? pd[kt][r + 1] * p.inv_keep : 0.f;
+            // the 1 / (1 - p) of the kept probabilities is applied once, to O at the end
+            pd[kt][r] = fs2_keep_pair_bit(h, idx, p.thr16) ? pd[kt][r] : 0.f;
+            pd[kt][r + 1] = fs2_keep_pair_bit(h, idx + 1, p.thr16) ? pd[kt][r + 1] : 0.f;
           }
       }
       lrow[qg] = lrow[qg] * alpha + ls;
@@ -327,7 +328,7 @@ __global__ void __launch_bounds__(W8 * 64 / QG, 1) attn_fwd_kernel(AttnP p) {
 #pragma unroll
   for (int qg = 0; qg < QG; ++qg) {
     const float l = xg_sum(lrow[qg]);
-    const float inv = 1.f / l;
+    const float inv = p.inv_keep / l;
     if (qi[qg] >= p.T) continue;
     if (g == 0) p.lse[(long)z * p.T + qi[qg]] = mrow[qg] + log2f(l);
     bf16* orow = p.out + ((long)b * p.T + qi[qg]) * p.ldout + h * DH;
@@ -652,7 +653,7 @@ __global__ void __launch_bounds__(W8 * 64, 1) attn_bwd_dkv_kernel(AttnP p) {
         if (p.p_drop > 0.f) {
           const bool keep = fs2_keep_pair_bit(hx[r], (uint64_t)key, p.thr16);
           dp = keep ? dp * p.inv_keep : 0.f;
-          pd = keep ? pr * p.inv_keep : 0.f;
+          pd = keep ? pr : 0.f;       // 1 / (1 - p) applied to dV once, at the store
         }
         pdv[qt][r] = pd;
         dsv[qt][r] = pr * (dp - d4[r]);
@@ -683,7 +684,7 @@ __global__ void __launch_bounds__(W8 * 64, 1) attn_bwd_dkv_kernel(AttnP p) {
 #pragma unroll
     for (int d = 0; d < ND; ++d) {
       krow[16 * d + (lane & 15)] = (bf16)(dk[d][r] * p.scale);
-      vrow[16 * d + (lane & 15)] = (bf16)dv[d][r];
+      vrow[16 * d + (lane & 15)] = (bf16)(dv[d][r] * p.inv_keep);
     }
   }
 }

@@ -17,18 +17,19 @@ fi
 timeout -k 10 300 python -u bench.py > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -20 $O/bench.err; exit 1; }
 cat $O/bench.json
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-extractor \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-extractor --no-fp32-leg --no-config2-leg \
   > $O/prof_bench.json 2> $O/prof.err || { echo "rocprof failed"; tail -20 $O/prof.err; exit 1; }
 python $R/tools/rocprof_summary.py stats $O/prof 13 $O/kernel_stats.txt | head -40
 python $R/tools/rocprof_summary.py kernel $O/prof "gemm256_kernel<true, true, 1" 377856 100 | tee $O/roofline_kernel_trace.txt
+python $R/tools/rocprof_summary.py gaps $O/prof adamw_prep_tiles 10 $O/gaps.json | tail -3
 if [ "$3" == "pmc" ]; then
   for C in FETCH_SIZE WRITE_SIZE; do
-    timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d $O/pmc_$C -o run -- python $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extractor \
+    timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d $O/pmc_$C -o run -- python $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extractor --no-fp32-leg --no-config2-leg \
       > $O/pmc_$C.log 2>&1 || { echo "pmc $C failed"; tail -20 $O/pmc_$C.log; exit 1; }
   done
   python $R/tools/rocprof_summary.py traffic $O/pmc_FETCH_SIZE $O/pmc_WRITE_SIZE "gemm256_kernel<true, true, 1" 377856 100 $O/roofline_traffic.json
 fi
 if [ "$4" == "detail" ]; then
-  cd $R && timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-extractor --detail > $O/detail.json 2> $O/detail.txt || { echo "detail failed"; tail -20 $O/detail.txt; exit 1; }
+  cd $R && timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-extractor --no-fp32-leg --no-config2-leg --detail > $O/detail.json 2> $O/detail.txt || { echo "detail failed"; tail -20 $O/detail.txt; exit 1; }
   grep -v amdgpu.ids $O/detail.txt | head -60
 fi
