@@ -99,6 +99,7 @@ class GradBucketer:
 # 1.50 ms graph): the replayed multi-stream graph leaves more gaps between kernels than the
 # eager launches, whose host issue time (8-12 ms/step) is already below the GPU time
 _GRAPH = os.environ.get("FS2_GRAPH", "0") not in ("", "0")
+_PRIO = os.environ.get("FS2_PRIO", "1") not in ("", "0")
 
 
 class _StepGraph:
@@ -160,6 +161,7 @@ class FusedTrainer:
         # DP steps stay eager: their bucketed all-reduces are issued from the backward hooks
         self.use_graph = (self.world == 1 and _GRAPH) if graph is None else bool(graph)
         self._graphs = {}
+        self._prio = None
 
     def _graph_for(self, batch, intensity, mel_len_max):
         key = tuple(tuple(t.shape) for t in batch[:8]) + (tuple(intensity.shape), mel_len_max)
@@ -197,6 +199,32 @@ class FusedTrainer:
 
     def step(self, batch, intensity, mel_len_max=None):
         self.seed += 1
+        prio = self._prio_stream()
+        if prio is None:
+            return self._step(batch, intensity, mel_len_max)
+        # the data-gradient chain is the critical path; the weight-gradient side stream and the
+        # predictor aux stream (normal priority) fill the CUs it leaves idle
+        caller = torch.cuda.current_stream(self.model._flat.device)
+        prio.wait_stream(caller)
+        for t in list(batch[:8]) + [intensity]:
+            if t is not None and t.is_cuda:
+                t.record_stream(prio)
+        with torch.cuda.stream(prio):
+            loss = self._step(batch, intensity, mel_len_max)
+        caller.wait_stream(prio)
+        loss.record_stream(caller)
+        return loss
+
+    def _prio_stream(self):
+        """high-priority stream the step runs on (FS2_PRIO=0 keeps the caller's stream)"""
+        if not _PRIO or self.use_graph or not self.model._flat.is_cuda:
+            return None
+        if self._prio is None:
+            lo, hi = torch.cuda.Stream.priority_range()
+            self._prio = torch.cuda.Stream(self.model._flat.device, priority=hi)
+        return self._prio
+
+    def _step(self, batch, intensity, mel_len_max):
         if self.use_graph:
             mlm = mel_len_max if mel_len_max is not None else batch[3].shape[1]
             loss = self._graph_for(batch, intensity, mlm).replay(batch, intensity, self.seed)

@@ -385,6 +385,27 @@ def test_conv_dgrad_shift_plus_fold(cuda, dt, code, tol, KW, T, split):
     assert rel(dX, ref) < tol
 
 
+@pytest.mark.parametrize("split", [1, 3])
+def test_conv_fold_vector_form_bit_exact(cuda, split):
+    """the 8-channel, 16-byte-access bf16 fold (conv_fold8_kernel) equals the 4-channel form
+    (taken when the output stride is not a multiple of 8) bit for bit, with residual and both
+    row scales, at the decoder's T = 977 / P = 4"""
+    from fastspeech2 import ops
+    torch.manual_seed(11)
+    Bn, T, P, C = 4, 977, 4, 384
+    Mp = Bn * (T + 2 * P)
+    Xpad = torch.randn(split, Mp, C, device=cuda)
+    res = torch.randn(Bn * T, C + 8, device=cuda).to(torch.bfloat16)
+    rs = (torch.rand(Bn * T, device=cuda) > 0.3).float()
+    rs2 = torch.rand(Bn * T, device=cuda)
+    a = torch.empty(Bn * T, C, device=cuda, dtype=torch.bfloat16)
+    b = torch.empty(Bn * T, C + 4, device=cuda, dtype=torch.bfloat16)
+    for out, ldo in ((a, C), (b, C + 4)):
+        ops.conv_fold(Xpad, Bn, T, P, C, out, ldo, dt=1, residual=res, ldr=C + 8, row_scale=rs,
+                      row_scale_post=rs2, nsplit=split, split_stride=Mp * C)
+    assert torch.equal(a, b[:, :C])
+
+
 @pytest.mark.parametrize("Bn,T", [(32, 640), (1, 640), (32, 200), (32, 977)])
 def test_gemm_big_tile_paths_bf16(cuda, Bn, T):
     """BASELINE-sized GEMMs that take the 256x128 LDS-DMA kernel (gemm_big_kernel): implicit
