@@ -830,7 +830,8 @@ extern "C" int fs2_conv_fold(const float* Xpad, int nsplit, int64_t split_stride
     return FS2_EINVAL;
   const dim3 g((unsigned)((n / 4 + 255) / 256)), b(256);
   hipStream_t s = (hipStream_t)stream;
-  const bool v8 = dtype == FS2_BF16 && C % 8 == 0 && a16(out) && ldo % 8 == 0 &&
+  static const bool no8 = [] { const char* v = std::getenv("FS2_FOLD8"); return v && v[0] == '0'; }();
+  const bool v8 = !no8 && dtype == FS2_BF16 && C % 8 == 0 && a16(out) && ldo % 8 == 0 &&
                   (!residual || (a16(residual) && ldr % 8 == 0)) && a16(Xpad) &&
                   (nsplit == 1 || split_stride % 4 == 0) && n / 8 < (1L << 31);
   if (v8) {

@@ -99,7 +99,9 @@ class GradBucketer:
 # 1.50 ms graph): the replayed multi-stream graph leaves more gaps between kernels than the
 # eager launches, whose host issue time (8-12 ms/step) is already below the GPU time
 _GRAPH = os.environ.get("FS2_GRAPH", "0") not in ("", "0")
-_PRIO = os.environ.get("FS2_PRIO", "1") not in ("", "0")
+# opt-in: A/B 20.55-20.61 ms off vs 20.59-20.68 ms on (the persistent GEMMs' blocks are all
+# resident from launch, so queue priority changes little)
+_PRIO = os.environ.get("FS2_PRIO", "0") not in ("", "0")
 
 
 class _StepGraph:
@@ -216,7 +218,7 @@ class FusedTrainer:
         return loss
 
     def _prio_stream(self):
-        """high-priority stream the step runs on (FS2_PRIO=0 keeps the caller's stream)"""
+        """high-priority stream the step runs on (FS2_PRIO=1; default: the caller's stream)"""
         if not _PRIO or self.use_graph or not self.model._flat.is_cuda:
             return None
         if self._prio is None:
