@@ -1459,6 +1459,8 @@ __global__ void __launch_bounds__(BNT) gemm_pk_kernel(GemmP p) {
   const i32x4 rsE = make_rsrc(p.gate ? p.gate : (p.residual ? p.residual : p.C));
   const long lde = p.gate ? p.ldg : p.ldr;
   const bool has_e = p.gate || p.residual;
+  const int e0 = nk - 4;                                   // early epilogue-load iteration
+  const bool early_e = has_e && nk >= 4 && !(p.g4_flags & 32);
 
   // per-lane parts of the DMA addressing (as gemm_big_kernel, plain operands)
   int ar[4], alc[4], br[2], blc[2];
@@ -1516,7 +1518,10 @@ __global__ void __launch_bounds__(BNT) gemm_pk_kernel(GemmP p) {
     // stage it landed: younger than its 6 pieces are those of it + 1 and, after a tile's
     // epilogue, that epilogue's 16 stores
     if (more) {
-      if (!prev_last) vm_wait<6>();
+      // early epilogue loads (issued after iteration e0's prefetch) stay in flight through
+      // the stage waits of iterations e0 + 1 and e0 + 2 (kt >= 1, so never after an epilogue)
+      if (early_e && (kt == e0 + 1 || kt == e0 + 2)) vm_wait<6 + 16>();
+      else if (!prev_last) vm_wait<6>();
       else if (p.c_fp32) vm_wait<6 + PK_STORES32>();
       else vm_wait<6 + PK_STORES16>();
     } else {
@@ -1534,6 +1539,19 @@ __global__ void __launch_bounds__(BNT) gemm_pk_kernel(GemmP p) {
     // epilogue operands one iteration ahead of the epilogue (nk >= 2): issued before this
     // iteration's prefetch, they are retired by the NEXT iteration's stage wait, so the
     // epilogue itself never waits on a load (with nk == 1 they are issued in the same one)
+    auto load_e = [&]() {   // the tile's gate / residual operand: exactly 16 buffer loads
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = mb + 16 * i + li;
+        const bool in = m < p.mvalid;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int n = nb + 16 * j + 4 * lg;
+          const bool ok = in && n < p.nvalid;
+          ev[i][j] = llvm_raw_buffer_load_v2i32(rsE, ok ? (int)(((long)m * lde + n) * 2) : BUF_OOB, 0, 0);
+        }
+      }
+    };
     if (kt == (nk > 1 ? nk - 2 : 0)) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -1546,21 +1564,17 @@ __global__ void __launch_bounds__(BNT) gemm_pk_kernel(GemmP p) {
         const bool in = m < p.mvalid;
         rs[i] = (p.row_scale && in) ? p.row_scale[m] : 1.f;
         rs2[i] = (p.row_scale_post && in) ? p.row_scale_post[m] : 1.f;
-        if (has_e) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int n = nb + 16 * j + 4 * lg;
-            const bool ok = in && n < p.nvalid;
-            ev[i][j] = llvm_raw_buffer_load_v2i32(rsE, ok ? (int)(((long)m * lde + n) * 2) : BUF_OOB, 0, 0);
-          }
-        }
       }
+      if (has_e && !early_e) load_e();
     }
     const bool pre = it + 2 < total;
     if (pre) {
       issue(t2, kt2, (it + 2) % 3);
       if (++kt2 == nk) { kt2 = 0; ++t2; }
     }
+    // a gate / residual operand streams from HBM (64 KiB per tile): with nk >= 4 it is issued
+    // after iteration nk - 4's prefetch, so three K-tiles cover its latency instead of one
+    if (early_e && kt == e0) load_e();
     const char* la = smem + (it % 3) * BIG_STAGE;
     const char* lb = la + BIG_A;
     bf16x8 af[2][4], bfr[2][4];

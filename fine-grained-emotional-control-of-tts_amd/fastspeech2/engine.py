@@ -251,6 +251,7 @@ class FS2Engine:
             return
         if self._wtable is None:
             entries = []
+            self._wentries = {}
             for name, (O, C, KW) in self._wspecs.items():
                 ldf = round_up(KW * C, self.epc)
                 ldb = KW * O
@@ -260,6 +261,7 @@ class FS2Engine:
                 W = self.params[name]
                 # conv weights are [O][KW][C] in the flat buffer (model._kw_major)
                 entries.append((W, O, C, KW, int(KW > 1), Wf, ldf, Wb, ldb))
+                self._wentries[name] = entries[-1]
             self._wtable = ops.weight_prep_table(entries)
         ops.weight_prep_batched(*self._wtable, dt=self.dt)
         self._prepared_version = ver
@@ -277,6 +279,46 @@ class FS2Engine:
             else:
                 rng.append((off, k))
         return rng
+
+    def _group_tables(self):
+        """per backward group (model.group_tag): fs2_adamw_prep tables over that group's GEMM
+        weights and its other parameters"""
+        if getattr(self, "_gtables", None) is None:
+            from .model import group_tag
+            if self._wtable is None:
+                self.prepare_weights(force=True)
+            wl, rl = {}, {}
+            for name, off, k, _, key in self.m._layout:
+                tag = group_tag(key)
+                if name in self._wspecs:
+                    wl.setdefault(tag, []).append(self._wentries[name])
+                    continue
+                r = rl.setdefault(tag, [])
+                if r and off - (r[-1][0] + r[-1][1]) < 16:
+                    r[-1] = (r[-1][0], off + k - r[-1][0])
+                else:
+                    r.append((off, k))
+            self._gtables = {
+                tag: (ops.weight_prep_table(wl[tag]) if tag in wl else (None, 0, 0),
+                      ops.adamw_ranges_table(rl.get(tag, []), self.dev))
+                for tag in list(wl) + [t for t in rl if t not in wl]}
+        return self._gtables
+
+    def adamw_group(self, tag, opt, decay_mul, omb1, beta2, omb2, step_size, bc2_sqrt, eps,
+                    gscale):
+        """AdamW + weight images of one backward group's parameters on the current stream: the
+        train step runs it as soon as the group's gradients are complete (the same per-element
+        update as ``adamw_step``, so the result is bit-identical)"""
+        m = self.m
+        wt, rt = self._group_tables()[tag]
+        ops.adamw_prep(wt, rt, m._flat, m._gflat, opt.exp_avg, opt.exp_avg_sq, decay_mul, omb1,
+                       beta2, omb2, step_size, bc2_sqrt, eps, gscale, dt=self.dt)
+
+    def adamw_groups_done(self):
+        """after every group's update: the next forward finds the weight images current"""
+        m = self.m
+        m.mark_params_updated()
+        self._prepared_version = (m._param_version, m._flat._version)
 
     def adamw_step(self, opt, decay_mul, omb1, beta2, omb2, step_size, bc2_sqrt, eps, gscale):
         """AdamW over the flat buffers fused with the GEMM weight images (fs2_adamw_prep): the

@@ -33,17 +33,27 @@ class FusedAdamW:
         for n, p in self.model.named_parameters():
             p.grad = self.model._grad_views[n]
 
-    @torch.no_grad()
-    def step(self, grad_scale=1.0):
-        m = self.model
+    def begin_step(self, grad_scale=1.0):
+        """count the step and return its kernel scalars (torch single-tensor AdamW, double)"""
         self.step_count += 1
         b1, b2 = self.betas
         lr, wd, t = self.lr, self.weight_decay, self.step_count
         bc1 = 1 - b1 ** t
         bc2 = 1 - b2 ** t
-        args = (1 - lr * wd, 1 - b1, b2, 1 - b2, lr / bc1, bc2 ** 0.5, self.eps, grad_scale)
+        return (1 - lr * wd, 1 - b1, b2, 1 - b2, lr / bc1, bc2 ** 0.5, self.eps, grad_scale)
+
+    def fused_images(self):
+        """the update can also write the engine's GEMM weight images (fs2_adamw_prep)"""
+        m = self.model
         eng = m._engine
-        if eng is not None and not _NO_FUSED and eng._flat_is(m._flat):
+        return eng is not None and not _NO_FUSED and eng._flat_is(m._flat)
+
+    @torch.no_grad()
+    def step(self, grad_scale=1.0):
+        m = self.model
+        args = self.begin_step(grad_scale)
+        eng = m._engine
+        if self.fused_images():
             # the update also writes the next forward's GEMM weight images
             eng.adamw_step(self, *args)
             return

@@ -102,6 +102,10 @@ _GRAPH = os.environ.get("FS2_GRAPH", "0") not in ("", "0")
 # opt-in: A/B 20.55-20.61 ms off vs 20.59-20.68 ms on (the persistent GEMMs' blocks are all
 # resident from launch, so queue priority changes little)
 _PRIO = os.environ.get("FS2_PRIO", "0") not in ("", "0")
+# single process, opt-in (FS2_EARLY_ADAMW=1): AdamW per backward group as soon as the group's
+# gradients are complete, on its own stream.  Measured slower (A/B 21.19 vs 20.44 ms/step):
+# the update's blocks take CUs the persistent GEMM kernels expect to hold
+_EARLY = os.environ.get("FS2_EARLY_ADAMW", "0") not in ("", "0")
 
 
 class _StepGraph:
@@ -164,6 +168,8 @@ class FusedTrainer:
         self.use_graph = (self.world == 1 and _GRAPH) if graph is None else bool(graph)
         self._graphs = {}
         self._prio = None
+        self._opt_stream = None       # per-group AdamW beside the backward (single process)
+        self._early_done = set()
 
     def _graph_for(self, batch, intensity, mel_len_max):
         key = tuple(tuple(t.shape) for t in batch[:8]) + (tuple(intensity.shape), mel_len_max)
@@ -180,6 +186,9 @@ class FusedTrainer:
         produces them).  Returns the loss vector."""
         (phoneme, spk_ids, phon_len, mel_tgt, pitch_tgt, energy_tgt, duration_tgt, mel_len) = batch[:8]
         m = self.model
+        if self._opt_stream is not None:
+            # the previous step's group updates read and write the flat buffers
+            torch.cuda.current_stream(m._flat.device).wait_stream(self._opt_stream)
         m._gflat.zero_()
         out, ctx = self.eng.forward(phoneme, spk_ids, duration_tgt, pitch_tgt, energy_tgt,
                                     intensity=intensity, training=True,
@@ -191,6 +200,47 @@ class FusedTrainer:
                                  duration_tgt, avg_p.view(pd.shape), avg_e.view(pd.shape), mel_len,
                                  phon_len, self.weights)
         self.eng.backward(ctx, *grads)
+        return loss
+
+    def _early_hook(self, args):
+        """on_grads_ready hook of a single-process step: AdamW of a backward group on the
+        optimizer stream once its gradients are queued on the main and side streams -- the
+        HBM-bound update then runs under the MFMA-bound backward of the groups after it"""
+        s = self._opt_stream
+        done = self._early_done
+
+        def hook(tag, streams):
+            for st in streams:
+                s.wait_stream(st)
+            with torch.cuda.stream(s):
+                self.eng.adamw_group(tag, self.opt, *args)
+            done.add(tag)
+        return hook
+
+    def _early_on(self):
+        return (self.world == 1 and _EARLY and not self.use_graph and self.model._flat.is_cuda
+                and self.opt.fused_images())
+
+    def _step_early(self, batch, intensity, mel_len_max):
+        if self._opt_stream is None:
+            self._opt_stream = torch.cuda.Stream(self.model._flat.device)
+        self.eng._group_tables()
+        args = self.opt.begin_step(1.0)
+        self._early_done = set()
+        self.eng.on_grads_ready = self._early_hook(args)
+        try:
+            loss = self.forward_backward(batch, intensity, mel_len_max)
+        finally:
+            self.eng.on_grads_ready = None
+        main = torch.cuda.current_stream(self.model._flat.device)
+        missing = [t for t in self.eng._group_tables() if t not in self._early_done]
+        if missing:                      # defensive: groups the backward never reported
+            self._opt_stream.wait_stream(main)
+            with torch.cuda.stream(self._opt_stream):
+                for t in missing:
+                    self.eng.adamw_group(t, self.opt, *args)
+        main.wait_stream(self._opt_stream)
+        self.eng.adamw_groups_done()
         return loss
 
     def apply(self):
@@ -227,6 +277,8 @@ class FusedTrainer:
         return self._prio
 
     def _step(self, batch, intensity, mel_len_max):
+        if self._early_on():
+            return self._step_early(batch, intensity, mel_len_max)
         if self.use_graph:
             mlm = mel_len_max if mel_len_max is not None else batch[3].shape[1]
             loss = self._graph_for(batch, intensity, mlm).replay(batch, intensity, self.seed)

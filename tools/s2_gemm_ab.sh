@@ -1,0 +1,10 @@
+#!/bin/bash
+# GEMM call-site microbench (tools/gemm_bench.py) under env settings ($@; "-" = defaults)
+set -o pipefail
+cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out/gab
+for cfg in "$@"; do
+  [ "$cfg" == "-" ] && cfg="FS2_AB_DEFAULT=1"
+  echo "== $cfg"
+  env $cfg timeout -k 10 200 python -u tools/gemm_bench.py > gpurun_out/gab/g.txt 2>&1 || { tail -20 gpurun_out/gab/g.txt; exit 1; }
+  grep -v amdgpu.ids gpurun_out/gab/g.txt
+done
