@@ -1459,8 +1459,6 @@ __global__ void __launch_bounds__(BNT) gemm_pk_kernel(GemmP p) {
   const i32x4 rsE = make_rsrc(p.gate ? p.gate : (p.residual ? p.residual : p.C));
   const long lde = p.gate ? p.ldg : p.ldr;
   const bool has_e = p.gate || p.residual;
-  const int e0 = nk - 4;                                   // early epilogue-load iteration
-  const bool early_e = has_e && nk >= 4 && !(p.g4_flags & 32);
 
   // per-lane parts of the DMA addressing (as gemm_big_kernel, plain operands)
   int ar[4], alc[4], br[2], blc[2];
@@ -1503,9 +1501,9 @@ __global__ void __launch_bounds__(BNT) gemm_pk_kernel(GemmP p) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   // epilogue operands of the current tile
-  f32x4 bv[4];
-  float rs[4], rs2[4];
-  i32x2 ev[4][4];
+  f32x4 bv[4] = {};
+  float rs[4] = {1.f, 1.f, 1.f, 1.f}, rs2[4] = {1.f, 1.f, 1.f, 1.f};
+  i32x2 ev[4][4] = {};
 
   // (t, kt) of iterations it (current), it + 2 (prefetch)
   int t = 0, kt = 0, t2 = 0, kt2 = 0;
@@ -1518,10 +1516,7 @@ __global__ void __launch_bounds__(BNT) gemm_pk_kernel(GemmP p) {
     // stage it landed: younger than its 6 pieces are those of it + 1 and, after a tile's
     // epilogue, that epilogue's 16 stores
     if (more) {
-      // early epilogue loads (issued after iteration e0's prefetch) stay in flight through
-      // the stage waits of iterations e0 + 1 and e0 + 2 (kt >= 1, so never after an epilogue)
-      if (early_e && (kt == e0 + 1 || kt == e0 + 2)) vm_wait<6 + 16>();
-      else if (!prev_last) vm_wait<6>();
+      if (!prev_last) vm_wait<6>();
       else if (p.c_fp32) vm_wait<6 + PK_STORES32>();
       else vm_wait<6 + PK_STORES16>();
     } else {
@@ -1539,20 +1534,7 @@ __global__ void __launch_bounds__(BNT) gemm_pk_kernel(GemmP p) {
     // epilogue operands one iteration ahead of the epilogue (nk >= 2): issued before this
     // iteration's prefetch, they are retired by the NEXT iteration's stage wait, so the
     // epilogue itself never waits on a load (with nk == 1 they are issued in the same one)
-    auto load_e = [&]() {   // the tile's gate / residual operand: exactly 16 buffer loads
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int m = mb + 16 * i + li;
-        const bool in = m < p.mvalid;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int n = nb + 16 * j + 4 * lg;
-          const bool ok = in && n < p.nvalid;
-          ev[i][j] = llvm_raw_buffer_load_v2i32(rsE, ok ? (int)(((long)m * lde + n) * 2) : BUF_OOB, 0, 0);
-        }
-      }
-    };
-    if (kt == (nk > 1 ? nk - 2 : 0)) {
+    if (kt == (nk > 1 ? nk - 2 : 0) && !(p.g4_flags & 64)) {   // flag 64: timing only
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int n = nb + 16 * j + 4 * lg;
@@ -1564,17 +1546,21 @@ __global__ void __launch_bounds__(BNT) gemm_pk_kernel(GemmP p) {
         const bool in = m < p.mvalid;
         rs[i] = (p.row_scale && in) ? p.row_scale[m] : 1.f;
         rs2[i] = (p.row_scale_post && in) ? p.row_scale_post[m] : 1.f;
+        if (has_e) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int n = nb + 16 * j + 4 * lg;
+            const bool ok = in && n < p.nvalid;
+            ev[i][j] = llvm_raw_buffer_load_v2i32(rsE, ok ? (int)(((long)m * lde + n) * 2) : BUF_OOB, 0, 0);
+          }
+        }
       }
-      if (has_e && !early_e) load_e();
     }
     const bool pre = it + 2 < total;
     if (pre) {
       issue(t2, kt2, (it + 2) % 3);
       if (++kt2 == nk) { kt2 = 0; ++t2; }
     }
-    // a gate / residual operand streams from HBM (64 KiB per tile): with nk >= 4 it is issued
-    // after iteration nk - 4's prefetch, so three K-tiles cover its latency instead of one
-    if (early_e && kt == e0) load_e();
     const char* la = smem + (it % 3) * BIG_STAGE;
     const char* lb = la + BIG_A;
     bf16x8 af[2][4], bfr[2][4];
@@ -2071,8 +2057,14 @@ int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
       FS2_CHECK_LAUNCH();
       return 0;
     }
+    // narrow outputs with K >= 1152 (FFN conv2 forward, QKV data gradient) measured faster
+    // on the per-tile 256x128 kernel: decoder 70.5 -> 63.6 and 58.3 -> 55.6 us, encoder
+    // 33.7 -> 29.5 and 32.7 -> 29.0 (tools/gemm_bench.py, FS2_GEMM_NO_PK A/B);
+    // FS2_PK_NARROW=1 keeps them on the persistent kernel
+    static const bool pk_narrow = getenv_flag("FS2_PK_NARROW");
+    const bool pk_shape = p.K <= 768 || p.N > 512 || pk_narrow;
     if (!no_pk && ak && bk && p.conv_mode == 0 && batch == 1 && p.split_k <= 1 && p.vec_ok &&
-        !p.accumulate && !(p.gate && p.residual) && p.K <= 1536 && pk_fits) {
+        !p.accumulate && !(p.gate && p.residual) && p.K <= 1536 && pk_shape && pk_fits) {
       GemmP q = p;
       static const int pkf = [] { const char* v = std::getenv("FS2_PK_FLAGS"); return v ? std::atoi(v) : 0; }();
       q.g4_flags = pkf;

@@ -1,4 +1,5 @@
 #include <cstdlib>
+#include <algorithm>
 // LayerNorm forward/backward with fused residual-add, dropout, tanh, row-mask, post-add,
 // plus column-sum reductions for bias / gamma / beta gradients.
 //
@@ -672,7 +673,12 @@ __global__ void __launch_bounds__(256) sum_slices_kernel(const float* ws, int ns
   ((f32x4*)out)[i] = a;
 }
 
-int ln_blocks(int M) { return min(4096, max(1, (M + 31) / 32)); }
+// rows per LayerNorm-backward block (4 waves): FS2_LN_RPB for A/B runs (default 32)
+int ln_rpb() {
+  static const int r = [] { const char* v = std::getenv("FS2_LN_RPB"); return v && v[0] ? std::max(4, std::atoi(v)) : 32; }();
+  return r;
+}
+int ln_blocks(int M) { return min(8192, max(1, (M + ln_rpb() - 1) / ln_rpb())); }
 // rows in flight per wave in the bf16 LayerNorm backward (FS2_LN_ROWS=1 selects the one-row
 // kernel for A/B runs)
 int ln_rows_r() {

@@ -71,6 +71,10 @@ _PS_MODES = int(os.environ.get("FS2_PS_MODES", "5"))
 # sum instead of split-K fp32 atomics: decoder 428 -> 420 us, encoder 128 -> 119 us, and the
 # result no longer depends on atomic ordering.  FS2_NO_WGRAD_BIG_SLICES=1 restores the atomics.
 _BIG_SLICES = os.environ.get("FS2_NO_WGRAD_BIG_SLICES", "0") in ("", "0")
+_SLICE_TARGET = int(os.environ.get("FS2_WGRAD_SLICE_TARGET", "240"))
+# enqueue each weight gradient before the data gradient that does not need to precede it
+# (FS2_WGRAD_EARLY=0: the round-1 order, data gradient first)
+_WGRAD_EARLY = os.environ.get("FS2_WGRAD_EARLY", "1") not in ("", "0")
 _NO_SIDE = os.environ.get("FS2_NO_SIDE_STREAM", "0") not in ("", "0")
 _NO_AUX = os.environ.get("FS2_NO_AUX_STREAM", "0") not in ("", "0")
 # dQ and dK/dV of the encoder attention on two streams: opt-in, measured no faster (the side
@@ -404,7 +408,7 @@ class FS2Engine:
         ns = wgrad_slices(O, Ncols, ldc, K, self.dt) if not _NO_SLICES else 1
         if ns == 1 and _BIG_SLICES and self.dt == 1 and Ncols == ldc and O * ldc > 600_000:
             tiles = -(-O // 256) * -(-Ncols // 256)
-            ns = max(1, min(-(-240 // tiles), (K // 64) // 8))
+            ns = max(1, min(-(-_SLICE_TARGET // tiles), (K // 64) // 8))
         if ns > 1:
             # small outputs: split-K slices into fp32 planes, summed in a fixed order -- instead
             # of tens of fp32 atomics landing on every output element
@@ -509,16 +513,26 @@ class FS2Engine:
                    dr=dY, p_r=p_drop, salt_r=ctx["s_r2"], dgamma=G[prefix + "norm2.norm.weight"],
                    dbeta=G[prefix + "norm2.norm.bias"], dcol=G[prefix + "pos_ffn.2.conv.bias"])
         w2 = prefix + "pos_ffn.2.conv.weight"
-        dHc = self.empty(M, F)
-        self._dgrad(dY, D, M, T, w2, dHc, F, gate=ctx["Hc"], ldg=F)
-        self._wgrad(dY, D, ctx["Hc"], F, M, T, w2)
-        del dY
         w1 = prefix + "pos_ffn.0.conv.weight"
+        dHc = self.empty(M, F)
         dX1 = self.empty(M, D)
-        self._dgrad(dHc, F, M, T, w1, dX1, D, residual=ds2, ldr=D)
-        self._wgrad(dHc, F, ctx["X1"], D, M, T, w1)
-        self._bias_grad(dHc, F, M, F, prefix + "pos_ffn.0.conv.bias")
-        del dHc, ds2
+        if _WGRAD_EARLY:
+            # weight gradients enqueued as soon as their operands exist (the side stream waits
+            # for everything queued on main so far): conv2's before its data gradient, conv1's
+            # right after dHc, so the two big conv1 GEMMs overlap instead of the conv1 weight
+            # gradient holding every CU while main's out-projection waits behind it
+            self._wgrad(dY, D, ctx["Hc"], F, M, T, w2)
+            self._dgrad(dY, D, M, T, w2, dHc, F, gate=ctx["Hc"], ldg=F)
+            self._wgrad(dHc, F, ctx["X1"], D, M, T, w1)
+            self._bias_grad(dHc, F, M, F, prefix + "pos_ffn.0.conv.bias")
+            self._dgrad(dHc, F, M, T, w1, dX1, D, residual=ds2, ldr=D)
+        else:
+            self._dgrad(dY, D, M, T, w2, dHc, F, gate=ctx["Hc"], ldg=F)
+            self._wgrad(dY, D, ctx["Hc"], F, M, T, w2)
+            self._dgrad(dHc, F, M, T, w1, dX1, D, residual=ds2, ldr=D)
+            self._wgrad(dHc, F, ctx["X1"], D, M, T, w1)
+            self._bias_grad(dHc, F, M, F, prefix + "pos_ffn.0.conv.bias")
+        del dY, dHc, ds2
         lnws = self.ws(ops.ln_ws(M, D))
         ds1, dAo = self.empty(M, D), self.empty(M, D)
         ops.ln_bwd(dX1, D, ctx["s1"], D, ctx["mean1"], ctx["rstd1"], P[prefix + "norm1.norm.weight"],
@@ -529,8 +543,12 @@ class FS2Engine:
         del dX1
         wo = prefix + "self_att.att.out_proj.weight"
         dAtt = self.empty(M, D)
-        self._dgrad(dAo, D, M, T, wo, dAtt, D)
-        self._wgrad(dAo, D, ctx["Att"], D, M, T, wo)
+        if _WGRAD_EARLY:
+            self._wgrad(dAo, D, ctx["Att"], D, M, T, wo)
+            self._dgrad(dAo, D, M, T, wo, dAtt, D)
+        else:
+            self._dgrad(dAo, D, M, T, wo, dAtt, D)
+            self._wgrad(dAo, D, ctx["Att"], D, M, T, wo)
         del dAo
         QKV, Pm, Pd = ctx["QKV"], ctx["Pm"], ctx["Pd"]
         if "lse" in ctx:     # fused attention backward (dQ, dK, dV in one pass each)
@@ -583,9 +601,14 @@ class FS2Engine:
     def _qkv_bwd(self, dQKV, ctx, M, T, D, prefix, ds1):
         wi = prefix + "self_att.att.in_proj_weight"
         dX = self.empty(M, D)
-        self._dgrad(dQKV, 3 * D, M, T, wi, dX, D, residual=ds1, ldr=D)
-        self._wgrad(dQKV, 3 * D, ctx["X"], D, M, T, wi)
-        self._bias_grad(dQKV, 3 * D, M, 3 * D, prefix + "self_att.att.in_proj_bias")
+        if _WGRAD_EARLY:
+            self._wgrad(dQKV, 3 * D, ctx["X"], D, M, T, wi)
+            self._bias_grad(dQKV, 3 * D, M, 3 * D, prefix + "self_att.att.in_proj_bias")
+            self._dgrad(dQKV, 3 * D, M, T, wi, dX, D, residual=ds1, ldr=D)
+        else:
+            self._dgrad(dQKV, 3 * D, M, T, wi, dX, D, residual=ds1, ldr=D)
+            self._wgrad(dQKV, 3 * D, ctx["X"], D, M, T, wi)
+            self._bias_grad(dQKV, 3 * D, M, 3 * D, prefix + "self_att.att.in_proj_bias")
         return dX
 
     # ------------------------------------------------------------------ variance predictor

@@ -1,0 +1,12 @@
+#!/bin/bash
+# session-2 microbenchmarks: LayerNorm kernels, then GEMM call sites under $@ (env settings)
+set -o pipefail
+cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out/gab
+timeout -k 10 120 python -u tools/ln_bench.py > gpurun_out/gab/ln.txt 2>&1 || { tail -20 gpurun_out/gab/ln.txt; exit 1; }
+grep -v amdgpu.ids gpurun_out/gab/ln.txt
+for cfg in "$@"; do
+  [ "$cfg" == "-" ] && cfg="FS2_AB_DEFAULT=1"
+  echo "== gemm $cfg"
+  env $cfg timeout -k 10 200 python -u tools/gemm_bench.py > gpurun_out/gab/g.txt 2>&1 || { tail -20 gpurun_out/gab/g.txt; exit 1; }
+  grep -v amdgpu.ids gpurun_out/gab/g.txt | grep -v blas
+done
