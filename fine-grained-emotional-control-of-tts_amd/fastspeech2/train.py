@@ -106,6 +106,9 @@ _PRIO = os.environ.get("FS2_PRIO", "0") not in ("", "0")
 # gradients are complete, on its own stream.  Measured slower (A/B 21.19 vs 20.44 ms/step):
 # the update's blocks take CUs the persistent GEMM kernels expect to hold
 _EARLY = os.environ.get("FS2_EARLY_ADAMW", "0") not in ("", "0")
+# opt-in (FS2_ZERO_SIDE=1): the gradient memset on the weight-gradient side stream, beside the
+# forward, instead of on the step's stream before it (A/B 20.35-20.39 vs 20.36-20.40 ms: neutral)
+_ZERO_SIDE = os.environ.get("FS2_ZERO_SIDE", "0") not in ("", "0")
 
 
 class _StepGraph:
@@ -186,10 +189,19 @@ class FusedTrainer:
         produces them).  Returns the loss vector."""
         (phoneme, spk_ids, phon_len, mel_tgt, pitch_tgt, energy_tgt, duration_tgt, mel_len) = batch[:8]
         m = self.model
+        main = torch.cuda.current_stream(m._flat.device) if m._flat.is_cuda else None
         if self._opt_stream is not None:
             # the previous step's group updates read and write the flat buffers
-            torch.cuda.current_stream(m._flat.device).wait_stream(self._opt_stream)
-        m._gflat.zero_()
+            main.wait_stream(self._opt_stream)
+        side = self.eng._side if _ZERO_SIDE else None
+        if side is not None:
+            # the 341 MB gradient memset runs on the (idle) weight-gradient stream beside the
+            # forward; the backward, the first writer of any gradient, waits for it
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                m._gflat.zero_()
+        else:
+            m._gflat.zero_()
         out, ctx = self.eng.forward(phoneme, spk_ids, duration_tgt, pitch_tgt, energy_tgt,
                                     intensity=intensity, training=True,
                                     seed=self.seed if seed is None else seed,
@@ -199,6 +211,8 @@ class FusedTrainer:
         loss, grads = fused_loss(mel, post, pd, pp.view(pd.shape), pe.view(pd.shape), mel_tgt,
                                  duration_tgt, avg_p.view(pd.shape), avg_e.view(pd.shape), mel_len,
                                  phon_len, self.weights)
+        if side is not None:
+            main.wait_stream(side)
         self.eng.backward(ctx, *grads)
         return loss
 
