@@ -1511,7 +1511,14 @@ __global__ void __launch_bounds__(BNT) gemm_pk_kernel(GemmP p) {
   if (total > 1) { t2 = nk > 1 ? 0 : 1; kt2 = nk > 1 ? 1 : 0; issue(t2, kt2, 1); }
   if (++kt2 == nk) { kt2 = 0; ++t2; }     // (t2, kt2) = iteration 2
   bool prev_last = false;
-  for (int it = 0; it < total; ++it) {
+  int it = 0;
+  // One K-tile iteration.  The tile's second-to-final iteration (LOADS: epilogue operands)
+  // and its final one (EPI: epilogue) are separate instantiations, peeled out of the K loop:
+  // with the operand loads under a runtime test inside one loop body, the compiler saw them
+  // pending across the back edge and put a vmcnt(0) before every re-load -- one full DMA drain
+  // per tile (FS2_PK_FLAGS=64 timing runs: FFN conv2 data gradient 100 -> 78 us without it).
+  auto step = [&](auto LD, auto EP) __attribute__((always_inline)) {
+    constexpr bool LOADS = decltype(LD)::value, EPI = decltype(EP)::value;
     const bool more = it + 1 < total;
     // stage it landed: younger than its 6 pieces are those of it + 1 and, after a tile's
     // epilogue, that epilogue's 16 stores
@@ -1527,14 +1534,13 @@ __global__ void __launch_bounds__(BNT) gemm_pk_kernel(GemmP p) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    const bool last = kt == nk - 1;
     const int tile = c0 + local + t * nbx;
     const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
     const int mb = tm * BBM + wm * 64, nb = tn * 128 + wn * 64;
     // epilogue operands one iteration ahead of the epilogue (nk >= 2): issued before this
     // iteration's prefetch, they are retired by the NEXT iteration's stage wait, so the
     // epilogue itself never waits on a load (with nk == 1 they are issued in the same one)
-    if (kt == (nk > 1 ? nk - 2 : 0) && !(p.g4_flags & 64)) {   // flag 64: timing only
+    if constexpr (LOADS) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int n = nb + 16 * j + 4 * lg;
@@ -1580,7 +1586,7 @@ __global__ void __launch_bounds__(BNT) gemm_pk_kernel(GemmP p) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[s][j], af[s][i], acc[i][j], 0, 0, 0);
     __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);
     __builtin_amdgcn_sched_group_barrier(0x008, 32, 0);
-    if (last) {
+    if constexpr (EPI) {
       if (nk == 1) {   // operands issued this iteration: retire them, keep the prefetch in flight
         if (pre) vm_wait<6>(); else vm_wait<0>();
       }
@@ -1642,8 +1648,16 @@ __global__ void __launch_bounds__(BNT) gemm_pk_kernel(GemmP p) {
         }
       }
     }
-    prev_last = last;
+    prev_last = EPI;
     if (++kt == nk) { kt = 0; ++t; }
+    ++it;
+  };
+  using F_ = std::false_type;
+  using T_ = std::true_type;
+  for (int tt = 0; tt < mine; ++tt) {   // nk >= 2 (the dispatcher routes K <= 64 elsewhere)
+    for (int k = 0; k < nk - 2; ++k) step(F_{}, F_{});
+    step(T_{}, F_{});
+    step(F_{}, T_{});
   }
 }
 
@@ -2064,7 +2078,7 @@ int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
     static const bool pk_narrow = getenv_flag("FS2_PK_NARROW");
     const bool pk_shape = p.K <= 768 || p.N > 512 || pk_narrow;
     if (!no_pk && ak && bk && p.conv_mode == 0 && batch == 1 && p.split_k <= 1 && p.vec_ok &&
-        !p.accumulate && !(p.gate && p.residual) && p.K <= 1536 && pk_shape && pk_fits) {
+        !p.accumulate && !(p.gate && p.residual) && p.K > 64 && p.K <= 1536 && pk_shape && pk_fits) {
       GemmP q = p;
       static const int pkf = [] { const char* v = std::getenv("FS2_PK_FLAGS"); return v ? std::atoi(v) : 0; }();
       q.g4_flags = pkf;
