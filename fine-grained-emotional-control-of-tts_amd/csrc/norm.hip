@@ -80,6 +80,95 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(LnFwdP p) {
   }
 }
 
+// bf16, D <= 512 (one 16-byte chunk per lane): R rows per wave (rows w, w + 4, ... of the
+// block's 4R), every row's x / r / post-add loaded before the first row is reduced.  One row
+// per wave kept ~1.5 KB in flight per wave -- 48 KB per CU at full occupancy -- and ran the
+// decoder LayerNorm (96 MB) at 3.6 TB/s.  Per-row arithmetic, dropout indices and rounding
+// points are those of ln_fwd_vec_kernel<bf16, 1> (outputs bit-identical).
+template <int R>
+__global__ void __launch_bounds__(256) ln_fwd_rows_kernel(LnFwdP p) {
+  constexpr int V = 8;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int d0 = lane * V;
+  const bool act = d0 < p.D;
+  const int dd = act ? d0 : 0;
+  const float inv_r = p.p_r > 0.f ? 1.f / (1.f - p.p_r) : 1.f;
+  const float inv_o = p.p_o > 0.f ? 1.f / (1.f - p.p_o) : 1.f;
+  float g[V], b[V];
+  vload<float>(g, p.gamma + dd);
+  vload<float>(g + 4, p.gamma + dd + 4);
+  vload<float>(b, p.beta + dd);
+  vload<float>(b + 4, p.beta + dd + 4);
+  float v[R][V], rv[R][V], a[R][V], rm[R];
+  int rows[R];
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    rows[j] = blockIdx.x * (4 * R) + 4 * j + wave;
+    const int rr = min(rows[j], p.M - 1);
+    vload<bf16>(v[j], (const bf16*)p.x + (long)rr * p.ldx + dd);
+    if (p.r) vload<bf16>(rv[j], (const bf16*)p.r + (long)rr * p.ldr + dd);
+    if (p.post_add) vload<bf16>(a[j], (const bf16*)p.post_add + (long)rr * p.ldp + dd);
+    rm[j] = p.row_mask ? p.row_mask[rr] : 1.f;
+  }
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    const int row = rows[j];
+    if (row >= p.M) break;
+    float sum = 0.f;
+    if (act) {
+      if (p.r) {
+        bool kr[V];
+        if (p.p_r > 0.f) fs2_keep_run<V>(p.seed, p.salt_r, (uint64_t)row * p.D + d0, p.p_r, kr);
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+          float q = rv[j][e];
+          if (p.p_r > 0.f) q = kr[e] ? q * inv_r : 0.f;
+          v[j][e] += q;
+        }
+      }
+      if (p.s_out) {
+        vstore<bf16>((bf16*)p.s_out + (long)row * p.D + d0, v[j]);
+        if (p.r) {  // statistics of the stored (rounded) s, as the backward re-reads it
+#pragma unroll
+          for (int e = 0; e < V; ++e) v[j][e] = to_f(from_f<bf16>(v[j][e]));
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < V; ++e) sum += v[j][e];
+    }
+    const float mean = wave_sum(sum) / (float)p.D;
+    float sq = 0.f;
+    if (act) {
+#pragma unroll
+      for (int e = 0; e < V; ++e) { const float c = v[j][e] - mean; sq += c * c; }
+    }
+    const float var = wave_sum(sq) / (float)p.D;
+    const float rstd = 1.f / sqrtf(var + p.eps);
+    if (lane == 0) { p.mean[row] = mean; p.rstd[row] = rstd; }
+    if (act) {
+      float o[V];
+      bool ko[V];
+      if (p.p_o > 0.f) fs2_keep_run<V>(p.seed, p.salt_o, (uint64_t)row * p.D + d0, p.p_o, ko);
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        float q = (v[j][e] - mean) * rstd * g[e] + b[e];
+        if (p.do_tanh) q = tanhf(q);
+        if (p.p_o > 0.f) q = ko[e] ? q * inv_o : 0.f;
+        q *= rm[j];
+        if (p.post_add) q += a[j][e];
+        o[e] = q;
+      }
+      vstore<bf16>((bf16*)p.y + (long)row * p.ldy + d0, o);
+    }
+  }
+}
+
+// rows per wave of the bf16 LayerNorm forward (FS2_LN_FWD_ROWS: 1 = ln_fwd_vec_kernel)
+int ln_fwd_rows() {
+  static const int r = [] { const char* v = std::getenv("FS2_LN_FWD_ROWS"); return v && v[0] ? std::atoi(v) : 2; }();
+  return r;
+}
+
 struct LnBwdP {
   const char* dy; long lddy; const char* s; long lds; const float* mean; const float* rstd;
   const float* gamma; const float* beta; int do_tanh; float p_o; uint32_t salt_o;
@@ -718,6 +807,10 @@ extern "C" int fs2_ln_fwd(const void* x, int64_t ldx, const void* r, int64_t ldr
                    (!s_out || a16(s_out)) && (!post_add || (a16(post_add) && ldp % V == 0));
   if (dtype == FS2_BF16) {
     if (!vec) hipLaunchKernelGGL(ln_fwd_kernel<bf16>, grid, dim3(256), 0, s, p);
+    else if (nch == 1 && ln_fwd_rows() == 2 && a16(gamma) && a16(beta))
+      hipLaunchKernelGGL((ln_fwd_rows_kernel<2>), dim3((M + 7) / 8), dim3(256), 0, s, p);
+    else if (nch == 1 && ln_fwd_rows() == 4 && a16(gamma) && a16(beta))
+      hipLaunchKernelGGL((ln_fwd_rows_kernel<4>), dim3((M + 15) / 16), dim3(256), 0, s, p);
     else if (nch == 1) hipLaunchKernelGGL((ln_fwd_vec_kernel<bf16, 1>), grid, dim3(256), 0, s, p);
     else if (nch == 2) hipLaunchKernelGGL((ln_fwd_vec_kernel<bf16, 2>), grid, dim3(256), 0, s, p);
     else hipLaunchKernelGGL((ln_fwd_vec_kernel<bf16, 4>), grid, dim3(256), 0, s, p);
