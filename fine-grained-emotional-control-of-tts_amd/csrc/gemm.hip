@@ -59,6 +59,8 @@ struct GemmP {
   int tiles_m, tiles_n;
   int vec_ok;
   int vec_align;  // vector epilogue possible if K were not split
+  uint8_t* relu_mask; long ldm;         // bf16: packed (C > 0) bits, written by the vector epilogue
+  const uint8_t* gate_bits; long ldgb;  // bf16: packed gate bits (gate_bits-aware kernels)
 };
 
 __device__ __forceinline__ u32x4 add_bf16x8(u32x4 a, u32x4 b) {
@@ -774,7 +776,13 @@ __device__ __forceinline__ void epilogue_256x128(const GemmP& p, const float* cs
       }
     }
     float g[8], rr[8];
-    if (p.gate) load8<bf16>(g, (const bf16*)p.gate + (long)m * p.ldg + n, nn);
+    if (p.gate_bits) {
+      const unsigned gb = p.gate_bits[(long)m * p.ldgb + (n >> 3)];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) g[e] = (gb >> e) & 1u ? 1.f : 0.f;
+    } else if (p.gate) {
+      load8<bf16>(g, (const bf16*)p.gate + (long)m * p.ldg + n, nn);
+    }
     if (Rb) load8<bf16>(rr, (const bf16*)Rb + (long)m * p.ldr + n, nn);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -798,6 +806,15 @@ __device__ __forceinline__ void epilogue_256x128(const GemmP& p, const float* cs
       }
     } else {
       store8<bf16>((bf16*)Cb + off, v, nn);
+      if (p.relu_mask) {   // bits of the stored bf16 values (> 0: positive and non-zero)
+        unsigned bits = 0;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const unsigned short h = __builtin_bit_cast(unsigned short, (bf16)v[e]);
+          bits |= (e < nn && h != 0 && h < 0x8000u) ? 1u << e : 0u;
+        }
+        p.relu_mask[(long)m * p.ldm + (n >> 3)] = (uint8_t)bits;
+      }
     }
   }
 }
@@ -1038,7 +1055,7 @@ __global__ void __launch_bounds__(BNT) gemm_big_kernel(GemmP p) {
   char* Cb = p.C + (zb * p.sC1 + zh * p.sC2) * (p.c_fp32 ? 4 : 2);
   if (p.split_stride > 0 && p.split_k > 1) Cb += (long)blockIdx.z * p.split_stride * 4;
   const char* Rb = p.residual ? p.residual + (zb * p.sR1 + zh * p.sR2) * 2 : nullptr;
-  if (p.vec_ok && !(p.g4_flags & 64)) {
+  if (p.vec_ok && !(p.g4_flags & 64) && !p.relu_mask && !p.gate_bits) {
     epilogue_direct(p, &acc[0][0], m0 + wm * 64, n0 + wn * 64, Cb, Rb, lane);
     return;
   }
@@ -1432,6 +1449,8 @@ __device__ void llvm_raw_buffer_store_v4i32(i32x4 data, i32x4 rsrc, int voffset,
                                             int aux) __asm("llvm.amdgcn.raw.buffer.store.v4i32");
 __device__ i32x2 llvm_raw_buffer_load_v2i32(i32x4 rsrc, int voffset, int soffset,
                                             int aux) __asm("llvm.amdgcn.raw.buffer.load.v2i32");
+__device__ unsigned char llvm_raw_buffer_load_i8(i32x4 rsrc, int voffset, int soffset,
+                                                 int aux) __asm("llvm.amdgcn.raw.buffer.load.i8");
 
 // epilogue store instructions per wave per tile: fp32 one 16-byte store per 16x16 block (16);
 // bf16 one 16-byte store per block PAIR (8: lanes l and l ^ 16 trade halves)
@@ -1456,7 +1475,9 @@ __global__ void __launch_bounds__(BNT) gemm_pk_kernel(GemmP p) {
   const int nk = (p.K + 63) / 64;
   const int total = mine * nk;
   const i32x4 rsA = make_rsrc(p.A), rsB = make_rsrc(p.B), rsC = make_rsrc(p.C);
-  const i32x4 rsE = make_rsrc(p.gate ? p.gate : (p.residual ? p.residual : p.C));
+  const bool gbits = p.gate_bits != nullptr;
+  const i32x4 rsE = make_rsrc(gbits ? (const void*)p.gate_bits
+                                    : (p.gate ? p.gate : (p.residual ? p.residual : p.C)));
   const long lde = p.gate ? p.ldg : p.ldr;
   const bool has_e = p.gate || p.residual;
 
@@ -1552,7 +1573,14 @@ __global__ void __launch_bounds__(BNT) gemm_pk_kernel(GemmP p) {
         const bool in = m < p.mvalid;
         rs[i] = (p.row_scale && in) ? p.row_scale[m] : 1.f;
         rs2[i] = (p.row_scale_post && in) ? p.row_scale_post[m] : 1.f;
-        if (has_e) {
+          if (gbits) {   // packed gate bits: one byte (8 columns) per block, same count
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int n = nb + 16 * j + 4 * lg;
+            const bool ok = in && n < p.nvalid;
+            ev[i][j][0] = llvm_raw_buffer_load_i8(rsE, ok ? (int)((long)m * p.ldgb + (n >> 3)) : BUF_OOB, 0, 0);
+          }
+        } else if (has_e) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const int n = nb + 16 * j + 4 * lg;
@@ -1599,7 +1627,8 @@ __global__ void __launch_bounds__(BNT) gemm_pk_kernel(GemmP p) {
           float x = epi_act(acc[i][j][e] + bv[j][e], p.relu);
           const unsigned w = (unsigned)ev[i][j][e >> 1];
           const float ef = __builtin_bit_cast(float, (e & 1) ? (w & 0xffff0000u) : (w << 16));
-          if (p.gate) x = ef > 0.f ? x : 0.f;
+          if (gbits) x = ((unsigned)ev[i][j][0] >> ((lg & 1) * 4 + e)) & 1u ? x : 0.f;
+          else if (p.gate) x = ef > 0.f ? x : 0.f;
           x *= rs[i];
           if (p.residual) x += ef;
           v[e] = x * rs2[i];
@@ -2006,6 +2035,25 @@ void launch4(const GemmP& p, dim3 grid, hipStream_t s, int ak, int bk) {
   else hipLaunchKernelGGL((gemm_kernel<T, false, false, GA, GB>), grid, dim3(NT), 0, s, p);
 }
 
+// bit n % 8 of mask[m][n / 8] = (C[m][n] > 0) for bf16 C (nvalid % 8 == 0): the packed ReLU
+// pattern for GEMM paths whose epilogue does not write it
+__global__ void __launch_bounds__(256) pack_relu_mask_kernel(const bf16* C, long ldc, int n8row,
+                                                             long n8, uint8_t* mask, long ldm) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n8) return;
+  const long m = i / n8row;
+  const int c = (int)(i - m * n8row);
+  const u32x4 u = *(const u32x4*)(C + m * ldc + 8 * c);
+  unsigned bits = 0;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const unsigned lo = u[w] & 0xffffu, hi = u[w] >> 16;
+    bits |= (lo != 0 && lo < 0x8000u) ? 1u << (2 * w) : 0u;
+    bits |= (hi != 0 && hi < 0x8000u) ? 1u << (2 * w + 1) : 0u;
+  }
+  mask[m * ldm + c] = (uint8_t)bits;
+}
+
 template <typename T>
 int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
   dim3 grid(p.tiles_m * p.tiles_n, 1, gz);
@@ -2047,7 +2095,7 @@ int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
                       : ((p.conv_mode == 1 || p.conv_mode == 4) && p.conv_dil == 1 && p.conv_c % 64 == 0
                              ? p.conv_mode : -1);
     const bool ps_on = cm_ps >= 0 && (ps_modes >> (cm_ps == 0 ? 0 : (cm_ps == 1 ? 1 : 2))) & 1;
-    if (!no_ps && ak && bk && ps_on && batch == 1 && p.split_k <= 1 && p.vec_ok &&
+    if (!no_ps && ak && bk && ps_on && batch == 1 && p.split_k <= 1 && p.vec_ok && !p.relu_mask &&
         !p.accumulate && !p.gate && !p.residual && p.relu <= 1 && p.K >= 2048 && p.N >= 128 && pk_fits) {
       GemmP q = p;
       static const int psf = [] { const char* v = std::getenv("FS2_PS_FLAGS"); return v ? std::atoi(v) : 0; }();
@@ -2077,7 +2125,7 @@ int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
     // FS2_PK_NARROW=1 keeps them on the persistent kernel
     static const bool pk_narrow = getenv_flag("FS2_PK_NARROW");
     const bool pk_shape = p.K <= 768 || p.N > 512 || pk_narrow;
-    if (!no_pk && ak && bk && p.conv_mode == 0 && batch == 1 && p.split_k <= 1 && p.vec_ok &&
+    if (!no_pk && ak && bk && p.conv_mode == 0 && batch == 1 && p.split_k <= 1 && p.vec_ok && !p.relu_mask &&
         !p.accumulate && !(p.gate && p.residual) && p.K > 64 && p.K <= 1536 && pk_shape && pk_fits) {
       GemmP q = p;
       static const int pkf = [] { const char* v = std::getenv("FS2_PK_FLAGS"); return v ? std::atoi(v) : 0; }();
@@ -2178,8 +2226,17 @@ int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
       } else {
         hipLaunchKernelGGL((gemm_big_kernel<false, true, -1, -1>), g2, dim3(BNT), 0, s, q);
       }
-    } else if (p.conv_mode == 2) launch4<T, false, true>(p, grid, s, ak, bk);
-    else launch4<T, true, true>(p, grid, s, ak, bk);
+    } else {
+      if (p.conv_mode == 2) launch4<T, false, true>(p, grid, s, ak, bk);
+      else launch4<T, true, true>(p, grid, s, ak, bk);
+      // the 128x128 kernel's epilogue does not pack the ReLU pattern: derive it from C
+      if (p.relu_mask) {
+        FS2_CHECK_LAUNCH();
+        const long n8 = (long)p.mvalid * (p.nvalid / 8);
+        hipLaunchKernelGGL(pack_relu_mask_kernel, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0,
+                           s, (const bf16*)p.C, p.ldc, p.nvalid / 8, n8, p.relu_mask, p.ldm);
+      }
+    }
   } else {
     launch4<T, false, false>(p, grid, s, ak, bk);
   }
@@ -2218,6 +2275,8 @@ extern "C" int fs2_gemm(const fs2_gemm_desc* d, void* stream) {
   p.batch_div = d->batch_div > 0 ? d->batch_div : 1;
   p.sA1 = d->sA1; p.sA2 = d->sA2; p.sB1 = d->sB1; p.sB2 = d->sB2;
   p.sC1 = d->sC1; p.sC2 = d->sC2; p.sR1 = d->sR1; p.sR2 = d->sR2;
+  p.relu_mask = d->relu_mask; p.ldm = d->ldm;
+  p.gate_bits = d->gate_bits; p.ldgb = d->ldgb;
   p.tiles_m = (p.M + BM - 1) / BM;
   p.tiles_n = (p.N + BN - 1) / BN;
   const int batch = d->batch > 1 ? d->batch : 1;
@@ -2256,6 +2315,11 @@ extern "C" int fs2_gemm(const fs2_gemm_desc* d, void* stream) {
     p.split_k = (nkt + kps - 1) / kps;
   }
   if (p.accumulate && !p.c_fp32) return FS2_EINVAL;
+  if (p.relu_mask && (d->dtype != FS2_BF16 || p.c_fp32 || batch > 1 || p.split_k > 1 ||
+                      (p.nvalid % 8) || p.ldm * 8 < p.nvalid || (p.ldc % 8) || !aligned16(p.C)))
+    return FS2_EINVAL;
+  if (p.gate_bits && (!p.gate || d->dtype != FS2_BF16 || batch > 1 || p.ldgb * 8 < p.nvalid))
+    return FS2_EINVAL;
   {
     const int oes = p.c_fp32 ? 4 : es;
     const int ov = 16 / oes;  // output elements per 16 bytes

@@ -43,6 +43,8 @@ class GemmDesc(ctypes.Structure):
         ("sA1", ctypes.c_int64), ("sA2", ctypes.c_int64), ("sB1", ctypes.c_int64),
         ("sB2", ctypes.c_int64), ("sC1", ctypes.c_int64), ("sC2", ctypes.c_int64),
         ("sR1", ctypes.c_int64), ("sR2", ctypes.c_int64), ("conv_dil", ctypes.c_int),
+        ("relu_mask", ctypes.c_void_p), ("ldm", ctypes.c_int64),
+        ("gate_bits", ctypes.c_void_p), ("ldgb", ctypes.c_int64),
     ]
 
 

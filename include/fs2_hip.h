@@ -73,6 +73,13 @@ typedef struct fs2_gemm_desc {
   int batch, batch_div;
   int64_t sA1, sA2, sB1, sB2, sC1, sC2, sR1, sR2;
   int conv_dil;         /* dilation of conv modes 1 / 5 (tap j reads row t + (j-P)*dil); 0 = 1 */
+  /* bf16 only.  relu_mask: also write bit (n % 8) of relu_mask[m*ldm + n/8] = (stored C > 0), the
+   * FFN conv1 forward's ReLU pattern (SB pos_ffn, model.py:241-267) in 1/16 of the bytes of C;
+   * needs nvalid % 8 == 0, batch 1, no split.  gate_bits: the same packed pattern used as the
+   * gate instead of re-reading gate's bf16 values (gate must still be given: kernels that
+   * do not read the bits fall back to it).                                                  */
+  uint8_t* relu_mask; int64_t ldm;
+  const uint8_t* gate_bits; int64_t ldgb;
 } fs2_gemm_desc;
 
 int fs2_gemm(const fs2_gemm_desc* d, void* stream);

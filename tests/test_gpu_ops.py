@@ -491,6 +491,38 @@ def test_gemm_persistent_long_k(cuda, M, N, K, c32):
     assert (C2[:, N:] == 0).all()
 
 
+@pytest.mark.parametrize("M,T", [(31264, 977), (6400, 200), (1000, 250), (200, 50)])
+def test_relu_bits_gate(cuda, M, T):
+    """bf16 FFN pair through the packed ReLU pattern: the conv1 forward (implicit reflect conv,
+    bias + ReLU) also writes bit n%8 of mask[m][n/8] = (stored output > 0), and the conv2 data
+    gradient reading those bits as its gate equals the one re-reading the bf16 activations,
+    bit for bit (decoder / encoder shapes, a small ragged one, and M = 200, whose GEMMs take the
+    128x128 kernel: its mask is packed from C by a separate pass)."""
+    from fastspeech2 import ops
+    torch.manual_seed(M)
+    C, F, KW = 384, 1536, 9
+    X = (torch.randn(M, C, device=cuda) * 0.5).to(torch.bfloat16)
+    W1 = (torch.randn(F, KW * C, device=cuda) * 0.03).to(torch.bfloat16)
+    b1 = torch.randn(F, device=cuda) * 0.1
+    H = torch.empty(M, F, device=cuda, dtype=torch.bfloat16)
+    mask = torch.full((M, F // 8), 0xA5, device=cuda, dtype=torch.uint8)
+    ops.gemm(M, F, KW * C, X, C, W1, KW * C, H, F, dt=1, conv=(1, T, KW, C), bias=b1, relu=1,
+             relu_mask=mask, ldm=F // 8)
+    bits = (H.float() > 0).to(torch.uint8).view(M, F // 8, 8)
+    ref = (bits << torch.arange(8, device=cuda, dtype=torch.uint8)).sum(-1).to(torch.uint8)
+    assert torch.equal(mask, ref)
+    dY = (torch.randn(M, C, device=cuda) * 0.5).to(torch.bfloat16)
+    W2b = (torch.randn(F, C, device=cuda) * 0.05).to(torch.bfloat16)    # [F][C]: K-major
+    outs = []
+    for gb in (None, mask):
+        dH = torch.empty(M, F, device=cuda, dtype=torch.bfloat16)
+        kw = dict(gate_bits=gb, ldgb=F // 8) if gb is not None else {}
+        ops.gemm(M, F, C, dY, C, W2b, C, dH, F, dt=1, gate=H, ldg=F, **kw)
+        outs.append(dH)
+    assert torch.equal(outs[0], outs[1])
+    assert rel(outs[1], torch.where(H.float() > 0, dY.float() @ W2b.float().t(), 0.0)) < 1e-2
+
+
 def test_gemm_short_k_two_streams(cuda):
     """The persistent short-K kernel (gemm_pk_kernel) under concurrency: 40 back-to-back
     launches alternating between two streams (different tile counts, nk = 1 and nk = 6, bias
