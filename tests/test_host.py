@@ -51,6 +51,14 @@ def test_gemm_host_validation_rejects_bad_args():
     d.conv_mode = 0
     d.A = p16 + 2
     assert lib.fs2_gemm(ctypes.byref(d), None) == -2          # misaligned pointer
+    d.A = p16
+    d.relu_mask, d.ldm = p16, 1
+    assert lib.fs2_gemm(ctypes.byref(d), None) == -1          # relu_mask: ldm * 8 < nvalid
+    d.ldm, d.c_fp32 = 2, 1
+    assert lib.fs2_gemm(ctypes.byref(d), None) == -1          # relu_mask needs a bf16 output
+    d.c_fp32, d.relu_mask, d.ldm = 0, None, 0
+    d.gate_bits, d.ldgb = p16, 2
+    assert lib.fs2_gemm(ctypes.byref(d), None) == -1          # gate_bits without its gate
     assert lib.fs2_loss_fwd_bwd(None, None) == -1
     assert lib.fs2_gemm_workspace if hasattr(lib, "fs2_gemm_workspace") else True
 
