@@ -767,12 +767,14 @@ __global__ void __launch_bounds__(256) sum_slices_kernel(const float* ws, int ns
   ((f32x4*)out)[i] = a;
 }
 
-// rows per LayerNorm-backward block (4 waves): FS2_LN_RPB for A/B runs (default 32)
-int ln_rpb() {
-  static const int r = [] { const char* v = std::getenv("FS2_LN_RPB"); return v && v[0] ? std::max(4, std::atoi(v)) : 32; }();
-  return r;
+// rows per LayerNorm-backward block (4 waves): 32, or 16 when 32 leaves fewer than 512 blocks
+// (ln_bench, M = 6400: 20.0 -> 16.9 us; M = 31264: 38.5 vs 41.4 us with 16); FS2_LN_RPB forces
+int ln_rpb(int M) {
+  static const int r = [] { const char* v = std::getenv("FS2_LN_RPB"); return v && v[0] ? std::max(4, std::atoi(v)) : 0; }();
+  if (r) return r;
+  return (M + 31) / 32 >= 512 ? 32 : 16;
 }
-int ln_blocks(int M) { return min(8192, max(1, (M + ln_rpb() - 1) / ln_rpb())); }
+int ln_blocks(int M) { return min(8192, max(1, (M + ln_rpb(M) - 1) / ln_rpb(M))); }
 // rows in flight per wave in the bf16 LayerNorm backward (FS2_LN_ROWS=1 selects the one-row
 // kernel for A/B runs)
 int ln_rows_r() {
