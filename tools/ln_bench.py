@@ -62,5 +62,37 @@ def main():
                 print(f"M={M} torch {name:12s} {us:7.1f} us", flush=True)
 
 
+def postnet_case():
+    """PostNet LayerNorm backward: D = 512, tanh gate, output dropout, gamma / beta / bias
+    partials, no residual-branch output (engine._postnet_bwd)."""
+    from fastspeech2 import ops
+    M, D = 31264, 512
+    bf = torch.bfloat16
+    X = (torch.randn(M, D, device="cuda") * 0.5).to(bf)
+    dY = (torch.randn(M, D, device="cuda") * 0.5).to(bf)
+    g, be = torch.rand(D, device="cuda") + 0.5, torch.randn(D, device="cuda") * 0.1
+    Y = torch.empty_like(X)
+    mean = torch.empty(M, device="cuda")
+    rstd = torch.empty_like(mean)
+    ops.ln_fwd(X, D, g, be, 1e-5, Y, D, mean, rstd, M, D, dt=1, seed=7, do_tanh=1, p_o=0.5,
+               salt_o=5)
+    dS = torch.empty_like(X)
+    dg, db, dc = (torch.zeros(D, device="cuda") for _ in range(3))
+    ws = torch.empty(int(ops.ln_ws(M, D)), device="cuda")
+    bwd = lambda: ops.ln_bwd(dY, D, X, D, mean, rstd, g, be, dS, D, M, D, dt=1, ws=ws, seed=7,
+                             do_tanh=1, p_o=0.5, salt_o=5, dgamma=dg, dbeta=db, dcol=dc)
+    us = timed(bwd)
+    print(f"M={M} D=512 tanh ln_bwd {us:7.1f} us  {4 * M * D * 2 / us / 1e3:7.0f} GB/s", flush=True)
+    fwd = lambda: ops.ln_fwd(X, D, g, be, 1e-5, Y, D, mean, rstd, M, D, dt=1, seed=7, do_tanh=1,
+                             p_o=0.5, salt_o=5)
+    us = timed(fwd)
+    print(f"M={M} D=512 tanh ln_fwd {us:7.1f} us", flush=True)
+
+
 if __name__ == "__main__":
+    if os.environ.get("LN_POSTNET"):
+        from fastspeech2 import _native
+        _native.load()
+        postnet_case()
+        sys.exit(0)
     main()
