@@ -3,14 +3,20 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
 
-N>1 is launched by torch.distributed.run (one process per GPU, RCCL all-reduce).  A step is
-forward + loss + backward + bucketed all-reduce + AdamW over one synthetic EmoV-DB-shaped
-batch per rank, inputs resident in HBM.  Prints ONE JSON line on rank 0.
+N>1: one process per GPU with the nccl (= RCCL) backend.  Under torch.distributed.run (the
+driver's launch: WORLD_SIZE/RANK/LOCAL_RANK in the environment) WORLD_SIZE must equal --gpus.
+Started directly with --gpus N > 1, bench.py first checks that N devices are visible (without
+initialising the GPU) and then runs itself under ``torch.distributed.run --nproc-per-node N``
+as a child process, exiting with its status.  A step is forward + loss + backward + bucketed
+all-reduce + AdamW over one synthetic EmoV-DB-shaped batch per rank, inputs
+resident in HBM.  Prints ONE JSON line on rank 0.
 """
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -24,9 +30,48 @@ import torch.distributed as dist
 MFMA_BF16_PEAK_TFLOPS = 2500.0   # MI355X dense bf16 (MI355X_MICROARCH.md)
 
 
-def parse():
+class LaunchError(RuntimeError):
+    pass
+
+
+def _free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_plan(gpus, env, visible_devices, argv, port=None):
+    """What ``bench.py --gpus N`` does in this process: ``None`` = run the bench here (this
+    process is one rank, or N == 1), else the child command line that runs N ranks.
+
+    * WORLD_SIZE set (launched by torch.distributed.run): it must equal ``gpus``.
+    * WORLD_SIZE unset and gpus > 1: needs ``visible_devices >= gpus``, then returns
+      ``python -m torch.distributed.run --nnodes=1 --nproc-per-node gpus --master-addr
+      127.0.0.1 --master-port P bench.py <argv>``."""
+    if gpus < 1:
+        raise LaunchError(f"--gpus {gpus}: need at least one GPU")
+    ws = env.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != gpus:
+            raise LaunchError(f"WORLD_SIZE={ws} but --gpus {gpus}: the launcher and the "
+                              f"bench disagree on the number of ranks")
+        return None
+    if gpus == 1:
+        return None
+    if visible_devices < gpus:
+        raise LaunchError(f"--gpus {gpus} but only {visible_devices} GPU(s) visible: refusing "
+                          f"to measure fewer GPUs than asked")
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+            f"--nproc-per-node={gpus}", "--master-addr=127.0.0.1",
+            f"--master-port={port or _free_port()}", os.path.abspath(__file__)] + list(argv)
+
+
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--plumbing-check", action="store_true",
+                    help="CPU test of the launcher: each rank joins a gloo group, rank 0 prints "
+                         "the world size and the ranks seen; no GPU is touched")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=32)
@@ -48,7 +93,7 @@ def parse():
                     help="HIP-event time every GEMM / attention call site; table on stderr")
     ap.add_argument("--no-extractor", action="store_true",
                     help="skip the second timed loop that adds the frozen IntensityExtractor")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 def scaled_config(cfg_all):
@@ -245,11 +290,47 @@ def extractor_leg(cfg_all, args, trainer, b, bt, Tm, dt, world, frames_local):
                     "(train.py:69-81); extractor weights random-init, rank_X from the batch"}
 
 
+def plumbing_check(world, rank, local):
+    """--plumbing-check: the rank environment the launcher produced, gathered over gloo."""
+    if world > 1:
+        dist.init_process_group("gloo")
+    mine = torch.tensor([rank, local, world], dtype=torch.int64)
+    got = [torch.zeros_like(mine) for _ in range(world)]
+    if world > 1:
+        dist.all_gather(got, mine)
+    else:
+        got = [mine]
+    if rank == 0:
+        print(json.dumps({"plumbing": True, "n_gpus": world, "parallelism": f"dp{world}",
+                          "ranks": [int(g[0]) for g in got],
+                          "local_ranks": [int(g[1]) for g in got],
+                          "world_sizes": [int(g[2]) for g in got]}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    try:
+        # torch.cuda.device_count() does not initialise the GPU on this stack, so the child
+        # ranks start from a process that never touched the device
+        visible = args.gpus if args.plumbing_check else torch.cuda.device_count()
+        cmd = launch_plan(args.gpus, os.environ, visible, sys.argv[1:])
+    except LaunchError as e:
+        print(f"bench.py: {e}", file=sys.stderr)
+        sys.exit(2)
+    if cmd is not None:
+        sys.exit(subprocess.run(cmd).returncode)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.plumbing_check:
+        plumbing_check(world, rank, local)
+        return
+    if local >= torch.cuda.device_count():
+        print(f"bench.py: LOCAL_RANK {local} but only {torch.cuda.device_count()} GPU(s) "
+              f"visible", file=sys.stderr)
+        sys.exit(2)
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))

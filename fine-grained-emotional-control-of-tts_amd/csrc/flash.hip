@@ -53,7 +53,6 @@ struct AttnP {
   float scale, scale_log2, p_drop, inv_keep;
   uint32_t seed, salt;
   uint32_t thr16;                // dropout threshold (fs2_thr16)
-  int dsum_in;                   // backward: dsum already computed (attn_dsum_kernel)
 };
 
 __device__ __forceinline__ bf16x8 ld_frag(const bf16* g) { return *(const bf16x8*)g; }
@@ -381,23 +380,17 @@ __global__ void __launch_bounds__(W8 * 64 / QG, 1) attn_bwd_dq_kernel(AttnP p) {
         qf[qg][s] = ld_frag(Qb + (long)qi[qg] * p.ldq + 32 * s + 8 * g);
         const long ro = (long)b * p.T + qi[qg];
         dof[qg][s] = ld_frag(p.dout + ro * p.lddo + h * DH + 32 * s + 8 * g);
-        if (!p.dsum_in) {
-          const bf16x8 of = ld_frag(p.o + ro * p.ldo + h * DH + 32 * s + 8 * g);
+        const bf16x8 of = ld_frag(p.o + ro * p.ldo + h * DH + 32 * s + 8 * g);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) dot += (float)dof[qg][s][e] * (float)of[e];
-        }
+        for (int e = 0; e < 8; ++e) dot += (float)dof[qg][s][e] * (float)of[e];
       } else {
         qf[qg][s] = bf16x8{};
         dof[qg][s] = bf16x8{};
       }
     }
     lse[qg] = in ? p.lse[(long)z * p.T + qi[qg]] : 0.f;
-    if (p.dsum_in) {
-      dsum[qg] = in ? p.dsum[(long)z * p.T + qi[qg]] : 0.f;
-    } else {
-      dsum[qg] = xg_sum(dot);
-      if (in && g == 0) p.dsum[(long)z * p.T + qi[qg]] = dsum[qg];
-    }
+    dsum[qg] = xg_sum(dot);
+    if (in && g == 0) p.dsum[(long)z * p.T + qi[qg]] = dsum[qg];
   }
   f32x4 qacc[ND][QG];
 #pragma unroll
@@ -498,33 +491,6 @@ __global__ void __launch_bounds__(W8 * 64 / QG, 1) attn_bwd_dq_kernel(AttnP p) {
       *(u32x2*)(row + 16 * d + 4 * g) = w;
     }
   }
-}
-
-// ------------------------------------------------------------------------------ backward D
-// D[z][q] = rowsum(dO * O) over head h's dh features, with the lane mapping and summation order
-// of the dQ kernel's own computation (lane = 16 g + row: features 32 s + 8 g + e summed over
-// s then e, then across g by xg_sum), so the values are bit-identical.  Lets the dQ and dK/dV
-// kernels run concurrently (the dK/dV kernel reads D).  One wave = 16 query rows of one z.
-template <int DH>
-__global__ void __launch_bounds__(256) attn_dsum_kernel(AttnP p) {
-  constexpr int NS = DH / 32;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
-  const int z = blockIdx.y, b = z / p.H, h = z - b * p.H;
-  const int q = (blockIdx.x * 4 + wave) * 16 + (lane & 15);
-  const bool in = q < p.T;
-  float dot = 0.f;
-  if (in) {
-    const long ro = (long)b * p.T + q;
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      const bf16x8 df = ld_frag(p.dout + ro * p.lddo + h * DH + 32 * s + 8 * g);
-      const bf16x8 of = ld_frag(p.o + ro * p.ldo + h * DH + 32 * s + 8 * g);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) dot += (float)df[e] * (float)of[e];
-    }
-  }
-  const float d = xg_sum(dot);
-  if (in && g == 0) p.dsum[(long)z * p.T + q] = d;
 }
 
 // ------------------------------------------------------------------------------ backward dK dV
@@ -689,584 +655,30 @@ __global__ void __launch_bounds__(W8 * 64, 1) attn_bwd_dkv_kernel(AttnP p) {
   }
 }
 
-// ============================================================================================
-// 32x32x16 kernels (v_mfma_f32_32x32x16_bf16), one 32-token block per wave.
-//
-// A 32x32 MFMA consumes 2 x 1 KiB of operands per 32 KFLOP, half the operand bytes per FLOP of
-// the 16x16x32 form above, so every LDS-resident tile feeds twice the MFMA work per read (the
-// dK/dV kernel above re-read its Q / dO tile once per 16 keys: LDS traffic matched the MFMA
-// cycles one for one).  Orientation (CDNA4 guide: "an accumulator tile as the next MFMA's
-// operand"): each softmax-side product is computed so that its 32x32 f32 result X has the
-// token that owns the row statistics on the lane and the summed-over index on the registers;
-// the following product takes X as its B operand with no lane movement (registers 8s..8s+7
-// packed to bf16 = k-step s, k order permuted: element j of lane half h is row
-// 16s + 8(j>>2) + 4h + (j&3) of X), and the other operand is read transposed from LDS with
-// ds_read_b64_tr_b16 over exactly those rows.  Outputs come out with features on the
-// registers and tokens on the lanes: 8-byte stores of 4 consecutive features.
-//   forward:  S^T = K Q^T (lanes own queries)  ->  O^T  += V^T  P^T
-//   dQ:       S^T = K Q^T, dP^T = V dO^T        ->  dQ^T += K^T  dS^T
-//   dK, dV:   S = Q K^T,   dP = dO V^T (lanes own keys) -> dV^T += dO^T Pd,  dK^T += Q^T dS
-// LDS tile images: 8-row x 32-feature subtiles of 512 B, 16-byte chunk (c & 3) ^ ((row>>2) & 3)
-// inside a subtile: conflict-free for both the 32x32x16 row reads (ds_read_b128) and the
-// transposed reads (bank model check: scratch-free, tools/lds_banks.py).
-typedef __attribute__((ext_vector_type(16))) float f32x16;
-
-__device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-}
-
-template <int DH>
-__device__ __forceinline__ int img32(int r, int c) {
-  return (r >> 3) * (16 * DH) + 512 * (c >> 2) + 64 * (r & 7) + 16 * ((c & 3) ^ ((r >> 2) & 3));
-}
-
-// row-operand fragment (A[row][k] or B[k][col] with the token on the lane): rows r0..r0+31 of
-// the tile, features 16 s + 8 h .. +7
-template <int DH>
-__device__ __forceinline__ bf16x8 row32(const char* t, int r0, int s, int lane) {
-  return *(const bf16x8*)(t + img32<DH>(r0 + (lane & 31), 2 * s + (lane >> 5)));
-}
-
-// transposed fragment: the operand whose k index runs over tile rows kb + {4h..4h+3} (j < 4)
-// and kb + 8 + {4h..4h+3} (j >= 4), feature (the lane's row / column) fb + (lane & 31)
-template <int DH>
-__device__ __forceinline__ bf16x8 tr32(const char* t, int kb, int fb, int lane) {
-  const int li = lane & 15, q = li >> 2, p = li & 3, h = lane >> 5, c16 = (lane >> 4) & 1;
-  const int col = fb + 16 * c16 + 4 * p;
-  const int c = col >> 3, boff = (col & 4) * 2;
-  const int r1 = kb + 4 * h + q;
-  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(t + img32<DH>(r1, c) + boff));
-  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(t + img32<DH>(r1 + 8, c) + boff));
-  const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(bf16x8, v);
-}
-
-// registers 8s .. 8s+7 of an accumulator as a bf16 operand fragment (k-step s)
-__device__ __forceinline__ bf16x8 pack_acc(const float* x, int s) {
-  bf16x8 r;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = (bf16)x[8 * s + j];
-  return r;
-}
-
-// TR-row x DH tile filled by LDS-DMA into the img32 image: 1 KiB instruction i covers image
-// bytes [1024 i, 1024 i + 1024); each lane fetches the logical chunk that lands at its slot.
-template <int DH, int TR, int NW>
-struct TileDma32 {
-  static constexpr int NI = TR * DH * 2 / 1024;
-  static constexpr int PER = NI / NW;
-  static_assert(NI % NW == 0, "tile instructions must split evenly over the waves");
-  __device__ __forceinline__ void issue(char* tile, i32x4 rs, long ld, int r0, int nrows,
-                                        int wave, int lane) const {
-#pragma unroll
-    for (int j = 0; j < PER; ++j) {
-      const int o = (wave + j * NW) * 1024 + lane * 16;
-      const int rg = o / (16 * DH), rem = o - rg * 16 * DH;
-      const int rem2 = rem & 511, r7 = rem2 >> 6;
-      const int r = rg * 8 + r7;
-      const int c = (rem >> 9) * 4 + (((rem2 >> 4) & 3) ^ ((r >> 2) & 3));
-      const int vo = (r * (int)ld + c * 8) * 2;
-      blds16(rs, r0 + r < nrows ? vo : BUF_OOB, (int)((long)r0 * ld * 2),
-             tile + (wave + j * NW) * 1024);
-    }
-  }
-};
-
-// 8-byte store of 4 consecutive features (registers 4i..4i+3 of a 32x32 result block)
-__device__ __forceinline__ void store4(bf16* dst, const float* v, float sc) {
-  u32x2 w;
-  w[0] = (unsigned)__builtin_bit_cast(unsigned short, (bf16)(v[0] * sc)) |
-         ((unsigned)__builtin_bit_cast(unsigned short, (bf16)(v[1] * sc)) << 16);
-  w[1] = (unsigned)__builtin_bit_cast(unsigned short, (bf16)(v[2] * sc)) |
-         ((unsigned)__builtin_bit_cast(unsigned short, (bf16)(v[3] * sc)) << 16);
-  *(u32x2*)dst = w;
-}
-
-// ------------------------------------------------------------------------------ forward (32)
-// block: NW waves x 32 queries; K/V tiles of TR keys double-buffered through LDS-DMA
-template <int DH, int NW, int TR>
-__global__ void __launch_bounds__(NW * 64) attn_fwd32_kernel(AttnP p) {
-  constexpr int NK = DH / 16, NB = DH / 32, KB = TR / 32;
-  constexpr int TB = TR * DH * 2;
-  __shared__ __attribute__((aligned(16))) char smem[4 * TB + TMAX + 16];
-  uint8_t* kval = (uint8_t*)(smem + 4 * TB);
-  int& kend_s = *(int*)(smem + 4 * TB + TMAX);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hh = lane >> 5;
-  const int z = blockIdx.y, b = z / p.H, h = z - b * p.H;
-  const uint32_t dkey = fs2_drop_key(p.seed, p.salt);
-  const uint64_t T2 = (uint64_t)((p.T + 1) & ~1);
-  const int kend = build_kvalid(kval, &kend_s, p, b, h);
-  const bf16* Qb = p.qkv + (long)b * p.T * p.ldq + h * DH;
-  const bf16* Kb = Qb + p.D;
-  const bf16* Vb = Qb + 2 * p.D;
-  const int qi = blockIdx.x * (32 * NW) + wave * 32 + (lane & 31);
-  const bool qin = qi < p.T;
-  bf16x8 qf[NK];
-#pragma unroll
-  for (int s = 0; s < NK; ++s)
-    qf[s] = qin ? ld_frag(Qb + (long)qi * p.ldq + 16 * s + 8 * hh) : bf16x8{};
-  f32x16 oacc[NB];
-#pragma unroll
-  for (int d = 0; d < NB; ++d) oacc[d] = f32x16{};
-  float mrow = -INFINITY, lrow = 0.f;
-  const uint64_t rowi = ((uint64_t)z * p.T + qi) * T2;
-
-  TileDma32<DH, TR, NW> dma;
-  const i32x4 rsK = make_rsrc(Kb), rsV = make_rsrc(Vb);
-  const int ntile = (kend + TR - 1) / TR;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (ntile > 0) {
-    dma.issue(smem, rsK, p.ldq, 0, p.T, wave, lane);
-    dma.issue(smem + TB, rsV, p.ldq, 0, p.T, wave, lane);
-  }
-  for (int t = 0; t < ntile; ++t) {
-    const int k0 = t * TR;
-    const char* Ks = smem + (t & 1) * 2 * TB;
-    const char* Vs = Ks + TB;
-    if (t + 1 < ntile) {
-      char* nx = smem + ((t + 1) & 1) * 2 * TB;
-      dma.issue(nx, rsK, p.ldq, k0 + TR, p.T, wave, lane);
-      dma.issue(nx + TB, rsV, p.ldq, k0 + TR, p.T, wave, lane);
-      wait_vmcnt<2 * TileDma32<DH, TR, NW>::PER>();
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    f32x16 sacc[KB];
-#pragma unroll
-    for (int kb = 0; kb < KB; ++kb) sacc[kb] = f32x16{};
-#pragma unroll
-    for (int s = 0; s < NK; ++s)
-#pragma unroll
-      for (int kb = 0; kb < KB; ++kb)
-        sacc[kb] = mfma32(row32<DH>(Ks, kb * 32, s, lane), qf[s], sacc[kb]);
-    // online softmax over this tile's keys (32 per lane half; the halves exchange by xor 32)
-    float v[KB][16];
-    float mt = -INFINITY;
-#pragma unroll
-    for (int kb = 0; kb < KB; ++kb)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = k0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        const bool ok = key < p.T && kval[key];
-        v[kb][r] = ok ? sacc[kb][r] * p.scale_log2 : -INFINITY;
-        mt = fmaxf(mt, v[kb][r]);
-      }
-    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-    const float mnew = fmaxf(mrow, mt);
-    const float alpha = mnew == -INFINITY ? 1.f : fexp2(mrow - mnew);
-    mrow = mnew;
-    float ls = 0.f;
-#pragma unroll
-    for (int kb = 0; kb < KB; ++kb)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float e = v[kb][r] == -INFINITY ? 0.f : fexp2(v[kb][r] - mnew);
-        ls += e;
-        v[kb][r] = e;
-      }
-    if (p.p_drop > 0.f) {
-#pragma unroll
-      for (int kb = 0; kb < KB; ++kb)
-#pragma unroll
-        for (int r = 0; r < 16; r += 2) {
-          const uint64_t idx = rowi + k0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;   // even
-          const uint32_t hs = fs2_hash_pair(dkey, idx >> 1);
-          v[kb][r] = fs2_keep_pair_bit(hs, idx, p.thr16) ? v[kb][r] * p.inv_keep : 0.f;
-          v[kb][r + 1] = fs2_keep_pair_bit(hs, idx + 1, p.thr16) ? v[kb][r + 1] * p.inv_keep : 0.f;
-        }
-    }
-    ls += __shfl_xor(ls, 32, 64);
-    lrow = lrow * alpha + ls;
-#pragma unroll
-    for (int d = 0; d < NB; ++d) oacc[d] *= alpha;
-#pragma unroll
-    for (int kb = 0; kb < KB; ++kb)
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const bf16x8 pf = pack_acc(v[kb], s2);
-#pragma unroll
-        for (int d = 0; d < NB; ++d)
-          oacc[d] = mfma32(tr32<DH>(Vs, kb * 32 + 16 * s2, 32 * d, lane), pf, oacc[d]);
-      }
-    __builtin_amdgcn_s_barrier();
-  }
-  if (!qin) return;
-  const float inv = 1.f / lrow;
-  if (hh == 0) p.lse[(long)z * p.T + qi] = mrow + log2f(lrow);
-  bf16* orow = p.out + ((long)b * p.T + qi) * p.ldout + h * DH;
-#pragma unroll
-  for (int d = 0; d < NB; ++d)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      float w4[4] = {oacc[d][4 * i], oacc[d][4 * i + 1], oacc[d][4 * i + 2], oacc[d][4 * i + 3]};
-      store4(orow + 32 * d + 8 * i + 4 * hh, w4, inv);
-    }
-}
-
-// D[z][q] = rowsum(dO * O) in the 32-kernel lane order (lane = query, half hh holds features
-// 16 s + 8 hh + e; summed over s then e, then across the halves), so the staged backward and
-// the dQ kernel's own computation agree bit for bit.  One wave = 32 queries of one z.
-template <int DH>
-__device__ __forceinline__ float dsum32(const AttnP& p, int b, int h, int q, int hh) {
-  float dot = 0.f;
-  if (q < p.T) {
-    const long ro = (long)b * p.T + q;
-#pragma unroll
-    for (int s = 0; s < DH / 16; ++s) {
-      const bf16x8 df = ld_frag(p.dout + ro * p.lddo + h * DH + 16 * s + 8 * hh);
-      const bf16x8 of = ld_frag(p.o + ro * p.ldo + h * DH + 16 * s + 8 * hh);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) dot += (float)df[e] * (float)of[e];
-    }
-  }
-  return dot + __shfl_xor(dot, 32, 64);
-}
-
-template <int DH>
-__global__ void __launch_bounds__(256) attn_dsum32_kernel(AttnP p) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int z = blockIdx.y, b = z / p.H, h = z - b * p.H;
-  const int q = (blockIdx.x * 4 + wave) * 32 + (lane & 31);
-  const float d = dsum32<DH>(p, b, h, q, lane >> 5);
-  if (q < p.T && lane < 32) p.dsum[(long)z * p.T + q] = d;
-}
-
-// ------------------------------------------------------------------------------ dQ (32)
-template <int DH, int NW, int TR>
-__global__ void __launch_bounds__(NW * 64, 1) attn_dq32_kernel(AttnP p) {
-  constexpr int NK = DH / 16, NB = DH / 32, KB = TR / 32;
-  constexpr int TB = TR * DH * 2;
-  __shared__ __attribute__((aligned(16))) char smem[4 * TB + TMAX + 16];
-  uint8_t* kval = (uint8_t*)(smem + 4 * TB);
-  int& kend_s = *(int*)(smem + 4 * TB + TMAX);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hh = lane >> 5;
-  const int z = blockIdx.y, b = z / p.H, h = z - b * p.H;
-  const uint32_t dkey = fs2_drop_key(p.seed, p.salt);
-  const uint64_t T2 = (uint64_t)((p.T + 1) & ~1);
-  const int kend = build_kvalid(kval, &kend_s, p, b, h);
-  const bf16* Qb = p.qkv + (long)b * p.T * p.ldq + h * DH;
-  const bf16* Kb = Qb + p.D;
-  const bf16* Vb = Qb + 2 * p.D;
-  const int qi = blockIdx.x * (32 * NW) + wave * 32 + (lane & 31);
-  const bool qin = qi < p.T;
-  bf16x8 qf[NK], dof[NK];
-  const long ro = (long)b * p.T + qi;
-#pragma unroll
-  for (int s = 0; s < NK; ++s) {
-    qf[s] = qin ? ld_frag(Qb + (long)qi * p.ldq + 16 * s + 8 * hh) : bf16x8{};
-    dof[s] = qin ? ld_frag(p.dout + ro * p.lddo + h * DH + 16 * s + 8 * hh) : bf16x8{};
-  }
-  const float lse = qin ? p.lse[(long)z * p.T + qi] : 0.f;
-  float dsum;
-  if (p.dsum_in) {
-    dsum = qin ? p.dsum[(long)z * p.T + qi] : 0.f;
-  } else {
-    dsum = dsum32<DH>(p, b, h, qi, hh);
-    if (qin && hh == 0) p.dsum[(long)z * p.T + qi] = dsum;
-  }
-  f32x16 qacc[NB];
-#pragma unroll
-  for (int d = 0; d < NB; ++d) qacc[d] = f32x16{};
-  const uint64_t rowi = ((uint64_t)z * p.T + qi) * T2;
-
-  TileDma32<DH, TR, NW> dma;
-  const i32x4 rsK = make_rsrc(Kb), rsV = make_rsrc(Vb);
-  const int ntile = (kend + TR - 1) / TR;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (ntile > 0) {
-    dma.issue(smem, rsK, p.ldq, 0, p.T, wave, lane);
-    dma.issue(smem + TB, rsV, p.ldq, 0, p.T, wave, lane);
-  }
-  for (int t = 0; t < ntile; ++t) {
-    const int k0 = t * TR;
-    const char* Ks = smem + (t & 1) * 2 * TB;
-    const char* Vs = Ks + TB;
-    if (t + 1 < ntile) {
-      char* nx = smem + ((t + 1) & 1) * 2 * TB;
-      dma.issue(nx, rsK, p.ldq, k0 + TR, p.T, wave, lane);
-      dma.issue(nx + TB, rsV, p.ldq, k0 + TR, p.T, wave, lane);
-      wait_vmcnt<2 * TileDma32<DH, TR, NW>::PER>();
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int kb = 0; kb < KB; ++kb) {
-      f32x16 sacc = f32x16{}, pacc = f32x16{};
-#pragma unroll
-      for (int s = 0; s < NK; ++s) {
-        sacc = mfma32(row32<DH>(Ks, kb * 32, s, lane), qf[s], sacc);
-        pacc = mfma32(row32<DH>(Vs, kb * 32, s, lane), dof[s], pacc);
-      }
-      float ds[16];
-#pragma unroll
-      for (int r = 0; r < 16; r += 2) {
-        const int key = k0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;   // even
-        const uint32_t hs = p.p_drop > 0.f ? fs2_hash_pair(dkey, (rowi + key) >> 1) : 0u;
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const bool ok = key + e < p.T && kval[key + e];
-          const float pr = ok ? fexp2(sacc[r + e] * p.scale_log2 - lse) : 0.f;
-          float dp = pacc[r + e];
-          if (p.p_drop > 0.f) dp = fs2_keep_pair_bit(hs, rowi + key + e, p.thr16) ? dp * p.inv_keep : 0.f;
-          ds[r + e] = pr * (dp - dsum);
-        }
-      }
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const bf16x8 sf = pack_acc(ds, s2);
-#pragma unroll
-        for (int d = 0; d < NB; ++d)
-          qacc[d] = mfma32(tr32<DH>(Ks, kb * 32 + 16 * s2, 32 * d, lane), sf, qacc[d]);
-      }
-    }
-    __builtin_amdgcn_s_barrier();
-  }
-  if (!qin) return;
-  bf16* row = p.dqkv + ro * p.lddq + h * DH;
-#pragma unroll
-  for (int d = 0; d < NB; ++d)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      float w4[4] = {qacc[d][4 * i], qacc[d][4 * i + 1], qacc[d][4 * i + 2], qacc[d][4 * i + 3]};
-      store4(row + 32 * d + 8 * i + 4 * hh, w4, p.scale);
-    }
-}
-
-// ------------------------------------------------------------------------------ dK dV (32)
-// block: NW waves x 32 keys; query tiles of TR (Q, dO by LDS-DMA, lse / D rows by 4-byte
-// LDS-DMA from wave 0), double-buffered
-template <int DH, int NW, int TR>
-__global__ void __launch_bounds__(NW * 64, 1) attn_dkv32_kernel(AttnP p) {
-  constexpr int NK = DH / 16, NB = DH / 32, QB = TR / 32;
-  constexpr int TB = TR * DH * 2;
-  __shared__ __attribute__((aligned(16))) char smem[4 * TB + 4 * TR * 4 + TMAX + 16];
-  float* lsd = (float*)(smem + 4 * TB);                 // [buf][lse TR | D TR]
-  uint8_t* kval = (uint8_t*)(smem + 4 * TB + 4 * TR * 4);
-  int& kend_s = *(int*)(smem + 4 * TB + 4 * TR * 4 + TMAX);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hh = lane >> 5;
-  const int z = blockIdx.y, b = z / p.H, h = z - b * p.H;
-  const uint32_t dkey = fs2_drop_key(p.seed, p.salt);
-  const uint64_t T2 = (uint64_t)((p.T + 1) & ~1);
-  build_kvalid(kval, &kend_s, p, b, h);
-  const bf16* Qb = p.qkv + (long)b * p.T * p.ldq + h * DH;
-  const bf16* Kb = Qb + p.D;
-  const bf16* Vb = Qb + 2 * p.D;
-  const bf16* dOb = p.dout + (long)b * p.T * p.lddo + h * DH;
-  const int key = blockIdx.x * (32 * NW) + wave * 32 + (lane & 31);
-  const bool kin = key < p.T;
-  const bool kok = kin && kval[key];
-  bf16x8 kf[NK], vf[NK];
-#pragma unroll
-  for (int s = 0; s < NK; ++s) {
-    kf[s] = kin ? ld_frag(Kb + (long)key * p.ldq + 16 * s + 8 * hh) : bf16x8{};
-    vf[s] = kin ? ld_frag(Vb + (long)key * p.ldq + 16 * s + 8 * hh) : bf16x8{};
-  }
-  f32x16 dk[NB], dv[NB];
-#pragma unroll
-  for (int d = 0; d < NB; ++d) { dk[d] = f32x16{}; dv[d] = f32x16{}; }
-  const int anyk = __syncthreads_or(kok);
-
-  TileDma32<DH, TR, NW> dma;
-  const i32x4 rsQ = make_rsrc(Qb), rsO = make_rsrc(dOb);
-  const int ntile = anyk ? (p.T + TR - 1) / TR : 0;
-  const i32x4 rsL = make_rsrc(p.lse + (long)z * p.T), rsD = make_rsrc(p.dsum + (long)z * p.T);
-  auto issue_stats = [&](int q0, int buf) {
-    if (wave == 0) {
-#pragma unroll
-      for (int c = 0; c < TR / 64; ++c) {
-        const int vo = q0 + 64 * c + lane < p.T ? lane * 4 : BUF_OOB;
-        blds4(rsL, vo, (q0 + 64 * c) * 4, (char*)(lsd + buf * 2 * TR + 64 * c));
-        blds4(rsD, vo, (q0 + 64 * c) * 4, (char*)(lsd + buf * 2 * TR + TR + 64 * c));
-      }
-    }
-  };
-  constexpr int NSTAT = TR / 64 * 2;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (ntile > 0) {
-    issue_stats(0, 0);
-    dma.issue(smem, rsQ, p.ldq, 0, p.T, wave, lane);
-    dma.issue(smem + TB, rsO, p.lddo, 0, p.T, wave, lane);
-  }
-  for (int t = 0; t < ntile; ++t) {
-    const int q0 = t * TR;
-    const char* Qs = smem + (t & 1) * 2 * TB;
-    const char* Os = Qs + TB;
-    const float* ls_s = lsd + (t & 1) * 2 * TR;
-    const float* ds_s = ls_s + TR;
-    if (t + 1 < ntile) {
-      issue_stats(q0 + TR, (t + 1) & 1);
-      char* nx = smem + ((t + 1) & 1) * 2 * TB;
-      dma.issue(nx, rsQ, p.ldq, q0 + TR, p.T, wave, lane);
-      dma.issue(nx + TB, rsO, p.lddo, q0 + TR, p.T, wave, lane);
-      if (wave == 0) wait_vmcnt<2 * TileDma32<DH, TR, NW>::PER + NSTAT>();
-      else wait_vmcnt<2 * TileDma32<DH, TR, NW>::PER>();
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int qb = 0; qb < QB; ++qb) {
-      f32x16 sacc = f32x16{}, pacc = f32x16{};
-#pragma unroll
-      for (int s = 0; s < NK; ++s) {
-        sacc = mfma32(row32<DH>(Qs, qb * 32, s, lane), kf[s], sacc);
-        pacc = mfma32(row32<DH>(Os, qb * 32, s, lane), vf[s], pacc);
-      }
-      float pd[16], dsv[16];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int ql = qb * 32 + 8 * i + 4 * hh;
-        const f32x4 l4 = *(const f32x4*)(ls_s + ql);
-        const f32x4 d4 = *(const f32x4*)(ds_s + ql);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int q = q0 + ql + r;
-          const bool ok = kok && q < p.T;
-          const float pr = ok ? fexp2(sacc[4 * i + r] * p.scale_log2 - l4[r]) : 0.f;
-          float dp = pacc[4 * i + r];
-          float pdr = pr;
-          if (p.p_drop > 0.f) {
-            const bool keep = fs2_keep_fast(dkey, ((uint64_t)z * p.T + q) * T2 + key, p.thr16);
-            dp = keep ? dp * p.inv_keep : 0.f;
-            pdr = keep ? pr * p.inv_keep : 0.f;
-          }
-          pd[4 * i + r] = pdr;
-          dsv[4 * i + r] = pr * (dp - d4[r]);
-        }
-      }
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const bf16x8 pa = pack_acc(pd, s2);
-        const bf16x8 sa = pack_acc(dsv, s2);
-#pragma unroll
-        for (int d = 0; d < NB; ++d) {
-          dv[d] = mfma32(tr32<DH>(Os, qb * 32 + 16 * s2, 32 * d, lane), pa, dv[d]);
-          dk[d] = mfma32(tr32<DH>(Qs, qb * 32 + 16 * s2, 32 * d, lane), sa, dk[d]);
-        }
-      }
-    }
-    __builtin_amdgcn_s_barrier();
-  }
-  if (!kin) return;
-  bf16* krow = p.dqkv + ((long)b * p.T + key) * p.lddq + p.D + h * DH;
-  bf16* vrow = krow + p.D;
-#pragma unroll
-  for (int d = 0; d < NB; ++d)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      float k4[4] = {dk[d][4 * i], dk[d][4 * i + 1], dk[d][4 * i + 2], dk[d][4 * i + 3]};
-      float v4[4] = {dv[d][4 * i], dv[d][4 * i + 1], dv[d][4 * i + 2], dv[d][4 * i + 3]};
-      store4(krow + 32 * d + 8 * i + 4 * hh, k4, p.scale);
-      store4(vrow + 32 * d + 8 * i + 4 * hh, v4, 1.f);
-    }
-}
-
-// The 32x32 kernels (dh 64 / 128 / 192; dh 256 would need 256 accumulator registers per lane
-// for dK/dV alone) are opt-in, FS2_ATTN_V32=1 (read per launch, so a test can switch it):
-// parity-green, but measured slower than the 16x16 kernels in round 2 (decoder fwd 117.5 vs
-// 112 us, bwd 391 vs 320 us per layer): at one wave per SIMD the compiler exposes the LDS read
-// latency (lgkmcnt(0) before most MFMAs) and moves the dK/dV accumulators between the AGPR and
-// VGPR files (810 v_accvgpr moves per tile), which costs more than the halved LDS traffic saves.
-bool attn_v32(int dh) {
-  const char* v = std::getenv("FS2_ATTN_V32");
-  return v && v[0] == '1' && dh <= 192;
-}
-
-template <int DH, int NW, int TR>
-void fwd32(const AttnP& p, hipStream_t s) {
-  hipLaunchKernelGGL((attn_fwd32_kernel<DH, NW, TR>), dim3((p.T + 32 * NW - 1) / (32 * NW), p.B * p.H),
-                     dim3(NW * 64), 0, s, p);
-}
-template <int DH>
-void launch_fwd32(const AttnP& p, hipStream_t s) {
-  // widest block (fewest K/V tile re-reads) that still gives >= 256 blocks
-  const long bh = (long)p.B * p.H;
-  if ((p.T + 255) / 256 * bh >= 256) fwd32<DH, 8, 64>(p, s);
-  else if ((p.T + 127) / 128 * bh >= 256) fwd32<DH, 4, 64>(p, s);
-  else fwd32<DH, 2, 32>(p, s);
-}
-template <int DH>
-void launch_bwd32(const AttnP& p, hipStream_t s, int stage) {
-  const long bh = (long)p.B * p.H;
-  const bool wide = (p.T + 127) / 128 * bh >= 256;
-  if (stage == 0) {
-    hipLaunchKernelGGL(attn_dsum32_kernel<DH>, dim3((p.T + 127) / 128, p.B * p.H), dim3(256), 0, s, p);
-    return;
-  }
-  if (stage != 2) {
-    if (wide) hipLaunchKernelGGL((attn_dq32_kernel<DH, 4, 64>), dim3((p.T + 127) / 128, p.B * p.H), dim3(256), 0, s, p);
-    else hipLaunchKernelGGL((attn_dq32_kernel<DH, 2, 32>), dim3((p.T + 63) / 64, p.B * p.H), dim3(128), 0, s, p);
-  }
-  if (stage != 1) {
-    if (wide) hipLaunchKernelGGL((attn_dkv32_kernel<DH, 4, 64>), dim3((p.T + 127) / 128, p.B * p.H), dim3(256), 0, s, p);
-    else hipLaunchKernelGGL((attn_dkv32_kernel<DH, 2, 64>), dim3((p.T + 63) / 64, p.B * p.H), dim3(128), 0, s, p);
-  }
-}
-
-int attn_qg_fwd(int dh) {
-  static const int env = [] { const char* v = std::getenv("FS2_ATTN_QG"); return v ? std::atoi(v) : 0; }();
-  if (env == 1 || env == 2) return env;
-  return dh <= 128 ? 2 : 1;
-}
+int attn_qg_fwd(int dh) { return dh <= 128 ? 2 : 1; }
 
 // half-size forward blocks (64 queries) when 128-row blocks would leave CUs idle (the
 // encoder: T = 200, B*H = 64 -> 128 blocks of 128 rows for 256 CUs; 26.3 -> 24.2 us)
 bool attn_small_blocks(const AttnP& p) {
-  static const int env = [] { const char* v = std::getenv("FS2_ATTN_W8"); return v ? std::atoi(v) : 0; }();
-  if (env == 4) return true;
-  if (env == 8) return false;
   return (long)((p.T + 127) / 128) * p.B * p.H < 256;
 }
 
 template <int DH>
 void launch_fwd(const AttnP& p, hipStream_t s) {
-  if constexpr (DH <= 192) {
-    if (attn_v32(DH)) { launch_fwd32<DH>(p, s); return; }
-  }
   if (attn_small_blocks(p)) {
     dim3 grid((p.T + 63) / 64, p.B * p.H);
     if (attn_qg_fwd(DH) == 2) hipLaunchKernelGGL((attn_fwd_kernel<DH, 2, 4>), grid, dim3(128), 0, s, p);
     else hipLaunchKernelGGL((attn_fwd_kernel<DH, 1, 4>), grid, dim3(256), 0, s, p);
     return;
   }
-  static const int fcfg = [] { const char* v = std::getenv("FS2_ATTN_FWD"); return v ? std::atoi(v) : 0; }();
-  if (fcfg == 1) {   // 256-query blocks: 8 waves x 32 queries
-    hipLaunchKernelGGL((attn_fwd_kernel<DH, 2, 16>), dim3((p.T + 255) / 256, p.B * p.H), dim3(512), 0, s, p);
-    return;
-  }
   dim3 grid((p.T + 127) / 128, p.B * p.H);
   if (attn_qg_fwd(DH) == 2) hipLaunchKernelGGL((attn_fwd_kernel<DH, 2>), grid, dim3(256), 0, s, p);
   else hipLaunchKernelGGL((attn_fwd_kernel<DH, 1>), grid, dim3(512), 0, s, p);
 }
-// staged backward: 0 = D only, 1 = dQ (D precomputed), 2 = dK/dV (D precomputed)
-template <int DH>
-void launch_bwd_stage(const AttnP& p, int stage, hipStream_t s) {
-  if constexpr (DH <= 192) {
-    if (attn_v32(DH)) { launch_bwd32<DH>(p, s, stage); return; }
-  }
-  dim3 g1((p.T + 127) / 128, p.B * p.H);
-  if (stage == 0) {
-    hipLaunchKernelGGL(attn_dsum_kernel<DH>, dim3((p.T + 63) / 64, p.B * p.H), dim3(256), 0, s, p);
-  } else if (stage == 1) {
-    if (DH <= 64) hipLaunchKernelGGL((attn_bwd_dq_kernel<DH, 2>), g1, dim3(256), 0, s, p);
-    else hipLaunchKernelGGL((attn_bwd_dq_kernel<DH, 1>), g1, dim3(512), 0, s, p);
-  } else {
-    hipLaunchKernelGGL(attn_bwd_dkv_kernel<DH>, g1, dim3(512), 0, s, p);
-  }
-}
-
 template <int DH>
 void launch_bwd(const AttnP& p, hipStream_t s) {
-  if constexpr (DH <= 192) {
-    if (attn_v32(DH)) { launch_bwd32<DH>(p, s, -1); return; }
-  }
   // 64-key / 64-query blocks when 128-row blocks underfill the chip, as the forward (encoder
-  // T = 200 with the LDS-DMA dK/dV kernel: 60.2 -> 56.7 us; FS2_ATTN_W8=4 / 8 forces either)
+  // T = 200 with the LDS-DMA dK/dV kernel: 60.2 -> 56.7 us)
   if (attn_small_blocks(p)) {
     dim3 g1((p.T + 63) / 64, p.B * p.H);
     if (DH <= 64) hipLaunchKernelGGL((attn_bwd_dq_kernel<DH, 2, 4>), g1, dim3(128), 0, s, p);
@@ -1322,12 +734,11 @@ extern "C" int fs2_attn_fwd(const void* qkv, int64_t ldq, const uint8_t* key_pad
   return 0;
 }
 
-namespace {
-int attn_bwd_impl(const void* qkv, int64_t ldq, const uint8_t* key_pad, int mask_mode,
-                  const void* out, int64_t ldo, const void* dout, int64_t lddo, const float* lse,
-                  int B, int H, int T, int dh, float scale, float p_drop, uint32_t seed,
-                  uint32_t salt, void* dqkv, int64_t lddq, float* workspace, int dtype,
-                  void* stream, int stage) {
+extern "C" int fs2_attn_bwd(const void* qkv, int64_t ldq, const uint8_t* key_pad, int mask_mode,
+                            const void* out, int64_t ldo, const void* dout, int64_t lddo,
+                            const float* lse, int B, int H, int T, int dh, float scale,
+                            float p_drop, uint32_t seed, uint32_t salt, void* dqkv,
+                            int64_t lddq, float* workspace, int dtype, void* stream) {
   if (int rc = check(B, H, T, dh, ldq, qkv, dtype)) return rc;
   if (!key_pad || !out || !dout || !lse || !dqkv || !workspace) return FS2_EINVAL;
   if (!a16(out) || !a16(dout) || !a16(dqkv) || (ldo % 8) || (lddo % 8) || (lddq % 8))
@@ -1344,46 +755,14 @@ int attn_bwd_impl(const void* qkv, int64_t ldq, const uint8_t* key_pad, int mask
   p.seed = seed; p.salt = salt;
   p.thr16 = (uint32_t)(p_drop * 65536.f + 0.5f);
   hipStream_t s = (hipStream_t)stream;
-  if (stage < 0) {
-    switch (dh) {
-      case 64: launch_bwd<64>(p, s); break;
-      case 128: launch_bwd<128>(p, s); break;
-      case 192: launch_bwd<192>(p, s); break;
-      default: launch_bwd<256>(p, s); break;
-    }
-  } else {
-    p.dsum_in = 1;
-    switch (dh) {
-      case 64: launch_bwd_stage<64>(p, stage, s); break;
-      case 128: launch_bwd_stage<128>(p, stage, s); break;
-      case 192: launch_bwd_stage<192>(p, stage, s); break;
-      default: launch_bwd_stage<256>(p, stage, s); break;
-    }
+  switch (dh) {
+    case 64: launch_bwd<64>(p, s); break;
+    case 128: launch_bwd<128>(p, s); break;
+    case 192: launch_bwd<192>(p, s); break;
+    default: launch_bwd<256>(p, s); break;
   }
   FS2_CHECK_LAUNCH();
   return 0;
-}
-
-}  // namespace
-
-extern "C" int fs2_attn_bwd(const void* qkv, int64_t ldq, const uint8_t* key_pad, int mask_mode,
-                            const void* out, int64_t ldo, const void* dout, int64_t lddo,
-                            const float* lse, int B, int H, int T, int dh, float scale,
-                            float p_drop, uint32_t seed, uint32_t salt, void* dqkv,
-                            int64_t lddq, float* workspace, int dtype, void* stream) {
-  return attn_bwd_impl(qkv, ldq, key_pad, mask_mode, out, ldo, dout, lddo, lse, B, H, T, dh,
-                       scale, p_drop, seed, salt, dqkv, lddq, workspace, dtype, stream, -1);
-}
-
-extern "C" int fs2_attn_bwd_stage(const void* qkv, int64_t ldq, const uint8_t* key_pad,
-                                  int mask_mode, const void* out, int64_t ldo, const void* dout,
-                                  int64_t lddo, const float* lse, int B, int H, int T, int dh,
-                                  float scale, float p_drop, uint32_t seed, uint32_t salt,
-                                  void* dqkv, int64_t lddq, float* workspace, int dtype,
-                                  int stage, void* stream) {
-  if (stage < 0 || stage > 2) return FS2_EINVAL;
-  return attn_bwd_impl(qkv, ldq, key_pad, mask_mode, out, ldo, dout, lddo, lse, B, H, T, dh,
-                       scale, p_drop, seed, salt, dqkv, lddq, workspace, dtype, stream, stage);
 }
 
 extern "C" int64_t fs2_attn_workspace_floats(int B, int H, int T) { return (int64_t)B * H * T; }

@@ -31,11 +31,24 @@ __device__ void llvm_raw_buffer_load_lds(i32x4 rsrc, __attribute__((address_spac
 
 namespace {
 
-// host-side A/B switch for kernel variants (read once)
+// Measurement switches (FS2_* environment variables and the g4_flags timing bits, some of
+// which produce WRONG results on purpose) exist only in a build with -DFS2_EXPERIMENTS, the
+// one tools/ A/B runs use; the product library compiles them to their defaults.
+#ifdef FS2_EXPERIMENTS
 bool getenv_flag(const char* name) {
   const char* v = std::getenv(name);
   return v && v[0] && std::strcmp(v, "0") != 0;
 }
+int getenv_int(const char* name, int dflt) {
+  const char* v = std::getenv(name);
+  return v ? std::atoi(v) : dflt;
+}
+#define XFLAGS(p) ((p).g4_flags)
+#else
+constexpr bool getenv_flag(const char*) { return false; }
+constexpr int getenv_int(const char*, int dflt) { return dflt; }
+#define XFLAGS(p) 0
+#endif
 
 constexpr int BM = 128, BN = 128, NT = 256;
 constexpr int TILE_BYTES = 128 * 128;  // one operand, one stage
@@ -53,14 +66,12 @@ struct GemmP {
   const float* row_scale_post;
   int accumulate; int split_k; int k_per_split;
   long split_stride;  // >0: split z stores its partial to C + z*split_stride (no atomics)
-  int g4_flags;       // gemm256 A/B switches (FS2_G4_FLAGS): 1 no stagger, 2 no setprio
+  int g4_flags;       // FS2_EXPERIMENTS builds only (XFLAGS): timing switches of the large kernels
   int batch_div;
   long sA1, sA2, sB1, sB2, sC1, sC2, sR1, sR2;
   int tiles_m, tiles_n;
   int vec_ok;
   int vec_align;  // vector epilogue possible if K were not split
-  uint8_t* relu_mask; long ldm;         // bf16: packed (C > 0) bits, written by the vector epilogue
-  const uint8_t* gate_bits; long ldgb;  // bf16: packed gate bits (gate_bits-aware kernels)
 };
 
 __device__ __forceinline__ u32x4 add_bf16x8(u32x4 a, u32x4 b) {
@@ -96,7 +107,7 @@ __device__ __attribute__((noinline)) float epi_act_rare(float v, int act) {
 }
 __device__ __forceinline__ float epi_act(float v, int act) {
   if (act > 1) return epi_act_rare(v, act);
-  return fmaxf(v, act ? 0.f : -INFINITY);
+  return act ? fmaxf(v, 0.f) : v;   // a select: NaN passes through when there is no activation
 }
 
 template <typename T>
@@ -776,13 +787,7 @@ __device__ __forceinline__ void epilogue_256x128(const GemmP& p, const float* cs
       }
     }
     float g[8], rr[8];
-    if (p.gate_bits) {
-      const unsigned gb = p.gate_bits[(long)m * p.ldgb + (n >> 3)];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) g[e] = (gb >> e) & 1u ? 1.f : 0.f;
-    } else if (p.gate) {
-      load8<bf16>(g, (const bf16*)p.gate + (long)m * p.ldg + n, nn);
-    }
+    if (p.gate) load8<bf16>(g, (const bf16*)p.gate + (long)m * p.ldg + n, nn);
     if (Rb) load8<bf16>(rr, (const bf16*)Rb + (long)m * p.ldr + n, nn);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -806,15 +811,6 @@ __device__ __forceinline__ void epilogue_256x128(const GemmP& p, const float* cs
       }
     } else {
       store8<bf16>((bf16*)Cb + off, v, nn);
-      if (p.relu_mask) {   // bits of the stored bf16 values (> 0: positive and non-zero)
-        unsigned bits = 0;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const unsigned short h = __builtin_bit_cast(unsigned short, (bf16)v[e]);
-          bits |= (e < nn && h != 0 && h < 0x8000u) ? 1u << e : 0u;
-        }
-        p.relu_mask[(long)m * p.ldm + (n >> 3)] = (uint8_t)bits;
-      }
     }
   }
 }
@@ -1055,7 +1051,7 @@ __global__ void __launch_bounds__(BNT) gemm_big_kernel(GemmP p) {
   char* Cb = p.C + (zb * p.sC1 + zh * p.sC2) * (p.c_fp32 ? 4 : 2);
   if (p.split_stride > 0 && p.split_k > 1) Cb += (long)blockIdx.z * p.split_stride * 4;
   const char* Rb = p.residual ? p.residual + (zb * p.sR1 + zh * p.sR2) * 2 : nullptr;
-  if (p.vec_ok && !(p.g4_flags & 64) && !p.relu_mask && !p.gate_bits) {
+  if (p.vec_ok && !(XFLAGS(p) & 64)) {
     epilogue_direct(p, &acc[0][0], m0 + wm * 64, n0 + wn * 64, Cb, Rb, lane);
     return;
   }
@@ -1153,7 +1149,7 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256_kernel(GemmP p) {
       abt[i] = b * p.conv_t;
       at[i] = rr - b * rpu;
       avo[i] = aval[i] ? (int)(((long)rr * p.lda + ac[i] * 8) * 2) : BUF_OOB;
-      if (p.g4_flags & 128) {  // timing experiment: 8 full 128-B rows per piece (wrong results)
+      if (XFLAGS(p) & 128) {  // timing experiment: 8 full 128-B rows per piece (wrong results)
         const int r2 = m0 + piece * 16 + (lane >> 3) + 8 * i;
         avo[i] = r2 < p.M ? (int)(((long)r2 * p.lda + (lane & 7) * 8) * 2) : BUF_OOB;
       }
@@ -1181,7 +1177,7 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256_kernel(GemmP p) {
       const int row = n0 + r;
       bval[i] = row < p.N;
       bvo[i] = bval[i] ? (int)(((long)row * p.ldb + bc[i] * 8) * 2) : BUF_OOB;
-      if (p.g4_flags & 128) {
+      if (XFLAGS(p) & 128) {
         const int r2 = n0 + piece * 16 + (lane >> 3) + 8 * i;
         bvo[i] = r2 < p.N ? (int)(((long)r2 * p.ldb + (lane & 7) * 8) * 2) : BUF_OOB;
       }
@@ -1233,7 +1229,7 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256_kernel(GemmP p) {
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
           const int vo = (kin || k0 + ac[i] * 8 < K) ? avo[i] : BUF_OOB;
-          blds16(rsA, vo, ((p.g4_flags & 128) ? (k0 & ~63) : k0) * 2, dst + (wave * 2 + i) * 1024);
+          blds16(rsA, vo, ((XFLAGS(p) & 128) ? (k0 & ~63) : k0) * 2, dst + (wave * 2 + i) * 1024);
         }
       } else {                                  // taps not aligned to 32-wide regions
 #pragma unroll
@@ -1267,7 +1263,7 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256_kernel(GemmP p) {
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int vo = (kin || k0 + bc[i] * 8 < K) ? bvo[i] : BUF_OOB;
-        blds16(rsB, vo, ((p.g4_flags & 128) ? (k0 & ~63) : k0) * 2, dst + (wave * 2 + i) * 1024);
+        blds16(rsB, vo, ((XFLAGS(p) & 128) ? (k0 & ~63) : k0) * 2, dst + (wave * 2 + i) * 1024);
       }
     } else if (!bconv3) {
       const bool kin = k0 + 32 <= kva;
@@ -1324,11 +1320,11 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256_kernel(GemmP p) {
     asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   }
   __builtin_amdgcn_s_barrier();
-  const bool stag = !(p.g4_flags & 1);
-  const bool prio = !(p.g4_flags & 2);
-  const bool nowait = p.g4_flags & 4;   // timing experiments only (wrong results)
-  const bool noissue = p.g4_flags & 8;
-  const bool dma_mm = p.g4_flags & 256;  // LDS-DMA issued inside the matrix section
+  const bool stag = !(XFLAGS(p) & 1);
+  const bool prio = !(XFLAGS(p) & 2);
+  const bool nowait = XFLAGS(p) & 4;   // timing experiments only (wrong results)
+  const bool noissue = XFLAGS(p) & 8;
+  const bool dma_mm = XFLAGS(p) & 256;  // LDS-DMA issued inside the matrix section
   // stagger: waves 4-7 half a phase behind; without it both groups retire DMA like group 1
   const int grp = stag ? wr : 1;
   if (stag && wr == 1) __builtin_amdgcn_s_barrier();
@@ -1449,8 +1445,6 @@ __device__ void llvm_raw_buffer_store_v4i32(i32x4 data, i32x4 rsrc, int voffset,
                                             int aux) __asm("llvm.amdgcn.raw.buffer.store.v4i32");
 __device__ i32x2 llvm_raw_buffer_load_v2i32(i32x4 rsrc, int voffset, int soffset,
                                             int aux) __asm("llvm.amdgcn.raw.buffer.load.v2i32");
-__device__ unsigned char llvm_raw_buffer_load_i8(i32x4 rsrc, int voffset, int soffset,
-                                                 int aux) __asm("llvm.amdgcn.raw.buffer.load.i8");
 
 // epilogue store instructions per wave per tile: fp32 one 16-byte store per 16x16 block (16);
 // bf16 one 16-byte store per block PAIR (8: lanes l and l ^ 16 trade halves)
@@ -1475,9 +1469,7 @@ __global__ void __launch_bounds__(BNT) gemm_pk_kernel(GemmP p) {
   const int nk = (p.K + 63) / 64;
   const int total = mine * nk;
   const i32x4 rsA = make_rsrc(p.A), rsB = make_rsrc(p.B), rsC = make_rsrc(p.C);
-  const bool gbits = p.gate_bits != nullptr;
-  const i32x4 rsE = make_rsrc(gbits ? (const void*)p.gate_bits
-                                    : (p.gate ? p.gate : (p.residual ? p.residual : p.C)));
+  const i32x4 rsE = make_rsrc(p.gate ? p.gate : (p.residual ? p.residual : p.C));
   const long lde = p.gate ? p.ldg : p.ldr;
   const bool has_e = p.gate || p.residual;
 
@@ -1573,14 +1565,7 @@ __global__ void __launch_bounds__(BNT) gemm_pk_kernel(GemmP p) {
         const bool in = m < p.mvalid;
         rs[i] = (p.row_scale && in) ? p.row_scale[m] : 1.f;
         rs2[i] = (p.row_scale_post && in) ? p.row_scale_post[m] : 1.f;
-          if (gbits) {   // packed gate bits: one byte (8 columns) per block, same count
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int n = nb + 16 * j + 4 * lg;
-            const bool ok = in && n < p.nvalid;
-            ev[i][j][0] = llvm_raw_buffer_load_i8(rsE, ok ? (int)((long)m * p.ldgb + (n >> 3)) : BUF_OOB, 0, 0);
-          }
-        } else if (has_e) {
+        if (has_e) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const int n = nb + 16 * j + 4 * lg;
@@ -1618,7 +1603,7 @@ __global__ void __launch_bounds__(BNT) gemm_pk_kernel(GemmP p) {
       if (nk == 1) {   // operands issued this iteration: retire them, keep the prefetch in flight
         if (pre) vm_wait<6>(); else vm_wait<0>();
       }
-      const bool nost = p.g4_flags & 16;   // timing experiments only: no stores (wrong results)
+      const bool nost = XFLAGS(p) & 16;   // timing experiments only: no stores (wrong results)
       const bool odd = lg & 1;
       auto fin = [&](int i, int j) {         // epilogue values of block (i, j); acc cleared
         f32x4 v;
@@ -1627,8 +1612,7 @@ __global__ void __launch_bounds__(BNT) gemm_pk_kernel(GemmP p) {
           float x = epi_act(acc[i][j][e] + bv[j][e], p.relu);
           const unsigned w = (unsigned)ev[i][j][e >> 1];
           const float ef = __builtin_bit_cast(float, (e & 1) ? (w & 0xffff0000u) : (w << 16));
-          if (gbits) x = ((unsigned)ev[i][j][0] >> ((lg & 1) * 4 + e)) & 1u ? x : 0.f;
-          else if (p.gate) x = ef > 0.f ? x : 0.f;
+          if (p.gate) x = ef > 0.f ? x : 0.f;
           x *= rs[i];
           if (p.residual) x += ef;
           v[e] = x * rs2[i];
@@ -1730,7 +1714,8 @@ __global__ void __launch_bounds__(BNT, 1) gemm_ps_kernel(GemmP p) {
   constexpr int AIMG = 256 * 128;
   constexpr int SLOT = AIMG + BN * 128;
   constexpr int NB1 = (BN - 128) / 64;     // B1 pieces per wave
-  constexpr int S = 8 * NJ;                // epilogue stores per wave per tile
+  constexpr int S32 = 8 * NJ;              // epilogue stores per wave per tile: fp32 output
+  constexpr int S16 = 8 * ((NJ + 1) / 2);  // bf16 output (fragment pairs, one 16-B store each)
   static_assert(2 * SLOT <= 160 * 1024, "LDS");
   __shared__ __attribute__((aligned(16))) char smem[2 * SLOT];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1903,8 +1888,15 @@ __global__ void __launch_bounds__(BNT, 1) gemm_ps_kernel(GemmP p) {
       if (ph == 3 && more2) issue_b(1, cur);
       auto dwait = [&]() {
         if constexpr (ph == 1) {
-          if (more1) { if (first) vm_wait<6 + NB1 + S>(); else vm_wait<6 + NB1>(); }
-          else { if (first) vm_wait<S>(); else vm_wait<0>(); }
+          if (more1) {
+            if (!first) vm_wait<6 + NB1>();
+            else if (p.c_fp32) vm_wait<6 + NB1 + S32>();
+            else vm_wait<6 + NB1 + S16>();
+          } else {
+            if (!first) vm_wait<0>();
+            else if (p.c_fp32) vm_wait<S32>();
+            else vm_wait<S16>();
+          }
         } else {
           if (more2) vm_wait<4 + NB1>();
           else if (more1) vm_wait<2>();
@@ -1925,9 +1917,9 @@ __global__ void __launch_bounds__(BNT, 1) gemm_ps_kernel(GemmP p) {
               __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[kh][j], af[i], acc[mq * 4 + i][j], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
       if constexpr ((ph & 1) != 0) { if (wr == 0) dwait(); }
-      if (ph == 3 && last && !(p.g4_flags & 32)) {   // flag 32: timing only, no epilogue
+      if (ph == 3 && last && !(XFLAGS(p) & 32)) {   // flag 32: timing only, no epilogue
         // ---- tile epilogue, straight from the accumulators ----
-        if (!(p.g4_flags & 64)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (!(XFLAGS(p) & 64)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const int tile = c0 + local + t * nbx;
         const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
         const int mb = tm * 256 + wr * 128, nb = tn * BN + wc * WN;
@@ -1944,15 +1936,15 @@ __global__ void __launch_bounds__(BNT, 1) gemm_ps_kernel(GemmP p) {
           rs[i] = ((p.row_scale && m < p.mvalid) ? p.row_scale[m] : 1.f) *
                   ((p.row_scale_post && m < p.mvalid) ? p.row_scale_post[m] : 1.f);
         }
-        // compact, branch-free body (ReLU as a max against 0 or -inf): the epilogue runs once
+        // compact, branch-free body (ReLU as a select): the epilogue runs once
         // per tile, so its code is fetched cold every time -- keep it small
-        const float lo = p.relu ? 0.f : -INFINITY;
-        const bool c32 = p.c_fp32, nost = p.g4_flags & 16;
+        const bool relu = p.relu;
+        const bool c32 = p.c_fp32, nost = XFLAGS(p) & 16;
         const bool odd = lg & 1;
         auto fin = [&](int i, int j) {   // epilogue values of fragment (i, j), acc cleared
           f32x4 v = acc[i][j] + bv[j];
-          v[0] = fmaxf(v[0], lo) * rs[i]; v[1] = fmaxf(v[1], lo) * rs[i];
-          v[2] = fmaxf(v[2], lo) * rs[i]; v[3] = fmaxf(v[3], lo) * rs[i];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = (relu ? fmaxf(v[e], 0.f) : v[e]) * rs[i];
           acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
           return v;
         };
@@ -2035,25 +2027,6 @@ void launch4(const GemmP& p, dim3 grid, hipStream_t s, int ak, int bk) {
   else hipLaunchKernelGGL((gemm_kernel<T, false, false, GA, GB>), grid, dim3(NT), 0, s, p);
 }
 
-// bit n % 8 of mask[m][n / 8] = (C[m][n] > 0) for bf16 C (nvalid % 8 == 0): the packed ReLU
-// pattern for GEMM paths whose epilogue does not write it
-__global__ void __launch_bounds__(256) pack_relu_mask_kernel(const bf16* C, long ldc, int n8row,
-                                                             long n8, uint8_t* mask, long ldm) {
-  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n8) return;
-  const long m = i / n8row;
-  const int c = (int)(i - m * n8row);
-  const u32x4 u = *(const u32x4*)(C + m * ldc + 8 * c);
-  unsigned bits = 0;
-#pragma unroll
-  for (int w = 0; w < 4; ++w) {
-    const unsigned lo = u[w] & 0xffffu, hi = u[w] >> 16;
-    bits |= (lo != 0 && lo < 0x8000u) ? 1u << (2 * w) : 0u;
-    bits |= (hi != 0 && hi < 0x8000u) ? 1u << (2 * w + 1) : 0u;
-  }
-  mask[m * ldm + c] = (uint8_t)bits;
-}
-
 template <typename T>
 int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
   dim3 grid(p.tiles_m * p.tiles_n, 1, gz);
@@ -2073,7 +2046,7 @@ int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
       const int nk = (p.K + 63) / 64;
       // ~one round of blocks: fewer K slices halve the fp32 atomics (decoder QKV weight
       // gradient 95 -> 75 us vs two rounds); FS2_WGRAD_BIG_TARGET overrides for A/B runs
-      static const int tgt = [] { const char* v = std::getenv("FS2_WGRAD_BIG_TARGET"); return v ? std::atoi(v) : 240; }();
+      static const int tgt = getenv_int("FS2_WGRAD_BIG_TARGET", 240);
       split_big = max(1, min((tgt + tiles_big - 1) / tiles_big, nk / 8));
     }
     const bool slices = p.split_stride > 0 && p.split_k > 1;  // caller-chosen split, plain stores
@@ -2090,16 +2063,15 @@ int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
     // FS2_PS_MODES: bit 0 plain, bit 1 reflect conv (fwd), bit 2 padded-domain conv (dgrad).
     // Default 5: in the bench step the unsplit decoder conv1 data gradient gains 0.15-0.2 ms,
     // while the conv1 forward measured 0-0.1 ms slower than gemm256_kernel (A/B runs)
-    static const int ps_modes = [] { const char* v = std::getenv("FS2_PS_MODES"); return v ? std::atoi(v) : 5; }();
+    static const int ps_modes = getenv_int("FS2_PS_MODES", 5);
     const int cm_ps = p.conv_mode == 0 ? 0
                       : ((p.conv_mode == 1 || p.conv_mode == 4) && p.conv_dil == 1 && p.conv_c % 64 == 0
                              ? p.conv_mode : -1);
     const bool ps_on = cm_ps >= 0 && (ps_modes >> (cm_ps == 0 ? 0 : (cm_ps == 1 ? 1 : 2))) & 1;
-    if (!no_ps && ak && bk && ps_on && batch == 1 && p.split_k <= 1 && p.vec_ok && !p.relu_mask &&
+    if (!no_ps && ak && bk && ps_on && batch == 1 && p.split_k <= 1 && p.vec_ok &&
         !p.accumulate && !p.gate && !p.residual && p.relu <= 1 && p.K >= 2048 && p.N >= 128 && pk_fits) {
       GemmP q = p;
-      static const int psf = [] { const char* v = std::getenv("FS2_PS_FLAGS"); return v ? std::atoi(v) : 0; }();
-      q.g4_flags = psf;
+      q.g4_flags = getenv_int("FS2_PS_FLAGS", 0);
       q.tiles_m = (p.M + 255) / 256;
       // tile width by rounds x width over the 256 CUs (ties to the wider tile)
       const int t256 = q.tiles_m * ((p.N + 255) / 256), t192 = q.tiles_m * ((p.N + 191) / 192);
@@ -2125,11 +2097,10 @@ int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
     // FS2_PK_NARROW=1 keeps them on the persistent kernel
     static const bool pk_narrow = getenv_flag("FS2_PK_NARROW");
     const bool pk_shape = p.K <= 768 || p.N > 512 || pk_narrow;
-    if (!no_pk && ak && bk && p.conv_mode == 0 && batch == 1 && p.split_k <= 1 && p.vec_ok && !p.relu_mask &&
+    if (!no_pk && ak && bk && p.conv_mode == 0 && batch == 1 && p.split_k <= 1 && p.vec_ok &&
         !p.accumulate && !(p.gate && p.residual) && p.K > 64 && p.K <= 1536 && pk_shape && pk_fits) {
       GemmP q = p;
-      static const int pkf = [] { const char* v = std::getenv("FS2_PK_FLAGS"); return v ? std::atoi(v) : 0; }();
-      q.g4_flags = pkf;
+      q.g4_flags = getenv_int("FS2_PK_FLAGS", 0);
       q.tiles_m = (p.M + BBM - 1) / BBM;
       const int nt = q.tiles_m * q.tiles_n;
       // >= 8 blocks: every XCD chunk needs a block (blocks with no tile exit at once)
@@ -2151,15 +2122,14 @@ int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
     }
     // from 150 tiles: the encoder FFN conv1 forward (M = 6400, N = 1536: 150 tiles of 256^2 in
     // one round vs 300 of 256x128 in 1.2 rounds) 122 -> 112 us; FS2_G4_MIN_TILES overrides
-    static const int g4_min = [] { const char* v = std::getenv("FS2_G4_MIN_TILES"); return v ? std::atoi(v) : 150; }();
+    static const int g4_min = getenv_int("FS2_G4_MIN_TILES", 150);
     const bool use256 = !no256 && wide && p.conv_mode != 2 &&
                         ((p.vec_ok && p.split_k <= 1 && tiles256 * batch >= g4_min) ||
                          (slices && p.vec_ok && tiles256 * p.split_k >= 160) ||
                          (wgrad && tiles256 * split256 >= 160));
     if (use256) {
       GemmP q = p;
-      static const int g4f = [] { const char* v = std::getenv("FS2_G4_FLAGS"); return v ? std::atoi(v) : 0; }();
-      q.g4_flags = g4f;
+      q.g4_flags = getenv_int("FS2_G4_FLAGS", 0);
       q.tiles_m = tm256;
       q.tiles_n = tn256;
       int gz2 = slices ? p.split_k : gz;
@@ -2193,7 +2163,7 @@ int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
     // 256x128 tiles down to 60 of them (M = 6400 encoder / predictor GEMMs: 75 tiles beat the
     // 150 tiles of the 128x128 kernel, e.g. predictor conv fwd 45 -> 31 us); FS2_GEMM_BIG_MIN
     // overrides for A/B runs
-    static const int big_min = [] { const char* v = std::getenv("FS2_GEMM_BIG_MIN"); return v ? std::atoi(v) : 60; }();
+    static const int big_min = getenv_int("FS2_GEMM_BIG_MIN", 60);
     const bool use_big = !no_big && p.conv_mode != 2 &&
                          ((p.vec_ok && p.split_k <= 1 && tiles_big * batch >= big_min) ||
                           (slices && p.vec_ok && tiles_big * p.split_k >= 160) ||
@@ -2229,13 +2199,6 @@ int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
     } else {
       if (p.conv_mode == 2) launch4<T, false, true>(p, grid, s, ak, bk);
       else launch4<T, true, true>(p, grid, s, ak, bk);
-      // the 128x128 kernel's epilogue does not pack the ReLU pattern: derive it from C
-      if (p.relu_mask) {
-        FS2_CHECK_LAUNCH();
-        const long n8 = (long)p.mvalid * (p.nvalid / 8);
-        hipLaunchKernelGGL(pack_relu_mask_kernel, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0,
-                           s, (const bf16*)p.C, p.ldc, p.nvalid / 8, n8, p.relu_mask, p.ldm);
-      }
     }
   } else {
     launch4<T, false, false>(p, grid, s, ak, bk);
@@ -2275,8 +2238,6 @@ extern "C" int fs2_gemm(const fs2_gemm_desc* d, void* stream) {
   p.batch_div = d->batch_div > 0 ? d->batch_div : 1;
   p.sA1 = d->sA1; p.sA2 = d->sA2; p.sB1 = d->sB1; p.sB2 = d->sB2;
   p.sC1 = d->sC1; p.sC2 = d->sC2; p.sR1 = d->sR1; p.sR2 = d->sR2;
-  p.relu_mask = d->relu_mask; p.ldm = d->ldm;
-  p.gate_bits = d->gate_bits; p.ldgb = d->ldgb;
   p.tiles_m = (p.M + BM - 1) / BM;
   p.tiles_n = (p.N + BN - 1) / BN;
   const int batch = d->batch > 1 ? d->batch : 1;
@@ -2315,11 +2276,6 @@ extern "C" int fs2_gemm(const fs2_gemm_desc* d, void* stream) {
     p.split_k = (nkt + kps - 1) / kps;
   }
   if (p.accumulate && !p.c_fp32) return FS2_EINVAL;
-  if (p.relu_mask && (d->dtype != FS2_BF16 || p.c_fp32 || batch > 1 || p.split_k > 1 ||
-                      (p.nvalid % 8) || p.ldm * 8 < p.nvalid || (p.ldc % 8) || !aligned16(p.C)))
-    return FS2_EINVAL;
-  if (p.gate_bits && (!p.gate || d->dtype != FS2_BF16 || batch > 1 || p.ldgb * 8 < p.nvalid))
-    return FS2_EINVAL;
   {
     const int oes = p.c_fp32 ? 4 : es;
     const int ov = 16 / oes;  // output elements per 16 bytes

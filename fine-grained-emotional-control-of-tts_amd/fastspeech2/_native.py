@@ -13,6 +13,26 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FS2_HIP_LIB", os.path.join(_HERE, "libfs2_hip.so"))
+# The measurement build (``make experiments`` -> libfs2_hip_exp.so, -DFS2_EXPERIMENTS) is the
+# only one whose FS2_* A/B switches do anything; the host side honours them under the same
+# condition, so the product path has one configuration.
+EXPERIMENTS = os.path.basename(LIB_PATH).startswith("libfs2_hip_exp")
+
+
+def exp_flag(name, default=False):
+    """FS2_* boolean A/B switch: read only with the experiments library, else ``default``."""
+    if not EXPERIMENTS:
+        return default
+    v = os.environ.get(name)
+    return default if v is None else v not in ("", "0")
+
+
+def exp_int(name, default):
+    """FS2_* integer A/B switch: read only with the experiments library, else ``default``."""
+    if not EXPERIMENTS:
+        return default
+    v = os.environ.get(name)
+    return default if v is None else int(v)
 
 F32 = 0
 BF16 = 1
@@ -43,8 +63,6 @@ class GemmDesc(ctypes.Structure):
         ("sA1", ctypes.c_int64), ("sA2", ctypes.c_int64), ("sB1", ctypes.c_int64),
         ("sB2", ctypes.c_int64), ("sC1", ctypes.c_int64), ("sC2", ctypes.c_int64),
         ("sR1", ctypes.c_int64), ("sR2", ctypes.c_int64), ("conv_dil", ctypes.c_int),
-        ("relu_mask", ctypes.c_void_p), ("ldm", ctypes.c_int64),
-        ("gate_bits", ctypes.c_void_p), ("ldgb", ctypes.c_int64),
     ]
 
 
@@ -99,8 +117,6 @@ SIGNATURES = {
     "fs2_attn_bwd": (I, [P, I64, P, I, P, I64, P, I64, P, I, I, I, I, Fl, Fl, U32, U32, P, I64,
                          P, I, P]),
     "fs2_attn_workspace_floats": (I64, [I, I, I]),
-    "fs2_attn_bwd_stage": (I, [P, I64, P, I, P, I64, P, I64, P, I, I, I, I, Fl, Fl, U32, U32, P,
-                               I64, P, I, I, P]),
     "fs2_softmax_fwd": (I, [P, P, I, I, I, I, I, I, Fl, Fl, U32, U32, P, P, I, P]),
     "fs2_softmax_bwd": (I, [P, P, I, I, I, I, I, Fl, Fl, U32, U32, P, I, P]),
     "fs2_embed_fwd": (I, [P, P, P, I, I, I, I, P, P, I, P]),

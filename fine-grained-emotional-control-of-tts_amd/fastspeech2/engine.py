@@ -14,7 +14,6 @@ gradients, LayerNorm statistics and losses are fp32 in both.
 """
 
 import math
-import os
 import re
 
 import torch
@@ -35,7 +34,7 @@ class _Salt:
         return self.n
 
 
-_NO_FLASH = os.environ.get("FS2_NO_FLASH", "0") not in ("", "0")
+_NO_FLASH = N.exp_flag("FS2_NO_FLASH")
 
 
 def dgrad_split(Mp, C, K, dt, n_cu=256, max_split=8):
@@ -64,26 +63,17 @@ def dgrad_split(Mp, C, K, dt, n_cu=256, max_split=8):
     return best
 
 
-_NO_SLICES = os.environ.get("FS2_NO_WGRAD_SLICES", "0") not in ("", "0")
-_NO_PS = os.environ.get("FS2_GEMM_NO_PS", "0") not in ("", "0")
-_PS_MODES = int(os.environ.get("FS2_PS_MODES", "5"))
+_NO_SLICES = N.exp_flag("FS2_NO_WGRAD_SLICES")
+_NO_PS = N.exp_flag("FS2_GEMM_NO_PS")
+_PS_MODES = N.exp_int("FS2_PS_MODES", 5)
 # large weight gradients (the FFN conv1 weights, 5.3 M floats) as split-K planes + fixed-order
 # sum instead of split-K fp32 atomics: decoder 428 -> 420 us, encoder 128 -> 119 us, and the
 # result no longer depends on atomic ordering.  FS2_NO_WGRAD_BIG_SLICES=1 restores the atomics.
-_BIG_SLICES = os.environ.get("FS2_NO_WGRAD_BIG_SLICES", "0") in ("", "0")
-_SLICE_TARGET = int(os.environ.get("FS2_WGRAD_SLICE_TARGET", "240"))
-# enqueue each weight gradient before the data gradient that does not need to precede it
-# (FS2_WGRAD_EARLY=0: the round-1 order, data gradient first)
-_WGRAD_EARLY = os.environ.get("FS2_WGRAD_EARLY", "1") not in ("", "0")
-# opt-in (FS2_RELU_BITS=1): the FFN ReLU pattern as packed bits for the conv2 data gradient's
-# gate instead of re-reading the bf16 activations (90 MB less read per decoder layer; A/B
-# 20.46-20.53 on vs 20.42-20.43 ms off: the conv1 epilogue's byte stores cost more)
-_RELU_BITS = os.environ.get("FS2_RELU_BITS", "0") not in ("", "0")
-_NO_SIDE = os.environ.get("FS2_NO_SIDE_STREAM", "0") not in ("", "0")
-_NO_AUX = os.environ.get("FS2_NO_AUX_STREAM", "0") not in ("", "0")
-# dQ and dK/dV of the encoder attention on two streams: opt-in, measured no faster (the side
-# stream's weight gradients already fill those CUs: A/B 22.49-22.54 off vs 22.56-22.59 on)
-_ATTN_SPLIT = os.environ.get("FS2_ATTN_SPLIT", "0") not in ("", "0")
+_BIG_SLICES = not N.exp_flag("FS2_NO_WGRAD_BIG_SLICES")
+_SLICE_TARGET = N.exp_int("FS2_WGRAD_SLICE_TARGET", 240)
+# serial mode for per-call-site timing (bench.py --detail runs with the experiments library)
+_NO_SIDE = N.exp_flag("FS2_NO_SIDE_STREAM")
+_NO_AUX = N.exp_flag("FS2_NO_AUX_STREAM")
 
 
 def wgrad_slices(O, Ncols, ldc, K, dt, n_cu=256):
@@ -288,46 +278,6 @@ class FS2Engine:
                 rng.append((off, k))
         return rng
 
-    def _group_tables(self):
-        """per backward group (model.group_tag): fs2_adamw_prep tables over that group's GEMM
-        weights and its other parameters"""
-        if getattr(self, "_gtables", None) is None:
-            from .model import group_tag
-            if self._wtable is None:
-                self.prepare_weights(force=True)
-            wl, rl = {}, {}
-            for name, off, k, _, key in self.m._layout:
-                tag = group_tag(key)
-                if name in self._wspecs:
-                    wl.setdefault(tag, []).append(self._wentries[name])
-                    continue
-                r = rl.setdefault(tag, [])
-                if r and off - (r[-1][0] + r[-1][1]) < 16:
-                    r[-1] = (r[-1][0], off + k - r[-1][0])
-                else:
-                    r.append((off, k))
-            self._gtables = {
-                tag: (ops.weight_prep_table(wl[tag]) if tag in wl else (None, 0, 0),
-                      ops.adamw_ranges_table(rl.get(tag, []), self.dev))
-                for tag in list(wl) + [t for t in rl if t not in wl]}
-        return self._gtables
-
-    def adamw_group(self, tag, opt, decay_mul, omb1, beta2, omb2, step_size, bc2_sqrt, eps,
-                    gscale):
-        """AdamW + weight images of one backward group's parameters on the current stream: the
-        train step runs it as soon as the group's gradients are complete (the same per-element
-        update as ``adamw_step``, so the result is bit-identical)"""
-        m = self.m
-        wt, rt = self._group_tables()[tag]
-        ops.adamw_prep(wt, rt, m._flat, m._gflat, opt.exp_avg, opt.exp_avg_sq, decay_mul, omb1,
-                       beta2, omb2, step_size, bc2_sqrt, eps, gscale, dt=self.dt)
-
-    def adamw_groups_done(self):
-        """after every group's update: the next forward finds the weight images current"""
-        m = self.m
-        m.mark_params_updated()
-        self._prepared_version = (m._param_version, m._flat._version)
-
     def adamw_step(self, opt, decay_mul, omb1, beta2, omb2, step_size, bc2_sqrt, eps, gscale):
         """AdamW over the flat buffers fused with the GEMM weight images (fs2_adamw_prep): the
         next forward's prepare_weights finds them current and skips its own pass."""
@@ -484,15 +434,10 @@ class FS2Engine:
         del Ao
         F = self._wspecs[prefix + "pos_ffn.0.conv.weight"][0]
         Hc = self.empty(M, F)
-        # bf16: the conv1 epilogue also packs the ReLU pattern (Hc > 0) into F/8 bytes per row,
-        # which the conv2 data gradient reads as its gate instead of the 2F bytes of Hc
-        Hmask = (torch.empty(M, F // 8, dtype=torch.uint8, device=self.dev)
-                 if self.dt == N.BF16 and F % 8 == 0 and _RELU_BITS else None)
-        mask_kw = dict(relu_mask=Hmask, ldm=F // 8) if Hmask is not None else {}
         tag = "ffn_conv1_fwd." + prefix.split(".")[0]
         self._tic(tag)
         self._fwd(X1, D, M, T, prefix + "pos_ffn.0.conv.weight", Hc, F,
-                  bias=P[prefix + "pos_ffn.0.conv.bias"], relu=1, **mask_kw)
+                  bias=P[prefix + "pos_ffn.0.conv.bias"], relu=1)
         self._toc(tag)
         Y = self.empty(M, D)
         self._fwd(Hc, F, M, T, prefix + "pos_ffn.2.conv.weight", Y, D,
@@ -505,7 +450,6 @@ class FS2Engine:
                    mean2, rstd2, M, D, dt=self.dt, seed=seed, r=Y, ldr=D, p_r=p_drop, salt_r=s_r2,
                    s_out=s2)
         ctx.update(QKV=QKV, Pm=Pm, Pd=Pd, Att=Att, X1=X1, s1=s1, mean1=mean1, rstd1=rstd1, Hc=Hc,
-                   Hmask=Hmask,
                    s2=s2, mean2=mean2, rstd2=rstd2, s_att=s_att, s_r1=s_r1, s_r2=s_r2, F=F,
                    ldt=ldt)
         return X2, ctx
@@ -526,24 +470,15 @@ class FS2Engine:
         w1 = prefix + "pos_ffn.0.conv.weight"
         dHc = self.empty(M, F)
         dX1 = self.empty(M, D)
-        Hm = ctx.get("Hmask")
-        gbits = dict(gate_bits=Hm, ldgb=F // 8) if Hm is not None else {}
-        if _WGRAD_EARLY:
-            # weight gradients enqueued as soon as their operands exist (the side stream waits
-            # for everything queued on main so far): conv2's before its data gradient, conv1's
-            # right after dHc, so the two big conv1 GEMMs overlap instead of the conv1 weight
-            # gradient holding every CU while main's out-projection waits behind it
-            self._wgrad(dY, D, ctx["Hc"], F, M, T, w2)
-            self._dgrad(dY, D, M, T, w2, dHc, F, gate=ctx["Hc"], ldg=F, **gbits)
-            self._wgrad(dHc, F, ctx["X1"], D, M, T, w1)
-            self._bias_grad(dHc, F, M, F, prefix + "pos_ffn.0.conv.bias")
-            self._dgrad(dHc, F, M, T, w1, dX1, D, residual=ds2, ldr=D)
-        else:
-            self._dgrad(dY, D, M, T, w2, dHc, F, gate=ctx["Hc"], ldg=F, **gbits)
-            self._wgrad(dY, D, ctx["Hc"], F, M, T, w2)
-            self._dgrad(dHc, F, M, T, w1, dX1, D, residual=ds2, ldr=D)
-            self._wgrad(dHc, F, ctx["X1"], D, M, T, w1)
-            self._bias_grad(dHc, F, M, F, prefix + "pos_ffn.0.conv.bias")
+        # weight gradients enqueued as soon as their operands exist (the side stream waits for
+        # everything queued on main so far): conv2's before its data gradient, conv1's right
+        # after dHc, so the two big conv1 GEMMs overlap instead of the conv1 weight gradient
+        # holding every CU while main's out-projection waits behind it
+        self._wgrad(dY, D, ctx["Hc"], F, M, T, w2)
+        self._dgrad(dY, D, M, T, w2, dHc, F, gate=ctx["Hc"], ldg=F)
+        self._wgrad(dHc, F, ctx["X1"], D, M, T, w1)
+        self._bias_grad(dHc, F, M, F, prefix + "pos_ffn.0.conv.bias")
+        self._dgrad(dHc, F, M, T, w1, dX1, D, residual=ds2, ldr=D)
         del dY, dHc, ds2
         lnws = self.ws(ops.ln_ws(M, D))
         ds1, dAo = self.empty(M, D), self.empty(M, D)
@@ -555,12 +490,8 @@ class FS2Engine:
         del dX1
         wo = prefix + "self_att.att.out_proj.weight"
         dAtt = self.empty(M, D)
-        if _WGRAD_EARLY:
-            self._wgrad(dAo, D, ctx["Att"], D, M, T, wo)
-            self._dgrad(dAo, D, M, T, wo, dAtt, D)
-        else:
-            self._dgrad(dAo, D, M, T, wo, dAtt, D)
-            self._wgrad(dAo, D, ctx["Att"], D, M, T, wo)
+        self._wgrad(dAo, D, ctx["Att"], D, M, T, wo)
+        self._dgrad(dAo, D, M, T, wo, dAtt, D)
         del dAo
         QKV, Pm, Pd = ctx["QKV"], ctx["Pm"], ctx["Pd"]
         if "lse" in ctx:     # fused attention backward (dQ, dK, dV in one pass each)
@@ -571,17 +502,7 @@ class FS2Engine:
             args = (QKV, 3 * D, ctx["key_pad"], ctx["Att"], D, dAtt, D, ctx["lse"], B, H, T, dh,
                     1.0 / math.sqrt(dh), p_drop, seed, ctx["s_att"], dQKV, 3 * D)
             ws = self.ws(ops.attn_ws(B, H, T))
-            if self._aux is not None and _ATTN_SPLIT and -(-T // 128) * B * H < 256:
-                # dQ and dK/dV blocks each fill < 1 round of the 256 CUs (the encoder): run
-                # them on two streams after the shared D = rowsum(dO*O) pass
-                ops.attn_bwd_stage(0, *args, dt=self.dt, ws=ws)
-                h = self._aux_fork(QKV, ctx["key_pad"], dAtt, ctx["lse"], dQKV, ws)
-                ops.attn_bwd_stage(2, *args, dt=self.dt, ws=ws)
-                self._aux_exit(h)
-                ops.attn_bwd_stage(1, *args, dt=self.dt, ws=ws)
-                self._aux_join(h[1])
-            else:
-                ops.attn_bwd(*args, dt=self.dt, ws=ws)
+            ops.attn_bwd(*args, dt=self.dt, ws=ws)
             if tag:
                 self._toc(tag)
             return self._qkv_bwd(dQKV, ctx, M, T, D, prefix, ds1)
@@ -613,14 +534,9 @@ class FS2Engine:
     def _qkv_bwd(self, dQKV, ctx, M, T, D, prefix, ds1):
         wi = prefix + "self_att.att.in_proj_weight"
         dX = self.empty(M, D)
-        if _WGRAD_EARLY:
-            self._wgrad(dQKV, 3 * D, ctx["X"], D, M, T, wi)
-            self._bias_grad(dQKV, 3 * D, M, 3 * D, prefix + "self_att.att.in_proj_bias")
-            self._dgrad(dQKV, 3 * D, M, T, wi, dX, D, residual=ds1, ldr=D)
-        else:
-            self._dgrad(dQKV, 3 * D, M, T, wi, dX, D, residual=ds1, ldr=D)
-            self._wgrad(dQKV, 3 * D, ctx["X"], D, M, T, wi)
-            self._bias_grad(dQKV, 3 * D, M, 3 * D, prefix + "self_att.att.in_proj_bias")
+        self._wgrad(dQKV, 3 * D, ctx["X"], D, M, T, wi)
+        self._bias_grad(dQKV, 3 * D, M, 3 * D, prefix + "self_att.att.in_proj_bias")
+        self._dgrad(dQKV, 3 * D, M, T, wi, dX, D, residual=ds1, ldr=D)
         return dX
 
     # ------------------------------------------------------------------ variance predictor

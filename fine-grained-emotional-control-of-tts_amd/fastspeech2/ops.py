@@ -38,12 +38,9 @@ def round_up(x, m):
 def gemm(M, N_, K, A, lda, B, ldb, C, ldc, *, dt, a_kmajor=1, b_kmajor=1, conv=None, c_fp32=0,
          c_conv_kw=0, bias=None, relu=0, gate=None, ldg=0, row_scale=None, residual=None, ldr=0,
          row_scale_post=None, accumulate=0, split_k=1, split_stride=0, kvalid=0, mvalid=0,
-         nvalid=0, batch=1, batch_div=1, strides=None, conv_dil=1, relu_mask=None, ldm=0,
-         gate_bits=None, ldgb=0):
+         nvalid=0, batch=1, batch_div=1, strides=None, conv_dil=1):
     d = N.GemmDesc()
     d.conv_dil = conv_dil
-    d.relu_mask, d.ldm = _p(relu_mask), ldm
-    d.gate_bits, d.ldgb = _p(gate_bits), ldgb
     d.M, d.N, d.K, d.kvalid, d.mvalid, d.nvalid, d.dtype = M, N_, K, kvalid, mvalid, nvalid, dt
     d.A, d.lda, d.a_kmajor = _p(A), lda, a_kmajor
     d.B, d.ldb, d.b_kmajor = _p(B), ldb, b_kmajor
@@ -114,16 +111,6 @@ def attn_fwd(qkv, ldq, key_pad, B, H, T, dh, scale, p_drop, seed, salt, out, ldo
     _chk(N.lib().fs2_attn_fwd(_p(qkv), ldq, _p(key_pad), mask_mode, B, H, T, dh, scale, p_drop,
                               seed & 0xffffffff, salt, _p(out), ldo, _p(lse), dt, _s()),
          "fs2_attn_fwd")
-
-
-def attn_bwd_stage(stage, qkv, ldq, key_pad, out, ldo, dout, lddo, lse, B, H, T, dh, scale,
-                   p_drop, seed, salt, dqkv, lddq, *, dt, ws, mask_mode=1):
-    """one stage of ``attn_bwd``: 0 = D = rowsum(dO*O) into ws, 1 = dQ, 2 = dK/dV (1 and 2
-    read D, in either order or concurrently)."""
-    _chk(N.lib().fs2_attn_bwd_stage(_p(qkv), ldq, _p(key_pad), mask_mode, _p(out), ldo, _p(dout),
-                                    lddo, _p(lse), B, H, T, dh, scale, p_drop, seed & 0xffffffff,
-                                    salt, _p(dqkv), lddq, _p(ws), dt, stage, _s()),
-         "fs2_attn_bwd_stage")
 
 
 def attn_bwd(qkv, ldq, key_pad, out, ldo, dout, lddo, lse, B, H, T, dh, scale, p_drop, seed, salt,

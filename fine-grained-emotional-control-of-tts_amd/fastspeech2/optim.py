@@ -8,14 +8,14 @@ model's engine exists (the GEMM weights tile by tile, writing the next forward's
 images from the updated values; the rest element-wise), else ``fs2_adamw``.
 """
 
-import os
 
 import torch
 
+from . import _native as N
 from . import ops
 
 # FS2_NO_FUSED_ADAMW=1: separate AdamW pass + weight-image pass at the next forward (A/B runs)
-_NO_FUSED = os.environ.get("FS2_NO_FUSED_ADAMW", "0") not in ("", "0")
+_NO_FUSED = N.exp_flag("FS2_NO_FUSED_ADAMW")
 
 
 class FusedAdamW:

@@ -99,16 +99,6 @@ class GradBucketer:
 # 1.50 ms graph): the replayed multi-stream graph leaves more gaps between kernels than the
 # eager launches, whose host issue time (8-12 ms/step) is already below the GPU time
 _GRAPH = os.environ.get("FS2_GRAPH", "0") not in ("", "0")
-# opt-in: A/B 20.55-20.61 ms off vs 20.59-20.68 ms on (the persistent GEMMs' blocks are all
-# resident from launch, so queue priority changes little)
-_PRIO = os.environ.get("FS2_PRIO", "0") not in ("", "0")
-# single process, opt-in (FS2_EARLY_ADAMW=1): AdamW per backward group as soon as the group's
-# gradients are complete, on its own stream.  Measured slower (A/B 21.19 vs 20.44 ms/step):
-# the update's blocks take CUs the persistent GEMM kernels expect to hold
-_EARLY = os.environ.get("FS2_EARLY_ADAMW", "0") not in ("", "0")
-# opt-in (FS2_ZERO_SIDE=1): the gradient memset on the weight-gradient side stream, beside the
-# forward, instead of on the step's stream before it (A/B 20.35-20.39 vs 20.36-20.40 ms: neutral)
-_ZERO_SIDE = os.environ.get("FS2_ZERO_SIDE", "0") not in ("", "0")
 
 
 class _StepGraph:
@@ -167,12 +157,13 @@ class FusedTrainer:
             self.bucketer = GradBucketer(model._gflat, model.group_ranges(), bucket_bytes)
             self.eng.on_grads_ready = self.bucketer.ready
         self.seed = 0
-        # DP steps stay eager: their bucketed all-reduces are issued from the backward hooks
+        # DP steps stay eager: their bucketed all-reduces are issued from the backward hooks,
+        # and a captured step would record none of them (its warm-up pass already fired every
+        # bucket), so graph replay is refused there rather than silently unreduced
+        if graph and self.world > 1:
+            raise ValueError("FusedTrainer(graph=True) needs world size 1")
         self.use_graph = (self.world == 1 and _GRAPH) if graph is None else bool(graph)
         self._graphs = {}
-        self._prio = None
-        self._opt_stream = None       # per-group AdamW beside the backward (single process)
-        self._early_done = set()
 
     def _graph_for(self, batch, intensity, mel_len_max):
         key = tuple(tuple(t.shape) for t in batch[:8]) + (tuple(intensity.shape), mel_len_max)
@@ -189,19 +180,7 @@ class FusedTrainer:
         produces them).  Returns the loss vector."""
         (phoneme, spk_ids, phon_len, mel_tgt, pitch_tgt, energy_tgt, duration_tgt, mel_len) = batch[:8]
         m = self.model
-        main = torch.cuda.current_stream(m._flat.device) if m._flat.is_cuda else None
-        if self._opt_stream is not None:
-            # the previous step's group updates read and write the flat buffers
-            main.wait_stream(self._opt_stream)
-        side = self.eng._side if _ZERO_SIDE else None
-        if side is not None:
-            # the 341 MB gradient memset runs on the (idle) weight-gradient stream beside the
-            # forward; the backward, the first writer of any gradient, waits for it
-            side.wait_stream(main)
-            with torch.cuda.stream(side):
-                m._gflat.zero_()
-        else:
-            m._gflat.zero_()
+        m._gflat.zero_()
         out, ctx = self.eng.forward(phoneme, spk_ids, duration_tgt, pitch_tgt, energy_tgt,
                                     intensity=intensity, training=True,
                                     seed=self.seed if seed is None else seed,
@@ -211,50 +190,7 @@ class FusedTrainer:
         loss, grads = fused_loss(mel, post, pd, pp.view(pd.shape), pe.view(pd.shape), mel_tgt,
                                  duration_tgt, avg_p.view(pd.shape), avg_e.view(pd.shape), mel_len,
                                  phon_len, self.weights)
-        if side is not None:
-            main.wait_stream(side)
         self.eng.backward(ctx, *grads)
-        return loss
-
-    def _early_hook(self, args):
-        """on_grads_ready hook of a single-process step: AdamW of a backward group on the
-        optimizer stream once its gradients are queued on the main and side streams -- the
-        HBM-bound update then runs under the MFMA-bound backward of the groups after it"""
-        s = self._opt_stream
-        done = self._early_done
-
-        def hook(tag, streams):
-            for st in streams:
-                s.wait_stream(st)
-            with torch.cuda.stream(s):
-                self.eng.adamw_group(tag, self.opt, *args)
-            done.add(tag)
-        return hook
-
-    def _early_on(self):
-        return (self.world == 1 and _EARLY and not self.use_graph and self.model._flat.is_cuda
-                and self.opt.fused_images())
-
-    def _step_early(self, batch, intensity, mel_len_max):
-        if self._opt_stream is None:
-            self._opt_stream = torch.cuda.Stream(self.model._flat.device)
-        self.eng._group_tables()
-        args = self.opt.begin_step(1.0)
-        self._early_done = set()
-        self.eng.on_grads_ready = self._early_hook(args)
-        try:
-            loss = self.forward_backward(batch, intensity, mel_len_max)
-        finally:
-            self.eng.on_grads_ready = None
-        main = torch.cuda.current_stream(self.model._flat.device)
-        missing = [t for t in self.eng._group_tables() if t not in self._early_done]
-        if missing:                      # defensive: groups the backward never reported
-            self._opt_stream.wait_stream(main)
-            with torch.cuda.stream(self._opt_stream):
-                for t in missing:
-                    self.eng.adamw_group(t, self.opt, *args)
-        main.wait_stream(self._opt_stream)
-        self.eng.adamw_groups_done()
         return loss
 
     def apply(self):
@@ -265,35 +201,11 @@ class FusedTrainer:
 
     def step(self, batch, intensity, mel_len_max=None):
         self.seed += 1
-        prio = self._prio_stream()
-        if prio is None:
-            return self._step(batch, intensity, mel_len_max)
-        # the data-gradient chain is the critical path; the weight-gradient side stream and the
-        # predictor aux stream (normal priority) fill the CUs it leaves idle
-        caller = torch.cuda.current_stream(self.model._flat.device)
-        prio.wait_stream(caller)
-        for t in list(batch[:8]) + [intensity]:
-            if t is not None and t.is_cuda:
-                t.record_stream(prio)
-        with torch.cuda.stream(prio):
-            loss = self._step(batch, intensity, mel_len_max)
-        caller.wait_stream(prio)
-        loss.record_stream(caller)
-        return loss
-
-    def _prio_stream(self):
-        """high-priority stream the step runs on (FS2_PRIO=1; default: the caller's stream)"""
-        if not _PRIO or self.use_graph or not self.model._flat.is_cuda:
-            return None
-        if self._prio is None:
-            lo, hi = torch.cuda.Stream.priority_range()
-            self._prio = torch.cuda.Stream(self.model._flat.device, priority=hi)
-        return self._prio
-
-    def _step(self, batch, intensity, mel_len_max):
-        if self._early_on():
-            return self._step_early(batch, intensity, mel_len_max)
         if self.use_graph:
+            if self.world > 1:
+                raise RuntimeError("FusedTrainer: graph replay under data parallelism is not "
+                                   "supported (the bucket all-reduces are issued from the "
+                                   "backward hooks); use the eager step")
             mlm = mel_len_max if mel_len_max is not None else batch[3].shape[1]
             loss = self._graph_for(batch, intensity, mlm).replay(batch, intensity, self.seed)
         else:

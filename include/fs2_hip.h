@@ -73,13 +73,6 @@ typedef struct fs2_gemm_desc {
   int batch, batch_div;
   int64_t sA1, sA2, sB1, sB2, sC1, sC2, sR1, sR2;
   int conv_dil;         /* dilation of conv modes 1 / 5 (tap j reads row t + (j-P)*dil); 0 = 1 */
-  /* bf16 only.  relu_mask: also write bit (n % 8) of relu_mask[m*ldm + n/8] = (stored C > 0), the
-   * FFN conv1 forward's ReLU pattern (SB pos_ffn, model.py:241-267) in 1/16 of the bytes of C;
-   * needs nvalid % 8 == 0, batch 1, no split.  gate_bits: the same packed pattern used as the
-   * gate instead of re-reading gate's bf16 values (gate must still be given: kernels that
-   * do not read the bits fall back to it).                                                  */
-  uint8_t* relu_mask; int64_t ldm;
-  const uint8_t* gate_bits; int64_t ldgb;
 } fs2_gemm_desc;
 
 int fs2_gemm(const fs2_gemm_desc* d, void* stream);
@@ -163,15 +156,6 @@ int fs2_attn_bwd(const void* qkv, int64_t ldq, const uint8_t* key_pad, int mask_
                  int T, int dh, float scale, float p_drop, uint32_t seed, uint32_t salt,
                  void* dqkv, int64_t lddq, float* workspace, int dtype, void* stream);
 int64_t fs2_attn_workspace_floats(int B, int H, int T);
-/* fs2_attn_bwd in three stream-ordered stages, so dQ and dK/dV can run on two streams when one
- * alone underfills the chip: stage 0 writes D = rowsum(dO*O) into workspace, then stage 1 (dQ)
- * and stage 2 (dK, dV) both read it (each after stage 0; no order between 1 and 2).  Results
- * are bit-identical to fs2_attn_bwd.                                                       */
-int fs2_attn_bwd_stage(const void* qkv, int64_t ldq, const uint8_t* key_pad, int mask_mode,
-                       const void* out, int64_t ldo, const void* dout, int64_t lddo,
-                       const float* lse, int B, int H, int T, int dh, float scale, float p_drop,
-                       uint32_t seed, uint32_t salt, void* dqkv, int64_t lddq, float* workspace,
-                       int dtype, int stage, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Token embedding + positional encoding + pad mask (K1, K2; model.py:331-337)

@@ -349,65 +349,3 @@ def test_fused_adamw_writes_the_weight_images(cuda, cfg_all, dtname, monkeypatch
         assert torch.equal(w1[k][0], w2[k][0]), k
         assert torch.equal(w1[k][1], w2[k][1]), k
 
-
-def test_per_group_adamw_equals_one_pass(cuda, cfg_all):
-    """The single-process step can update each backward group on its own stream as soon as
-    its gradients are complete (FusedTrainer._step_early, FS2_EARLY_ADAMW=1): the per-group fs2_adamw_prep launches
-    cover every parameter once and equal the one-pass update bit for bit -- parameters, both
-    moments, every Wf / Wb weight image; and an early-update step matches a one-pass step on
-    the same initial weights within the split-K atomic noise."""
-    from fastspeech2.model import FastSpeech2
-    from fastspeech2.train import FusedTrainer
-    from fastspeech2 import train as train_mod
-    from fastspeech2.synthetic import make_batch, as_tuple
-    kw = dict(cfg_all["model"]["fastspeech2"], enc_num_layers=2, dec_num_layers=2)
-    b = make_batch(B=8, tp_min=60, tp_max=90, seed=23, device="cuda")
-    bt, inten = as_tuple(b)
-    torch.manual_seed(0)
-    m = FastSpeech2(**kw, n_speakers=4, act_dtype=torch.bfloat16).cuda().train()
-    tr = FusedTrainer(m, lr=1e-3)
-    eng = tr.eng
-    tr.forward_backward(bt, inten)
-    torch.cuda.synchronize()
-    tabs = eng._group_tables()
-    assert set(tabs) == {t for t, _, _ in m.group_ranges()}
-    state0 = [t.clone() for t in (m._flat, tr.opt.exp_avg, tr.opt.exp_avg_sq)]
-    args = tr.opt.begin_step(1.0)
-    out = []
-    for per_group in (True, False):
-        for dst, src in zip((m._flat, tr.opt.exp_avg, tr.opt.exp_avg_sq), state0):
-            dst.copy_(src)
-        for Wf, Wb in eng.w.values():
-            Wf.fill_(float("nan"))
-            Wb.fill_(float("nan"))
-        if per_group:
-            for tag in tabs:
-                eng.adamw_group(tag, tr.opt, *args)
-        else:
-            eng.adamw_step(tr.opt, *args)
-        torch.cuda.synchronize()
-        out.append([m._flat.clone(), tr.opt.exp_avg.clone(), tr.opt.exp_avg_sq.clone()] +
-                   [t.clone() for pair in eng.w.values() for t in pair])
-    assert not torch.equal(out[0][0], state0[0])
-    for a, c in zip(*out):
-        assert torch.equal(a, c)
-    res = {}
-    saved = train_mod._EARLY
-    for early in (True, False):
-        train_mod._EARLY = early
-        try:
-            torch.manual_seed(0)
-            m = FastSpeech2(**kw, n_speakers=4, act_dtype=torch.bfloat16).cuda().train()
-            tr = FusedTrainer(m, lr=1e-4)
-            losses = [tr.step(bt, inten).clone() for _ in range(3)]
-            torch.cuda.synchronize()
-            assert (tr._opt_stream is not None) == early
-            res[early] = (torch.stack(losses).cpu(), m._flat.cpu())
-        finally:
-            train_mod._EARLY = saved
-    (le, pe), (ll, pl) = res[True], res[False]
-    assert torch.equal(le[0], ll[0])
-    assert torch.allclose(le, ll, rtol=1e-4, atol=0)
-    dp = (pe - pl).abs()
-    assert dp.max().item() <= 3 * 2.1e-4
-    assert (dp > 1e-6).float().mean().item() <= 1e-3

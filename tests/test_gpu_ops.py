@@ -491,38 +491,6 @@ def test_gemm_persistent_long_k(cuda, M, N, K, c32):
     assert (C2[:, N:] == 0).all()
 
 
-@pytest.mark.parametrize("M,T", [(31264, 977), (6400, 200), (1000, 250), (200, 50)])
-def test_relu_bits_gate(cuda, M, T):
-    """bf16 FFN pair through the packed ReLU pattern: the conv1 forward (implicit reflect conv,
-    bias + ReLU) also writes bit n%8 of mask[m][n/8] = (stored output > 0), and the conv2 data
-    gradient reading those bits as its gate equals the one re-reading the bf16 activations,
-    bit for bit (decoder / encoder shapes, a small ragged one, and M = 200, whose GEMMs take the
-    128x128 kernel: its mask is packed from C by a separate pass)."""
-    from fastspeech2 import ops
-    torch.manual_seed(M)
-    C, F, KW = 384, 1536, 9
-    X = (torch.randn(M, C, device=cuda) * 0.5).to(torch.bfloat16)
-    W1 = (torch.randn(F, KW * C, device=cuda) * 0.03).to(torch.bfloat16)
-    b1 = torch.randn(F, device=cuda) * 0.1
-    H = torch.empty(M, F, device=cuda, dtype=torch.bfloat16)
-    mask = torch.full((M, F // 8), 0xA5, device=cuda, dtype=torch.uint8)
-    ops.gemm(M, F, KW * C, X, C, W1, KW * C, H, F, dt=1, conv=(1, T, KW, C), bias=b1, relu=1,
-             relu_mask=mask, ldm=F // 8)
-    bits = (H.float() > 0).to(torch.uint8).view(M, F // 8, 8)
-    ref = (bits << torch.arange(8, device=cuda, dtype=torch.uint8)).sum(-1).to(torch.uint8)
-    assert torch.equal(mask, ref)
-    dY = (torch.randn(M, C, device=cuda) * 0.5).to(torch.bfloat16)
-    W2b = (torch.randn(F, C, device=cuda) * 0.05).to(torch.bfloat16)    # [F][C]: K-major
-    outs = []
-    for gb in (None, mask):
-        dH = torch.empty(M, F, device=cuda, dtype=torch.bfloat16)
-        kw = dict(gate_bits=gb, ldgb=F // 8) if gb is not None else {}
-        ops.gemm(M, F, C, dY, C, W2b, C, dH, F, dt=1, gate=H, ldg=F, **kw)
-        outs.append(dH)
-    assert torch.equal(outs[0], outs[1])
-    assert rel(outs[1], torch.where(H.float() > 0, dY.float() @ W2b.float().t(), 0.0)) < 1e-2
-
-
 def test_gemm_short_k_two_streams(cuda):
     """The persistent short-K kernel (gemm_pk_kernel) under concurrency: 40 back-to-back
     launches alternating between two streams (different tile counts, nk = 1 and nk = 6, bias
@@ -605,18 +573,10 @@ def _keep_np(seed, salt, idx, p):
     return bits >= np.uint64(int(p * 65536 + 0.5))
 
 
-@pytest.fixture(params=["v16", "v32"])
-def attn_variant(request, monkeypatch):
-    """the default 16x16x32 attention kernels and the opt-in 32x32x16 ones (FS2_ATTN_V32=1,
-    read by the library at every launch)"""
-    monkeypatch.setenv("FS2_ATTN_V32", "1" if request.param == "v32" else "0")
-    return request.param
-
-
 @pytest.mark.parametrize("dh,T,p_drop,B", [(192, 150, 0.0, 3), (192, 150, 0.1, 3), (64, 70, 0.1, 3),
                                             (256, 130, 0.0, 3), (192, 977, 0.0, 32),
                                             (192, 200, 0.0, 32), (128, 300, 0.1, 4)])
-def test_fused_attention_vs_torch(cuda, dh, T, p_drop, B, attn_variant):
+def test_fused_attention_vs_torch(cuda, dh, T, p_drop, B):
     """fs2_attn_fwd/bwd (bf16) against torch fp32 on the same bf16 Q/K/V: the head-major mask
     tiling rule, ragged lengths, and (p > 0) the counter-hash dropout masks restated in numpy.
     B=32 with T=977 / 200 are the bench's decoder / encoder shapes: 128-row (W8 = 8) blocks for
@@ -669,41 +629,6 @@ def test_fused_attention_vs_torch(cuda, dh, T, p_drop, B, attn_variant):
     for i, t in enumerate((q, k, v)):
         r = t.grad.permute(0, 2, 1, 3).reshape(B * T, D)
         assert rel(dqkv[:, i * D:(i + 1) * D], r) < 3e-2, i
-
-
-@pytest.mark.parametrize("dh,T,p_drop", [(192, 200, 0.1), (64, 70, 0.0)])
-def test_attention_backward_stages_equal_fused(cuda, dh, T, p_drop, attn_variant):
-    """fs2_attn_bwd_stage: D pass, then dQ and dK/dV on two streams, bit-identical to the
-    one-call fs2_attn_bwd (the engine splits the encoder's backward this way)."""
-    from fastspeech2 import ops
-    torch.manual_seed(dh * T)
-    B, H = 4, 2
-    D = H * dh
-    qkv = (torch.randn(B * T, 3 * D, device=cuda) * 0.5).to(torch.bfloat16)
-    kp = torch.zeros(B, T, dtype=torch.uint8, device=cuda)
-    for b, L in enumerate([T, T - 11, T - 40, 5]):
-        kp[b, L:] = 1
-    scale = 1.0 / math.sqrt(dh)
-    out = torch.empty(B * T, D, device=cuda, dtype=torch.bfloat16)
-    lse = torch.empty(B * H, T, device=cuda)
-    ops.attn_fwd(qkv, 3 * D, kp, B, H, T, dh, scale, p_drop, 9, 4, out, D, lse, dt=1)
-    dout = torch.randn(B * T, D, device=cuda).to(torch.bfloat16)
-    args = (qkv, 3 * D, kp, out, D, dout, D, lse, B, H, T, dh, scale, p_drop, 9, 4)
-    ref = torch.full((B * T, 3 * D), float("nan"), device=cuda, dtype=torch.bfloat16)
-    ws = torch.empty(int(ops.attn_ws(B, H, T)), device=cuda)
-    ops.attn_bwd(*args, ref, 3 * D, dt=1, ws=ws)
-    got = torch.full_like(ref, float("nan"))
-    ws2 = torch.empty_like(ws)
-    ops.attn_bwd_stage(0, *args, got, 3 * D, dt=1, ws=ws2)
-    side = torch.cuda.Stream()
-    side.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(side):
-        ops.attn_bwd_stage(2, *args, got, 3 * D, dt=1, ws=ws2)
-    ops.attn_bwd_stage(1, *args, got, 3 * D, dt=1, ws=ws2)
-    torch.cuda.current_stream().wait_stream(side)
-    torch.cuda.synchronize()
-    assert torch.equal(ws, ws2)
-    assert torch.equal(got, ref)
 
 
 def test_weight_prep_batched_layouts(cuda):

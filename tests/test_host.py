@@ -52,15 +52,10 @@ def test_gemm_host_validation_rejects_bad_args():
     d.A = p16 + 2
     assert lib.fs2_gemm(ctypes.byref(d), None) == -2          # misaligned pointer
     d.A = p16
-    d.relu_mask, d.ldm = p16, 1
-    assert lib.fs2_gemm(ctypes.byref(d), None) == -1          # relu_mask: ldm * 8 < nvalid
-    d.ldm, d.c_fp32 = 2, 1
-    assert lib.fs2_gemm(ctypes.byref(d), None) == -1          # relu_mask needs a bf16 output
-    d.c_fp32, d.relu_mask, d.ldm = 0, None, 0
-    d.gate_bits, d.ldgb = p16, 2
-    assert lib.fs2_gemm(ctypes.byref(d), None) == -1          # gate_bits without its gate
+    d.split_k, d.c_fp32 = 2, 0
+    assert lib.fs2_gemm(ctypes.byref(d), None) == -1          # split-K needs an fp32 output
+    d.split_k = 1
     assert lib.fs2_loss_fwd_bwd(None, None) == -1
-    assert lib.fs2_gemm_workspace if hasattr(lib, "fs2_gemm_workspace") else True
 
 
 def _tiny_cfg():

@@ -1,6 +1,5 @@
 """Fused attention fwd / bwd timing at the bench's decoder (T=977) and encoder (T=200) shapes,
-B=32, H=2, dh=192, with and without probability dropout.  FS2_ATTN_V32=1 selects the 32x32x16
-kernels (read per launch)."""
+B=32, H=2, dh=192, with and without probability dropout."""
 import math
 import os
 import sys

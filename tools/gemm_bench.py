@@ -10,6 +10,9 @@ import sys
 
 os.environ.setdefault("FS2_NO_SIDE_STREAM", "1")
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# the FS2_* switches act only in the experiments library (make ... experiments)
+os.environ.setdefault("FS2_HIP_LIB", os.path.join(ROOT, "fine-grained-emotional-control-of-tts_amd",
+                                                  "fastspeech2", "libfs2_hip_exp.so"))
 sys.path.insert(0, os.path.join(ROOT, "fine-grained-emotional-control-of-tts_amd"))
 sys.path.insert(0, ROOT)
 import torch  # noqa: E402
