@@ -491,6 +491,37 @@ def test_gemm_persistent_long_k(cuda, M, N, K, c32):
     assert (C2[:, N:] == 0).all()
 
 
+@pytest.mark.parametrize("M,N,K,conv", [(31264, 1152, 384, None), (6400, 384, 1536, None),
+                                         (31264, 1536, 3456, (1, 977, 9, 384)),
+                                         (31264, 384, 13824, (4, 977, 9, 1536)), (200, 80, 384, None)])
+def test_gemm_nan_passes_without_activation(cuda, M, N, K, conv):
+    """A NaN input row comes out NaN through every bf16 GEMM kernel family when the epilogue
+    has no activation (persistent short-K, 256x128, 256x256 implicit conv, persistent long-K
+    padded-domain conv, 128x128): the epilogue's 'no activation' is a select, not a max
+    against -inf, so NaN-based divergence checks still see the NaN."""
+    from fastspeech2 import ops
+    torch.manual_seed(K)
+    if conv is not None and conv[0] == 4:
+        T = conv[1]
+        M = (M // T) * (T + 2 * 4)            # padded-domain rows (T + 2P per utterance)
+        A = (torch.randn(31264, conv[3], device=cuda) * 0.5).to(torch.bfloat16)
+        A[5, :] = float("nan")
+        lda = conv[3]
+    else:
+        A = (torch.randn(M if conv is None else M, K if conv is None else conv[3], device=cuda)
+             * 0.5).to(torch.bfloat16)
+        A[5, :] = float("nan")
+        lda = A.shape[1]
+    W = (torch.randn(N, K, device=cuda) * 0.05).to(torch.bfloat16)
+    C = torch.zeros(M, N, device=cuda, dtype=torch.bfloat16)
+    ops.gemm(M, N, K, A, lda, W, K, C, N, dt=1, conv=conv)
+    torch.cuda.synchronize()
+    nan_rows = torch.isnan(C.float()).any(1).nonzero().flatten().tolist()
+    assert nan_rows, "the NaN input did not reach the output"
+    if conv is None:
+        assert nan_rows == [5]
+
+
 def test_gemm_short_k_two_streams(cuda):
     """The persistent short-K kernel (gemm_pk_kernel) under concurrency: 40 back-to-back
     launches alternating between two streams (different tile counts, nk = 1 and nk = 6, bias
