@@ -60,8 +60,9 @@ def synthesize(model, phonemes, speakers, intensities, pace=1.0, batched=True):
 
     phonemes: list of 1-D int64 token tensors; speakers: list / tensor of speaker ids;
     intensities: list of (T_i, n_emotions) tensors (or (1, T_i, n_emotions)).  Returns a list
-    of (T_mel_i, n_mels) mel tensors (PostNet output, ``model(...)[0]`` as the reference uses,
-    trimmed to the predicted mel length) and the list of mel lengths."""
+    of (T_mel_i, n_mels) mel tensors -- ``model(...)[0]`` as the reference's inference.py:82
+    uses, i.e. ``mel_post``, the mel-linear output BEFORE the PostNet residual
+    (model.py:430,433) -- trimmed to the predicted mel length, and the list of mel lengths."""
     dev = next(model.parameters()).device
     if not batched:
         mels, lens = [], []

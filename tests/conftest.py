@@ -18,6 +18,33 @@ for p in (ROOT, PKG):
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 
+# Observed parity errors recorded by GPU tests (``parity_log`` fixture): written at session end
+# to gpurun_out/parity_observed.json so a GPU run's numbers can be committed under profiles/
+# and quoted in DESIGN.md section 2 next to the asserted tolerances.
+_PARITY = {}
+
+
+@pytest.fixture(scope="session")
+def parity_log():
+    return _PARITY
+
+
+def pytest_sessionfinish(session, exitstatus):
+    if _PARITY:
+        import json
+        out = os.path.join(ROOT, "gpurun_out")
+        os.makedirs(out, exist_ok=True)
+        path = os.path.join(out, "parity_observed.json")
+        old = {}
+        if os.path.exists(path):
+            try:
+                old = json.load(open(path))
+            except ValueError:
+                old = {}
+        old.update(_PARITY)
+        json.dump(old, open(path, "w"), indent=1, sort_keys=True)
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP kernels through libfs2_hip.so)")
 

@@ -70,3 +70,56 @@ def test_synthesize_unbatched_equals_single_sentence_calls(cuda, cfg_all):
         assert L == int(po[7][0])
         if L > 0:
             assert rel(mel, po[0][0, :L]) <= 1e-3
+
+
+@pytest.mark.parametrize("dtname", ["float32", "bfloat16"])
+def test_config5_256_sentence_sweep_equals_oracle(cuda, cfg_all, dtname, parity_log):
+    """BASELINE config 5 at its batch size: 256 sentences (ragged, 20-70 phonemes) over the 5
+    emotions x 3 intensity levels (prototype lookup, inference.py:12-21) and 4 speakers, ONE
+    batched synthesis with predicted durations, against the oracle's forward on the same padded
+    batch (2 + 2 layers).  fp32: mel rel 1e-3, mel lengths exact; bf16: mel lengths exact on
+    the utterances whose predicted durations do not sit at a truncation edge, and the observed
+    errors recorded (parity_log)."""
+    from fastspeech2.inference import get_intensity_rep, synthesize
+    o, m = _pair(cfg_all, seed=8)
+    dt = getattr(torch, dtname)
+    if dt != torch.float32:
+        from fastspeech2.model import FastSpeech2
+        kw = dict(cfg_all["model"]["fastspeech2"], enc_num_layers=2, dec_num_layers=2)
+        mb = FastSpeech2(**kw, n_speakers=4, act_dtype=dt).cuda().eval()
+        mb.load_state_dict(m.state_dict())
+        m = mb
+    g = torch.Generator().manual_seed(5)
+    bank = _bank(2)
+    phs, spk, inten = [], [], []
+    for i in range(256):
+        n = int(torch.randint(20, 71, (1,), generator=g))
+        phs.append(torch.randint(1, 95, (n,), generator=g))
+        s, e, lv = i % 4, (i // 4) % 5, (i // 20) % 3
+        spk.append(s)
+        inten.append(get_intensity_rep(s, e, lv, n, bank)[0])
+    mels, lens = synthesize(m, phs, spk, inten)
+    Tp = max(p.numel() for p in phs)
+    tok = torch.zeros(256, Tp, dtype=torch.int64)
+    it = torch.zeros(256, Tp, 5)
+    for i, (p, x) in enumerate(zip(phs, inten)):
+        tok[i, :p.numel()] = p
+        it[i, :p.numel()] = x
+    torch.set_num_threads(max(1, min(32, torch.get_num_threads())))
+    with torch.no_grad():
+        po = o(tok, torch.tensor(spk), intensity=it)
+    ref_lens = po[7].tolist()
+    same = [i for i in range(256) if lens[i] == ref_lens[i]]
+    errs = [rel(mels[i], po[0][i, :lens[i]]) for i in same if lens[i] > 0]
+    parity_log[f"config5_256_sentences_{dtname}"] = {
+        "mel_rel_max": max(errs), "mel_rel_median": float(np.median(errs)),
+        "mel_len_equal": len(same), "sentences": 256, "frames": int(sum(lens))}
+    assert sum(lens) > 256 * 20
+    if dt == torch.float32:
+        assert lens == ref_lens
+        assert max(errs) <= 1e-3
+    else:
+        # bf16 log-durations differ by ~1e-2: a duration whose expm1 lands within that of an
+        # integer may truncate the other way (the reference's own .long() edge)
+        assert len(same) >= 0.9 * 256, len(same)
+        assert max(errs) <= 5e-2

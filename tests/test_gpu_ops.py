@@ -546,8 +546,10 @@ def test_gemm_short_k_two_streams(cuda):
     outs = []
     for i in range(40):
         M, N, K, A, W, bias, G, ref = data[i % len(data)]
-        C = torch.full((M, N), float("nan"), device=cuda, dtype=torch.bfloat16)
         with torch.cuda.stream(s1 if i % 2 == 0 else s2):
+            # the NaN fill on the GEMM's own stream: a fill on the default stream would race
+            # the launch (the two streams waited for the default stream only before the loop)
+            C = torch.full((M, N), float("nan"), device=cuda, dtype=torch.bfloat16)
             ops.gemm(M, N, K, A, K, W, K, C, N, dt=1, bias=bias, gate=G, ldg=N)
         outs.append((i, C))
     torch.cuda.synchronize()
