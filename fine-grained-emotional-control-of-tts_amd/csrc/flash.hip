@@ -53,7 +53,6 @@ struct AttnP {
   float scale, scale_log2, p_drop, inv_keep;
   uint32_t seed, salt;
   uint32_t thr16;                // dropout threshold (fs2_thr16)
-  int pair32;                    // every dropout pair index ((z*T+q)*T2 + k) / 2 < 2^32
 };
 
 __device__ __forceinline__ bf16x8 ld_frag(const bf16* g) { return *(const bf16x8*)g; }
@@ -343,247 +342,6 @@ __global__ void __launch_bounds__(W8 * 64 / QG, 1) attn_fwd_kernel(AttnP p) {
       *(u32x2*)(orow + 16 * d + 4 * g) = w;
     }
   }
-}
-
-// ============================================================================================
-// Forward with v_mfma_f32_32x32x16_bf16, 32 queries per wave (dh <= 192).
-//
-// Why: the 16x16 forward above runs at ~16 % MFMA busy (r03 PMC: 6.4 VALU instructions per
-// MFMA): per element it tests a mask byte, scales and selects, and it rescales its 48
-// accumulators whenever a row maximum moves, with every wave of the block in lock step between
-// two barriers per key tile, so the softmax VALU never overlaps another wave's MFMAs.
-// How:
-//  * S^T = K Q^T on the 32x32 shape: a lane owns one query and 16 keys of each 32-key block
-//    (the other 16 in lane ^ 32); P^T feeds O^T += V^T P^T straight from the registers, V^T read
-//    with ds_read_b64_tr_b16 over exactly the keys the lane holds (img32 image below).  One
-//    32x32x16 MFMA needs half the operand bytes of two 16x16x32 ones.
-//  * the softmax works in raw score units: row max over the raw S, one FMA per element builds
-//    the exp2 argument (scale folded), the row sum stays per half-wave until the end; tiles
-//    whose keys are all valid (the prefix of valid keys the block computes once) skip the mask.
-//  * the O rescale runs only when some lane's max moved (the row maxima settle after a few
-//    tiles); the dropout hash is the same pair hash and element index as every other path.
-//  * K/V tiles stream through a 3-buffer LDS-DMA ring, one barrier per tile (the barrier that
-//    releases tile t also certifies tile t-1 consumed, so tile t+2 may overwrite it).
-//  * O leaves as 16-byte stores: permlane32_swap pairs the two half-waves' 4-column groups.
-// ============================================================================================
-typedef __attribute__((ext_vector_type(16))) float f32x16;
-
-__device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-}
-
-// LDS image of a [rows][DH] bf16 tile: 8-row x 32-feature subtiles of 512 B, 16-byte chunk
-// (c & 3) ^ ((r >> 2) & 3) inside a subtile -- conflict-free for the 32x32x16 row reads
-// (ds_read_b128) and the transposed reads (ds_read_b64_tr_b16) alike.
-template <int DH>
-__device__ __forceinline__ int img32(int r, int c) {
-  return (r >> 3) * (16 * DH) + 512 * (c >> 2) + 64 * (r & 7) + 16 * ((c & 3) ^ ((r >> 2) & 3));
-}
-
-// row-operand fragment (token on the lane): rows r0 .. r0+31, features 16 s + 8 h .. +7
-template <int DH>
-__device__ __forceinline__ bf16x8 row32(const char* t, int r0, int s, int lane) {
-  return *(const bf16x8*)(t + img32<DH>(r0 + (lane & 31), 2 * s + (lane >> 5)));
-}
-
-// transposed fragment: k runs over tile rows kb + {4h .. 4h+3} (j < 4) and kb + 8 + {4h ..
-// 4h+3} (j >= 4), the lane's row / column is feature fb + (lane & 31)
-template <int DH>
-__device__ __forceinline__ bf16x8 tr32(const char* t, int kb, int fb, int lane) {
-  const int li = lane & 15, q = li >> 2, p = li & 3, h = lane >> 5, c16 = (lane >> 4) & 1;
-  const int col = fb + 16 * c16 + 4 * p;
-  const int c = col >> 3, boff = (col & 4) * 2;
-  const int r1 = kb + 4 * h + q;
-  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(t + img32<DH>(r1, c) + boff));
-  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(t + img32<DH>(r1 + 8, c) + boff));
-  const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(bf16x8, v);
-}
-
-// TR-row x DH tile into the img32 image by LDS-DMA: 1 KiB instruction i covers image bytes
-// [1024 i, 1024 i + 1024); each lane fetches the logical chunk that lands at its slot.
-template <int DH, int TR, int NW>
-struct TileDma32 {
-  static constexpr int NI = TR * DH * 2 / 1024;
-  static constexpr int PER = NI / NW;
-  static_assert(NI % NW == 0, "tile instructions must split evenly over the waves");
-  __device__ __forceinline__ void issue(char* tile, i32x4 rs, long ld, int r0, int nrows,
-                                        int wave, int lane) const {
-#pragma unroll
-    for (int j = 0; j < PER; ++j) {
-      const int o = (wave + j * NW) * 1024 + lane * 16;
-      const int rg = o / (16 * DH), rem = o - rg * 16 * DH;
-      const int rem2 = rem & 511, r7 = rem2 >> 6;
-      const int r = rg * 8 + r7;
-      const int c = (rem >> 9) * 4 + (((rem2 >> 4) & 3) ^ ((r >> 2) & 3));
-      const int vo = (r * (int)ld + c * 8) * 2;
-      blds16(rs, r0 + r < nrows ? vo : BUF_OOB, (int)((long)r0 * ld * 2),
-             tile + (wave + j * NW) * 1024);
-    }
-  }
-};
-
-__device__ __forceinline__ unsigned pack_bf16x2(float a, float b) {
-  return (unsigned)__builtin_bit_cast(unsigned short, (bf16)a) |
-         ((unsigned)__builtin_bit_cast(unsigned short, (bf16)b) << 16);
-}
-
-// key-valid flags for (b, h), the end of the last valid key and the length of the leading run
-// of valid keys (tiles inside it need no mask)
-__device__ __forceinline__ int build_kvalid2(uint8_t* kval, int* sh, const AttnP& p, int b, int h,
-                                             int& kfull) {
-  const int b2 = p.tiled ? (b * p.H + h) % p.B : b;
-  const uint8_t* k1 = p.kpad + (long)b * p.T;
-  const uint8_t* k2 = p.kpad + (long)b2 * p.T;
-  if (threadIdx.x == 0) { sh[0] = 0; sh[1] = p.T; }
-  __syncthreads();
-  int last = 0, first_bad = p.T;
-  const int tpad = (p.T + 63) & ~63;
-  for (int j = threadIdx.x; j < tpad; j += blockDim.x) {
-    const uint8_t v = j < p.T ? !(k1[j] | k2[j]) : 0;
-    kval[j] = v;
-    if (v) last = j + 1;
-    else if (j < p.T) first_bad = min(first_bad, j);
-  }
-  atomicMax(sh, last);
-  atomicMin(sh + 1, first_bad);
-  __syncthreads();
-  kfull = sh[1];
-  return sh[0];
-}
-
-template <int DH, int NW, int TR>
-__global__ void __launch_bounds__(NW * 64, 1) attn_fwd32_kernel(AttnP p) {
-  constexpr int NK = DH / 16, NB = DH / 32, KB = TR / 32;
-  constexpr int TB = TR * DH * 2;
-  // one LDS array: [3 ring buffers x (K, V)] [kval] [kend, kfull]
-  __shared__ __attribute__((aligned(16))) char smem[6 * TB + TMAX + 16];
-  uint8_t* kval = (uint8_t*)(smem + 6 * TB);
-  int* sh = (int*)(smem + 6 * TB + TMAX);
-  const int lane = threadIdx.x & 63, hh = lane >> 5;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int z = blockIdx.y, b = z / p.H, h = z - b * p.H;
-  const uint32_t dkey = fs2_drop_key(p.seed, p.salt);
-  const uint64_t T2 = (uint64_t)((p.T + 1) & ~1);
-  int kfull_v;
-  const int kend = __builtin_amdgcn_readfirstlane(build_kvalid2(kval, sh, p, b, h, kfull_v));
-  const int kfull = __builtin_amdgcn_readfirstlane(kfull_v);
-  const bf16* Qb = p.qkv + (long)b * p.T * p.ldq + h * DH;
-  const bf16* Kb = Qb + p.D;
-  const bf16* Vb = Qb + 2 * p.D;
-  const int qi = blockIdx.x * (32 * NW) + wave * 32 + (lane & 31);
-  const bool qin = qi < p.T;
-  bf16x8 qf[NK];
-#pragma unroll
-  for (int s = 0; s < NK; ++s)
-    qf[s] = qin ? ld_frag(Qb + (long)qi * p.ldq + 16 * s + 8 * hh) : bf16x8{};
-  f32x16 oacc[NB];
-#pragma unroll
-  for (int d = 0; d < NB; ++d) oacc[d] = f32x16{};
-  const float c = p.scale_log2;
-  float mrow = -INFINITY, lrow = 0.f;   // raw-score max (shared by both halves); half's sum
-  const bool drop = p.p_drop > 0.f;
-  // pair index of (q, key 0): ((z T + q) T2) / 2, below 2^32 (the launcher checks pair32)
-  const uint32_t pair0 = (uint32_t)(((uint64_t)z * p.T + qi) * T2 >> 1);
-
-  TileDma32<DH, TR, NW> dma;
-  const i32x4 rsK = make_rsrc(Kb), rsV = make_rsrc(Vb);
-  const int ntile = (kend + TR - 1) / TR;
-  auto issue = [&](int t) {
-    char* buf = smem + (t % 3) * 2 * TB;
-    dma.issue(buf, rsK, p.ldq, t * TR, p.T, wave, lane);
-    dma.issue(buf + TB, rsV, p.ldq, t * TR, p.T, wave, lane);
-  };
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // Q fragments resident before the ring
-  if (ntile > 0) issue(0);
-  if (ntile > 1) issue(1);
-  for (int t = 0; t < ntile; ++t) {
-    const int k0 = t * TR;
-    // tile t landed for this wave (tile t + 1's pieces may stay in flight) ...
-    if (t + 1 < ntile) wait_vmcnt<2 * TileDma32<DH, TR, NW>::PER>();
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    // ... and for every wave; every wave is also done with tile t - 1, whose buffer t + 2 reuses
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    if (t + 2 < ntile) issue(t + 2);
-    const char* Ks = smem + (t % 3) * 2 * TB;
-    const char* Vs = Ks + TB;
-    // each 32-key block as its own online-softmax step (one 16-register score block live)
-#pragma unroll
-    for (int kb = 0; kb < KB; ++kb) {
-      f32x16 sacc = f32x16{};
-#pragma unroll
-      for (int s = 0; s < NK; ++s) sacc = mfma32(row32<DH>(Ks, kb * 32, s, lane), qf[s], sacc);
-      // keys of register r: k0 + 32 kb + (r & 3) + 8 (r >> 2) + 4 hh
-      const int kbase = k0 + kb * 32;
-      if (kbase + 32 > kfull) {   // a block with masked keys (wave-uniform)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const uint32_t kw = *(const uint32_t*)(kval + kbase + 8 * i + 4 * hh);
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            sacc[4 * i + r] = (kw >> (8 * r)) & 1u ? sacc[4 * i + r] : -INFINITY;
-        }
-      }
-      float mt = sacc[0];
-#pragma unroll
-      for (int r = 1; r < 16; ++r) mt = fmaxf(mt, sacc[r]);
-      mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-      const float mnew = fmaxf(mrow, mt);
-      if (__any(mnew > mrow)) {    // rescale O and the sum only when some row's max moved
-        const float alpha = mnew > mrow ? fexp2((mrow - mnew) * c) : 1.f;   // exp2(-inf) = 0
-#pragma unroll
-        for (int d = 0; d < NB; ++d) oacc[d] *= alpha;
-        lrow *= alpha;
-        mrow = mnew;
-      }
-      const float nmc = mrow == -INFINITY ? 0.f : -mrow * c;   // all keys masked so far: p = 0
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        sacc[r] = fexp2(__builtin_fmaf(sacc[r], c, nmc));
-        lrow += sacc[r];
-      }
-      if (drop) {
-#pragma unroll
-        for (int r = 0; r < 16; r += 2) {
-          const int ko = kbase + (r & 3) + 8 * (r >> 2) + 4 * hh;   // even
-          const uint32_t hs = fs2_hash_pair32(dkey, pair0 + (ko >> 1));   // launch: pair32
-          // the 1 / (1 - p) of the kept probabilities is applied once, to O at the end
-          sacc[r] = (hs & 0xffffu) >= p.thr16 ? sacc[r] : 0.f;
-          sacc[r + 1] = (hs >> 16) >= p.thr16 ? sacc[r + 1] : 0.f;
-        }
-      }
-      // P^T as the B operand of O^T += V^T P^T: registers 8 s2 .. 8 s2 + 7 = k-step s2
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        bf16x8 pf;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) pf[j] = (bf16)sacc[8 * s2 + j];
-#pragma unroll
-        for (int d = 0; d < NB; ++d)
-          oacc[d] = mfma32(tr32<DH>(Vs, kb * 32 + 16 * s2, 32 * d, lane), pf, oacc[d]);
-      }
-    }
-  }
-  const float l = lrow + __shfl_xor(lrow, 32, 64);
-  if (qin && hh == 0) p.lse[(long)z * p.T + qi] = mrow * c + log2f(l);
-  const float inv = p.inv_keep / l;
-  bf16* orow = p.out + ((long)b * p.T + (qin ? qi : 0)) * p.ldout + h * DH;
-  // O^T block d, register 4 i + e = feature 32 d + 8 i + 4 hh + e: the two half-waves' 4-column
-  // groups i, i + 1 are paired by permlane32_swap into 16 contiguous bytes per lane
-#pragma unroll
-  for (int d = 0; d < NB; ++d)
-#pragma unroll
-    for (int i = 0; i < 4; i += 2) {
-      unsigned a0 = pack_bf16x2(oacc[d][4 * i] * inv, oacc[d][4 * i + 1] * inv);
-      unsigned a1 = pack_bf16x2(oacc[d][4 * i + 2] * inv, oacc[d][4 * i + 3] * inv);
-      unsigned b0 = pack_bf16x2(oacc[d][4 * i + 4] * inv, oacc[d][4 * i + 5] * inv);
-      unsigned b1 = pack_bf16x2(oacc[d][4 * i + 6] * inv, oacc[d][4 * i + 7] * inv);
-      const auto r0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
-      const auto r1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
-      const u32x4 o = {r0[0], r1[0], r0[1], r1[1]};
-      if (qin) *(u32x4*)(orow + 32 * d + 8 * i + 8 * hh) = o;
-    }
 }
 
 // ------------------------------------------------------------------------------ backward dQ
@@ -907,15 +665,6 @@ bool attn_small_blocks(const AttnP& p) {
 
 template <int DH>
 void launch_fwd(const AttnP& p, hipStream_t s) {
-  // 32x32x16 kernel, 8 waves x 32 queries per block, when those blocks fill the chip (the
-  // decoder: T = 977, B*H = 64 -> 256 blocks); the 16x16 kernels below otherwise
-  if constexpr (DH <= 192) {
-    if ((long)((p.T + 255) / 256) * p.B * p.H >= 256 && p.pair32) {
-      hipLaunchKernelGGL((attn_fwd32_kernel<DH, 8, 64>), dim3((p.T + 255) / 256, p.B * p.H),
-                         dim3(512), 0, s, p);
-      return;
-    }
-  }
   if (attn_small_blocks(p)) {
     dim3 grid((p.T + 63) / 64, p.B * p.H);
     if (attn_qg_fwd(DH) == 2) hipLaunchKernelGGL((attn_fwd_kernel<DH, 2, 4>), grid, dim3(128), 0, s, p);
@@ -974,7 +723,6 @@ extern "C" int fs2_attn_fwd(const void* qkv, int64_t ldq, const uint8_t* key_pad
   p.inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
   p.seed = seed; p.salt = salt;
   p.thr16 = (uint32_t)(p_drop * 65536.f + 0.5f);
-  p.pair32 = (uint64_t)B * H * T * (uint64_t)((T + 1) & ~1) / 2 < (1ull << 32);
   hipStream_t s = (hipStream_t)stream;
   switch (dh) {
     case 64: launch_fwd<64>(p, s); break;

@@ -117,13 +117,6 @@ __device__ __forceinline__ uint32_t fs2_hash_pair(uint32_t key, uint64_t pair) {
   h ^= h >> 15; h *= 0x2C1B3C6Du; h ^= h >> 12; h *= 0x297A2D39u; h ^= h >> 15;
   return h;
 }
-// the same hash for pair indices below 2^32 (the high word's term is 0): kernels whose
-// launches satisfy B*H*T*T2/2 < 2^32 use it to keep the index arithmetic in 32 bits
-__device__ __forceinline__ uint32_t fs2_hash_pair32(uint32_t key, uint32_t pair) {
-  uint32_t h = (pair * 0x9E3779B1u) ^ key;
-  h ^= h >> 15; h *= 0x2C1B3C6Du; h ^= h >> 12; h *= 0x297A2D39u; h ^= h >> 15;
-  return h;
-}
 __device__ __forceinline__ bool fs2_keep_pair_bit(uint32_t h, uint64_t idx, uint32_t thr16) {
   return ((h >> ((uint32_t)(idx & 1) * 16)) & 0xffffu) >= thr16;
 }

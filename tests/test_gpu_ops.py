@@ -609,15 +609,13 @@ def _keep_np(seed, salt, idx, p):
 @pytest.mark.parametrize("dh,T,p_drop,B", [(192, 150, 0.0, 3), (192, 150, 0.1, 3), (64, 70, 0.1, 3),
                                             (256, 130, 0.0, 3), (192, 977, 0.0, 32),
                                             (192, 977, 0.1, 32), (256, 977, 0.1, 32),
-                                            (192, 200, 0.0, 32), (128, 300, 0.1, 4),
-                                            (64, 300, 0.1, 64), (128, 257, 0.0, 128)])
+                                            (192, 200, 0.0, 32), (128, 300, 0.1, 4)])
 def test_fused_attention_vs_torch(cuda, dh, T, p_drop, B):
     """fs2_attn_fwd/bwd (bf16) against torch fp32 on the same bf16 Q/K/V: the head-major mask
     tiling rule, ragged lengths, and (p > 0) the counter-hash dropout masks restated in numpy.
-    B=32 with T=977 / 200 are the bench's decoder / encoder shapes: the 32x32x16 forward
-    (attn_fwd32_kernel, 256-query blocks: chosen when they fill the 256 CUs, also dh 64 / 128 at
-    B=64 / 128) and the 128-row backward blocks for the decoder, 64-row blocks for the encoder,
-    descending ragged lengths as the collate sorts; dh=256 (BASELINE config 4) at T=977.
+    B=32 with T=977 / 200 are the bench's decoder / encoder shapes: 128-row (W8 = 8) blocks for
+    the decoder, 64-row blocks for the encoder, descending ragged lengths as the collate sorts,
+    with and without dropout; dh=256 (BASELINE config 4) at T=977.
     Tolerance rel 2e-2 (O) / 3e-2 (dQ, dK, dV): bf16 operands and probabilities."""
     from fastspeech2 import ops
     torch.manual_seed(dh + T)
