@@ -31,12 +31,15 @@ def rel(a, b):
 
 OUT_NAMES = ("mel_post", "postnet_output", "log_durations", "pitch", "avg_pitch", "energy",
              "avg_energy", "mel_lens")
-# bf16 bounds per output index (0..6), mel L1, loss rel, worst gradient cosine: 2x observed
+# bf16 bounds: 2x the largest value observed over configs 2, 3 and 4 on MI355X
+# (profiles/r03_parity_observed.json): per output index 0..6 (avg_pitch / avg_energy are
+# computed from the fp32 targets: exact), mel L1, loss rel, worst per-tensor gradient cosine
+# (1 - 2 x (1 - 0.99972))
 BF16_TOL = {
-    "out": [5e-2] * 7,
-    "mel_l1": 2e-2,
-    "loss": 2e-2,
-    "grad_cos": 0.99,
+    "out": [2.2e-2, 3.0e-2, 2.6e-2, 2.4e-2, 1e-6, 2.8e-2, 1e-6],
+    "mel_l1": 1.9e-2,
+    "loss": 5e-3,
+    "grad_cos": 0.9994,
 }
 
 
