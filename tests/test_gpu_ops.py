@@ -450,6 +450,42 @@ def test_gemm_big_tile_paths_bf16(cuda, Bn, T):
     assert rel(dW - 0.5, Wr.grad.permute(0, 2, 1)) < 2e-2
 
 
+@pytest.mark.parametrize("Bn,T,O,Cin,KW,ns", [(32, 977, 1536, 384, 9, 3), (32, 200, 1536, 384, 9, 2),
+                                              (4, 77, 600, 72, 9, 1), (32, 977, 512, 512, 5, 2),
+                                              (3, 130, 520, 128, 5, 3)])
+def test_wgrad_conv3_slices(cuda, Bn, T, O, Cin, KW, ns):
+    """Implicit-reflect-conv weight gradients written as split-K fp32 planes (split_stride, the
+    engine's path for the large FFN / PostNet weights) -- the 4-wave 128x128-per-wave kernel
+    (gemm_w4_kernel) at the decoder / encoder FFN conv1 shapes, a PostNet-like k=5 shape, and
+    ragged ones (M, N not multiples of 256, utterance boundaries inside K-tiles, a slice count
+    that leaves no plane empty and one plane (ns = 1)).  The summed planes equal the fp32
+    reference of the same bf16 values (rel 2e-2); planes cover every output element exactly."""
+    from fastspeech2 import ops
+    torch.manual_seed(T + O)
+    P = (KW - 1) // 2
+    M = Bn * T
+    X = torch.randn(Bn, T, Cin, device=cuda).to(torch.bfloat16)
+    G = torch.randn(M, O, device=cuda).to(torch.bfloat16)
+    cols = []
+    idx = torch.arange(T, device=cuda)
+    for j in range(KW):
+        src = idx + j - P
+        src = torch.where(src < 0, -src, src)
+        src = torch.where(src >= T, 2 * (T - 1) - src, src)
+        cols.append(X[:, src, :].float())
+    Xcol = torch.cat(cols, dim=2).reshape(M, KW * Cin)
+    ref = G.float().t() @ Xcol                              # [O][KW*C]
+    K = ops.round_up(M, 8)
+    stride = O * KW * Cin
+    ws = torch.full((ns, O, KW * Cin), float("nan"), device=cuda)
+    ops.gemm(O, KW * Cin, K, G, O, X, Cin, ws, KW * Cin, dt=1, a_kmajor=0, b_kmajor=0,
+             conv=(3, T, KW, Cin), c_fp32=1, kvalid=M, nvalid=KW * Cin, split_k=ns,
+             split_stride=stride if ns > 1 else 0)
+    torch.cuda.synchronize()
+    assert torch.isfinite(ws).all()
+    assert rel(ws.sum(0), ref) < 2e-2
+
+
 @pytest.mark.parametrize("dt,code", [(torch.float32, 0), (torch.bfloat16, 1)])
 def test_add3_mask_rows(cuda, dt, code):
     """fs2_add3_mask_rows: X = (X + Y + Z) * keep[row] in fp32 with one rounding, row pitch > D."""
