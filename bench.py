@@ -204,12 +204,12 @@ def secondary_legs(cfg_all, args, rank, world):
     return out
 
 
-def pmc_traffic():
-    """HBM bytes per launch of the roofline kernel from the newest committed PMC summary
-    (profiles/r*_roofline_traffic.json, written by tools/rocprof_summary.py traffic from two
+def pmc_traffic(kind="roofline"):
+    """HBM bytes per launch of a roofline kernel from the newest committed PMC summary
+    (profiles/r*_<kind>_traffic.json, written by tools/rocprof_summary.py traffic from two
     separate rocprofv3 --pmc passes of this same bench command)."""
     import glob
-    hits = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_roofline_traffic.json")))
+    hits = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{kind}_traffic.json")))
     if not hits:
         return None, None
     d = json.load(open(hits[-1]))
@@ -409,6 +409,12 @@ def main():
         kflop = 2.0 * (args.batch * Tm) * F * (KW * D)
         achieved = kflop / (ms * 1e-3) / 1e12 if n else None
         traffic, traffic_src = pmc_traffic() if not args.scaled else (None, None)
+        # second entry: the decoder FFN conv1 weight gradient, the largest GEMM bucket of the
+        # step (2 M F 9D per launch like the forward); it runs on the side stream beside the
+        # main stream's conv1 data gradient, so its duration is the shared-GPU one
+        wn, wms = ks.get("ffn_conv1_wgrad.decoder", (0, float("nan")))
+        wach = kflop / (wms * 1e-3) / 1e12 if wn else None
+        wtraffic, wtraffic_src = (pmc_traffic("wgrad") if not args.scaled else (None, None))
         step_ms = elapsed / args.steps * 1e3
         step_tflops = train_flops(c, args.batch, Tp, Tm) * world / (step_ms * 1e-3) / 1e12
         fpf = train_flops(c, 1, 200, 1000) / 1000.0
@@ -438,6 +444,15 @@ def main():
                                     "eager pass of the same steps after the graph-replayed "
                                     "timed region" if graphed else
                                     "HIP events on the engine stream over the timed region")},
+            "roofline_conv1_wgrad": {
+                "bound": "mfma", "kernel": "decoder FFN conv1 (k=9) weight gradient, implicit "
+                                           "reflect-conv B operand, 3 split-K fp32 planes",
+                "achieved": wach, "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": (wach / MFMA_BF16_PEAK_TFLOPS) if wach else None,
+                "traffic": wtraffic, "traffic_source": wtraffic_src,
+                "launches": wn, "avg_ms": wms, "flop_per_launch": kflop,
+                "timing": "HIP events on the weight-gradient side stream around the GEMM launch, "
+                          "concurrent with the main stream's conv1 data gradient"},
             "hip_graph": graphed,
             # the step-level roofline on VALID frames -- frames/s x the train FLOPs
             # of one mel frame at T_phon=200, T_mel=1000 (338.8 MFLOP at default dims) / peak

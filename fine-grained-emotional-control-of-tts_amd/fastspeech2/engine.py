@@ -338,18 +338,20 @@ class FS2Engine:
                       row_scale_post=epi.get("row_scale_post"), nsplit=split,
                       split_stride=Mp * C)
 
-    def _wgrad(self, dY, lddy, X, ldx, M, T, wname, n_cols=None):
+    def _wgrad(self, dY, lddy, X, ldx, M, T, wname, n_cols=None, gemm_tag=None):
         h = self._side_enter(dY, X)
         tag = self._dtag("wgrad", wname, T)
         if tag:
             self._tic(tag)
-        self._wgrad_impl(dY, lddy, X, ldx, M, T, wname, n_cols)
+        self._wgrad_impl(dY, lddy, X, ldx, M, T, wname, n_cols, gemm_tag)
         if tag:
             self._toc(tag)
         self._side_exit(h)
 
-    def _wgrad_impl(self, dY, lddy, X, ldx, M, T, wname, n_cols=None):
-        """grad[O][KW][C] += sum_m dY[m][o] * X[reflect(t+j-P)][c]   (fp32, accumulate)."""
+    def _wgrad_impl(self, dY, lddy, X, ldx, M, T, wname, n_cols=None, gemm_tag=None):
+        """grad[O][KW][C] += sum_m dY[m][o] * X[reflect(t+j-P)][c]   (fp32, accumulate).
+        ``gemm_tag``: HIP events around the GEMM launch alone (bench.py's roofline entry for
+        the FFN conv1 weight gradient), on the stream it runs on (the side stream)."""
         O, C, KW = self._wspecs[wname]
         Ncols = n_cols or KW * C
         K = round_up(M, self.epc)
@@ -368,8 +370,12 @@ class FS2Engine:
             # of tens of fp32 atomics landing on every output element
             stride = O * ldc
             ws = self.ws(ns * stride)
+            if gemm_tag:
+                self._tic(gemm_tag)
             ops.gemm(O, Ncols, K, dY, lddy, X, ldx, ws, ldc, dt=self.dt, a_kmajor=0, b_kmajor=0,
                      conv=conv, c_fp32=1, kvalid=M, nvalid=ldc, split_k=ns, split_stride=stride)
+            if gemm_tag:
+                self._toc(gemm_tag)
             ops.sum_slices(ws, ns, stride, stride, self.grads[wname], accumulate=1)
             return
         # conv weight gradients land contiguous in the [O][KW][C] flat layout (model._kw_major)
@@ -476,7 +482,8 @@ class FS2Engine:
         # holding every CU while main's out-projection waits behind it
         self._wgrad(dY, D, ctx["Hc"], F, M, T, w2)
         self._dgrad(dY, D, M, T, w2, dHc, F, gate=ctx["Hc"], ldg=F)
-        self._wgrad(dHc, F, ctx["X1"], D, M, T, w1)
+        self._wgrad(dHc, F, ctx["X1"], D, M, T, w1,
+                    gemm_tag="ffn_conv1_wgrad." + prefix.split(".")[0])
         self._bias_grad(dHc, F, M, F, prefix + "pos_ffn.0.conv.bias")
         self._dgrad(dHc, F, M, T, w1, dX1, D, residual=ds2, ldr=D)
         del dY, dHc, ds2

@@ -455,8 +455,9 @@ def test_gemm_big_tile_paths_bf16(cuda, Bn, T):
                                               (3, 130, 520, 128, 5, 3)])
 def test_wgrad_conv3_slices(cuda, Bn, T, O, Cin, KW, ns):
     """Implicit-reflect-conv weight gradients written as split-K fp32 planes (split_stride, the
-    engine's path for the large FFN / PostNet weights) -- the 4-wave 128x128-per-wave kernel
-    (gemm_w4_kernel) at the decoder / encoder FFN conv1 shapes, a PostNet-like k=5 shape, and
+    engine's path for the large FFN / PostNet weights) -- the 256x256 MN-major kernel
+    (gemm256_kernel<false, false, 0, 1>) at the decoder / encoder FFN conv1 shapes, a
+    PostNet-like k=5 shape, and
     ragged ones (M, N not multiples of 256, utterance boundaries inside K-tiles, a slice count
     that leaves no plane empty and one plane (ns = 1)).  The summed planes equal the fp32
     reference of the same bf16 values (rel 2e-2); planes cover every output element exactly."""
@@ -502,11 +503,15 @@ def test_add3_mask_rows(cuda, dt, code):
 
 
 @pytest.mark.parametrize("M,N,K,c32", [(1000, 1536, 2048, 0), (31264, 1536, 3456, 0),
-                                        (700, 384, 4096, 1), (300, 200, 2056, 1)])
+                                        (700, 384, 4096, 1), (300, 200, 2056, 1),
+                                        (6400, 1536, 3456, 0), (2000, 384, 8192, 1),
+                                        (5000, 700, 3000, 1)])
 def test_gemm_persistent_long_k(cuda, M, N, K, c32):
     """Long-K K-major GEMMs take the persistent 256 x 256 / 256 x 192 kernel (gemm_ps_kernel):
     both tile widths, partial row / column tiles, a partial last K-tile (K = 2056), bf16 and
-    fp32 outputs, the bias + ReLU + row-scale epilogue; fp32 reference on the same bf16 values."""
+    fp32 outputs, the bias + ReLU + row-scale epilogue; fp32 reference on the same bf16 values.
+    The last three: the encoder FFN conv1 shape as a plain GEMM (one round of 200 tiles), 16
+    tiles at K = 8192, and a ragged one (partial rows, columns and last K-tile)."""
     from fastspeech2 import ops
     torch.manual_seed(M + N)
     A = torch.randn(M, K, device=cuda).to(torch.bfloat16)
