@@ -1678,7 +1678,9 @@ __global__ void __launch_bounds__(BNT) gemm_pk_kernel(GemmP p) {
 // Persistent 256 x BN kernel (BN = 4 * WN = 256 or 192) for the long-K GEMMs with K-major A and
 // B: the FFN conv1 forward (implicit reflect conv, K = 9 x 384) and its data gradient over the
 // padded domain (K = 9 x 1536, N = 384: 256 x 192 tiles put the decoder's 248 tiles in ONE round
-// of the 256 CUs without a K split).
+// of the 256 CUs without a K split) -- and the decoder's short-K projections whose tiles fill
+// a round (N = 384 / 1152, K = 384 / 1536 at M = 31264), where the continuous K-tile stream
+// across tiles and the LDS-staged epilogue operands beat the per-tile kernels.
 //
 // Why not gemm256_kernel: a K-sweep at M = 31264, N = 1536 (tools/gemm256_ksweep.py) split its
 // time into ~25 us per round of tiles (prologue DMA round trip, LDS-staged epilogue and store
@@ -1708,7 +1710,10 @@ __global__ void __launch_bounds__(BNT) gemm_pk_kernel(GemmP p) {
 // ============================================================================================
 __device__ __forceinline__ int ps_sw(int row) { return (row >> 1) & 7; }
 
-template <int CM, int WN>   // CM: 0 plain, 1 reflect "same" conv, 4 padded-domain conv (dgrad)
+// CM: 0 plain, 1 reflect "same" conv, 4 padded-domain conv (dgrad).  EO: 1 = a bf16 [M][N]
+// epilogue operand (the ReLU gate OR the residual; plain A, 256 x 192 tiles), loaded into
+// registers in the tile's last K-tile ahead of that iteration's DMA.
+template <int CM, int WN, int EO = 0>
 __global__ void __launch_bounds__(BNT, 1) gemm_ps_kernel(GemmP p) {
   constexpr int BN = 4 * WN, NJ = WN / 16;
   constexpr int AIMG = 256 * 128;
@@ -1716,11 +1721,15 @@ __global__ void __launch_bounds__(BNT, 1) gemm_ps_kernel(GemmP p) {
   constexpr int NB1 = (BN - 128) / 64;     // B1 pieces per wave
   constexpr int S32 = 8 * NJ;              // epilogue stores per wave per tile: fp32 output
   constexpr int S16 = 8 * ((NJ + 1) / 2);  // bf16 output (fragment pairs, one 16-B store each)
-  static_assert(2 * SLOT <= 160 * 1024, "LDS");
-  __shared__ __attribute__((aligned(16))) char smem[2 * SLOT];
+  // per-wave epilogue operands of the current tile, LDS-DMA'd at its first K-tile: bias of the
+  // wave's WN columns (256 B), row_scale and row_scale_post of its 128 rows (512 B each)
+  constexpr int EPW = 1280;
+  static_assert(2 * SLOT + 8 * EPW <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) char smem[2 * SLOT + 8 * EPW];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
+  char* const epl = smem + 2 * SLOT + wave * EPW;
   const int li = lane & 15, lg = lane >> 4;
   const int ntile = p.tiles_m * p.tiles_n;
   const int G = gridDim.x;
@@ -1732,6 +1741,11 @@ __global__ void __launch_bounds__(BNT, 1) gemm_ps_kernel(GemmP p) {
   const int total = mine * nk;
   if (total == 0) return;
   const i32x4 rsA = make_rsrc(p.A), rsB = make_rsrc(p.B), rsC = make_rsrc(p.C);
+  static_assert(EO == 0 || (CM == 0 && WN == 48), "epilogue operands: plain 256 x 192 only");
+  constexpr int EL = EO ? 8 * (WN / 16) : 0;   // operand loads per wave in a tile's last K-tile
+  const i32x4 rsE = make_rsrc(EO ? (p.gate ? (const void*)p.gate : (const void*)p.residual)
+                                 : (const void*)p.C);
+  const long lde = p.gate ? p.ldg : p.ldr;
   const int K = p.K;
   const int rpu = CM == 4 ? p.conv_t + 2 * p.conv_p : p.conv_t;
   const int cpt = CM ? p.conv_c / 64 : 1;   // K-tiles per tap
@@ -1843,7 +1857,34 @@ __global__ void __launch_bounds__(BNT, 1) gemm_ps_kernel(GemmP p) {
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // prologue: B0, B1, A0, A1 of iteration 0, then B0, B1 of iteration 1 (total >= nk >= 2)
+  // epilogue operands of tile ordinal tt: 5 LDS-DMA instructions per wave, always (absent
+  // operands at BUF_OOB read zeros), issued at the tile's first K-tile before A0 of the next
+  // iteration, so the ring's counted waits retire them long before the epilogue reads them --
+  // no vmcnt(0) drain of the ring per tile (global loads there cost ~5-10 us per tile)
+  auto issue_epi = [&](int tt) {
+    const int tile = c0 + local + tt * nbx;
+    const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
+    const int n = tn * BN + wc * WN + 4 * lane;
+    const bool bok = p.bias && lane < WN / 4 && n < p.nvalid;
+    blds16(make_rsrc(p.bias ? (const void*)p.bias : (const void*)p.C), bok ? n * 4 : BUF_OOB, 0,
+           epl);
+    const i32x4 r1 = make_rsrc(p.row_scale ? (const void*)p.row_scale : (const void*)p.C);
+    const i32x4 r2 = make_rsrc(p.row_scale_post ? (const void*)p.row_scale_post : (const void*)p.C);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int m = tm * 256 + wr * 128 + 64 * h + lane;
+      const bool in = m < p.mvalid;
+      llvm_raw_buffer_load_lds(r1, (__attribute__((address_space(3))) uint32_t*)(epl + 256 + 256 * h),
+                               4, (p.row_scale && in) ? m * 4 : BUF_OOB, 0, 0, 0);
+      llvm_raw_buffer_load_lds(r2, (__attribute__((address_space(3))) uint32_t*)(epl + 768 + 256 * h),
+                               4, (p.row_scale_post && in) ? m * 4 : BUF_OOB, 0, 0, 0);
+    }
+  };
+  constexpr int EPI_OPS = 5;
+
+  // prologue: tile 0's epilogue operands, B0, B1, A0, A1 of iteration 0, then B0, B1 of
+  // iteration 1 (total >= nk >= 2)
+  issue_epi(0);
   b_advance();
   issue_b(0, smem); issue_b(1, smem);
   a_advance();
@@ -1857,6 +1898,7 @@ __global__ void __launch_bounds__(BNT, 1) gemm_ps_kernel(GemmP p) {
 
   int t = 0, kt = 0;          // tile ordinal / k-tile of iteration g
   bf16x8 af[4], bfr[2][NJ];
+  i32x2 ev[EO ? 8 : 1][EO ? NJ : 1];   // EO: the tile's gate / residual values (4 bf16 each)
   for (int g = 0; g < total; ++g) {
     const bool more1 = g + 1 < total, more2 = g + 2 < total;
     const bool first = kt == 0 && g > 0;        // previous iteration ended a tile (stores)
@@ -1882,20 +1924,41 @@ __global__ void __launch_bounds__(BNT, 1) gemm_ps_kernel(GemmP p) {
         const int r = wr * 128 + mq * 64 + i * 16 + li;
         af[i] = *(const bf16x8*)(cur + r * 128 + (((kh * 4 + lg) ^ ps_sw(r)) << 4));
       }
+      if (ph == 0 && first) issue_epi(t);
+      if constexpr (EO && ph == 0) {
+        if (last) {   // older than this iteration's DMA: the epilogue waits for them, not it
+          const int tile = c0 + local + t * nbx;
+          const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
+          const int mb = tm * 256 + wr * 128, nb = tn * BN + wc * WN;
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+              const int m = mb + 16 * i + li, n = nb + 16 * j + 4 * lg;
+              ev[i][j] = llvm_raw_buffer_load_v2i32(
+                  rsE, (m < p.mvalid && n < p.nvalid) ? (int)(((long)m * lde + n) * 2) : BUF_OOB, 0, 0);
+            }
+        }
+      }
       if (ph == 0 && more1) { a_advance(); issue_a(0, nxt); }
       if (ph == 1 && more1) issue_a(1, nxt);
       if (ph == 2 && more2) { b_advance(); issue_b(0, cur); }
       if (ph == 3 && more2) issue_b(1, cur);
       auto dwait = [&]() {
         if constexpr (ph == 1) {
+          // younger than A1 of this iteration: B of the next one, the previous tile's
+          // epilogue stores and this tile's operands (first K-tile), A0 / A1 of the next one
+          // (EO: + the operand loads of a tile's last K-tile; nk >= 2, so never also first)
           if (more1) {
-            if (!first) vm_wait<6 + NB1>();
-            else if (p.c_fp32) vm_wait<6 + NB1 + S32>();
-            else vm_wait<6 + NB1 + S16>();
+            if (EO && last) vm_wait<6 + NB1 + EL>();
+            else if (!first) vm_wait<6 + NB1>();
+            else if (p.c_fp32) vm_wait<6 + NB1 + S32 + EPI_OPS>();
+            else vm_wait<6 + NB1 + S16 + EPI_OPS>();
           } else {
-            if (!first) vm_wait<0>();
-            else if (p.c_fp32) vm_wait<S32>();
-            else vm_wait<S16>();
+            if (EO && last) vm_wait<EL>();
+            else if (!first) vm_wait<0>();
+            else if (p.c_fp32) vm_wait<S32 + EPI_OPS>();
+            else vm_wait<S16 + EPI_OPS>();
           }
         } else {
           if (more2) vm_wait<4 + NB1>();
@@ -1918,23 +1981,23 @@ __global__ void __launch_bounds__(BNT, 1) gemm_ps_kernel(GemmP p) {
       __builtin_amdgcn_s_setprio(0);
       if constexpr ((ph & 1) != 0) { if (wr == 0) dwait(); }
       if (ph == 3 && last && !(XFLAGS(p) & 32)) {   // flag 32: timing only, no epilogue
-        // ---- tile epilogue, straight from the accumulators ----
-        if (!(XFLAGS(p) & 64)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // ---- tile epilogue, straight from the accumulators; operands from the wave's LDS
+        // area (landed: retired by the counted waits since the tile's first K-tile) ----
         const int tile = c0 + local + t * nbx;
         const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
         const int mb = tm * 256 + wr * 128, nb = tn * BN + wc * WN;
         f32x4 bv[NJ];
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-          const int n = nb + 16 * j + 4 * lg;
-          bv[j] = (p.bias && n < p.nvalid) ? *(const f32x4*)(p.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
-        }
-        float rs[8];
+        for (int j = 0; j < NJ; ++j) bv[j] = *(const f32x4*)(epl + (16 * j + 4 * lg) * 4);
+        float rs[8], rsp[8];   // EO: row_scale and row_scale_post apart (the operand between)
+        const float* rs1l = (const float*)(epl + 256);
+        const float* rs2l = (const float*)(epl + 768);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-          const int m = mb + 16 * i + li;
-          rs[i] = ((p.row_scale && m < p.mvalid) ? p.row_scale[m] : 1.f) *
-                  ((p.row_scale_post && m < p.mvalid) ? p.row_scale_post[m] : 1.f);
+          const int r = 16 * i + li;
+          rs[i] = p.row_scale ? rs1l[r] : 1.f;
+          rsp[i] = p.row_scale_post ? rs2l[r] : 1.f;
+          if constexpr (!EO) rs[i] *= rsp[i];
         }
         // compact, branch-free body (ReLU as a select): the epilogue runs once
         // per tile, so its code is fetched cold every time -- keep it small
@@ -1945,6 +2008,15 @@ __global__ void __launch_bounds__(BNT, 1) gemm_ps_kernel(GemmP p) {
           f32x4 v = acc[i][j] + bv[j];
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = (relu ? fmaxf(v[e], 0.f) : v[e]) * rs[i];
+          if constexpr (EO) {   // as gemm_pk_kernel: gate select / residual add, then rs2
+            const bool gate = p.gate;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const unsigned w = (unsigned)ev[i][j][e >> 1];
+              const float ef = __builtin_bit_cast(float, (e & 1) ? (w & 0xffff0000u) : (w << 16));
+              v[e] = (gate ? (ef > 0.f ? v[e] : 0.f) : v[e] + ef) * rsp[i];
+            }
+          }
           acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
           return v;
         };
@@ -2062,25 +2134,41 @@ int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
     static const bool no_ps = getenv_flag("FS2_GEMM_NO_PS");
     // FS2_PS_MODES: bit 0 plain, bit 1 reflect conv (fwd), bit 2 padded-domain conv (dgrad).
     // Default 5: in the bench step the unsplit decoder conv1 data gradient gains 0.15-0.2 ms,
-    // while the conv1 forward measured 0-0.1 ms slower than gemm256_kernel (A/B runs)
+    // while the conv1 forward measured 0-0.1 ms slower than gemm256_kernel (A/B runs).
+    // Short K (256 <= K < 2048) when the tiles fill at least 200 of the 256 CUs: the decoder's
+    // N = 384 / 1152 projections and FFN conv2 forward (M = 31264; tools/pk_bench.py: conv2 fwd
+    // 63.8 -> 49.1 us, out_proj 29.1 -> 22.0, in_proj 65.6 -> 52.6); the encoder's 25-row-tile
+    // shapes stay on the per-tile kernels (ps 30 -> 43 us).  FS2_PS_MIN_K / FS2_PS_SHORT_TILES
+    // override for A/B runs.
     static const int ps_modes = getenv_int("FS2_PS_MODES", 5);
+    static const int ps_min_k = getenv_int("FS2_PS_MIN_K", 256);
+    static const int ps_short_tiles = getenv_int("FS2_PS_SHORT_TILES", 200);
     const int cm_ps = p.conv_mode == 0 ? 0
                       : ((p.conv_mode == 1 || p.conv_mode == 4) && p.conv_dil == 1 && p.conv_c % 64 == 0
                              ? p.conv_mode : -1);
     const bool ps_on = cm_ps >= 0 && (ps_modes >> (cm_ps == 0 ? 0 : (cm_ps == 1 ? 1 : 2))) & 1;
+    // tile width by rounds x width over the 256 CUs (ties to the wider tile)
+    const int ps_tm = (p.M + 255) / 256;
+    const int ps_t256 = ps_tm * ((p.N + 255) / 256), ps_t192 = ps_tm * ((p.N + 191) / 192);
+    // a gate / residual operand (plain A only) takes the 256 x 192 instance (its register budget)
+    const bool ps_op = p.gate || p.residual;
+    const bool ps_w192 = ps_op ||
+                         (long)((ps_t192 + 255) / 256) * 192 < (long)((ps_t256 + 255) / 256) * 256;
+    const int ps_nt = ps_w192 ? ps_t192 : ps_t256;
+    const bool ps_k = p.K >= 2048 || (p.K >= max(ps_min_k, 128) && ps_nt >= ps_short_tiles);
     if (!no_ps && ak && bk && ps_on && batch == 1 && p.split_k <= 1 && p.vec_ok &&
-        !p.accumulate && !p.gate && !p.residual && p.relu <= 1 && p.K >= 2048 && p.N >= 128 && pk_fits) {
+        !p.accumulate && !(p.gate && p.residual) && (!ps_op || cm_ps == 0) && p.relu <= 1 && ps_k &&
+        p.N >= 128 && pk_fits) {
       GemmP q = p;
       q.g4_flags = getenv_int("FS2_PS_FLAGS", 0);
-      q.tiles_m = (p.M + 255) / 256;
-      // tile width by rounds x width over the 256 CUs (ties to the wider tile)
-      const int t256 = q.tiles_m * ((p.N + 255) / 256), t192 = q.tiles_m * ((p.N + 191) / 192);
-      const bool w192 = (long)((t192 + 255) / 256) * 192 < (long)((t256 + 255) / 256) * 256;
+      q.tiles_m = ps_tm;
+      const bool w192 = ps_w192;
       q.tiles_n = w192 ? (p.N + 191) / 192 : (p.N + 255) / 256;
       const int nt = q.tiles_m * q.tiles_n;
       const int g = nt < 256 ? (nt + 7) / 8 * 8 : 256;
       if (w192) {
-        if (cm_ps == 0) hipLaunchKernelGGL((gemm_ps_kernel<0, 48>), dim3(g), dim3(BNT), 0, s, q);
+        if (ps_op) hipLaunchKernelGGL((gemm_ps_kernel<0, 48, 1>), dim3(g), dim3(BNT), 0, s, q);
+        else if (cm_ps == 0) hipLaunchKernelGGL((gemm_ps_kernel<0, 48>), dim3(g), dim3(BNT), 0, s, q);
         else if (cm_ps == 1) hipLaunchKernelGGL((gemm_ps_kernel<1, 48>), dim3(g), dim3(BNT), 0, s, q);
         else hipLaunchKernelGGL((gemm_ps_kernel<4, 48>), dim3(g), dim3(BNT), 0, s, q);
       } else {

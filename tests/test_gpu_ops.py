@@ -532,6 +532,42 @@ def test_gemm_persistent_long_k(cuda, M, N, K, c32):
     assert (C2[:, N:] == 0).all()
 
 
+@pytest.mark.parametrize("M,N,K,op", [(31264, 384, 1152, "residual"), (31264, 1536, 384, "gate"),
+                                       (26000, 400, 384, "residual"), (26000, 400, 1000, "gate"),
+                                       (31264, 384, 1536, None), (26000, 1152, 384, None)])
+def test_gemm_persistent_short_k(cuda, M, N, K, op):
+    """Short-K GEMMs whose 256-row tiles fill a round of the CUs take the persistent kernel
+    (gemm_ps_kernel): the decoder's QKV data gradient (+ residual), FFN conv2 data gradient
+    (ReLU gate), conv2 forward and QKV projection shapes, and ragged ones (partial row / column
+    tiles, K not a multiple of 64).  The gate / residual instance loads its operand in the
+    tile's last K-tile; bias + row scales come from the LDS-staged epilogue operands.  fp32
+    reference on the same bf16 values, rel 1e-2."""
+    from fastspeech2 import ops
+    torch.manual_seed(M + N + K)
+    A = torch.randn(M, K, device=cuda).to(torch.bfloat16)
+    W = (torch.randn(N, K, device=cuda) * 0.05).to(torch.bfloat16)
+    bias = torch.randn(N, device=cuda)
+    rs = (torch.rand(M, device=cuda) > 0.2).float()
+    rs2 = torch.rand(M, device=cuda) + 0.5
+    E = torch.randn(M, N + 8, device=cuda).to(torch.bfloat16)     # operand with a row pitch > N
+    x = A.float() @ W.float().t() + bias
+    kw = {}
+    if op == "gate":
+        x = torch.where(E[:, :N].float() > 0, x, torch.zeros_like(x)) * rs[:, None]
+        kw = dict(gate=E, ldg=N + 8)
+    elif op == "residual":
+        x = x * rs[:, None] + E[:, :N].float()
+        kw = dict(residual=E, ldr=N + 8)
+    else:
+        x = x * rs[:, None]
+    ref = x * rs2[:, None]
+    C = torch.full((M, N), float("nan"), device=cuda, dtype=torch.bfloat16)
+    ops.gemm(M, N, K, A, K, W, K, C, N, dt=1, bias=bias, row_scale=rs, row_scale_post=rs2, **kw)
+    torch.cuda.synchronize()
+    assert torch.isfinite(C.float()).all()
+    assert rel(C, ref) < 1e-2
+
+
 @pytest.mark.parametrize("M,N,K,conv", [(31264, 1152, 384, None), (6400, 384, 1536, None),
                                          (31264, 1536, 3456, (1, 977, 9, 384)),
                                          (31264, 384, 13824, (4, 977, 9, 1536)), (200, 80, 384, None)])
