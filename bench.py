@@ -360,7 +360,8 @@ def main():
     torch.cuda.synchronize()
     timer = KernelTimer()
     timer.detail = args.detail
-    trainer.eng.timer = timer
+    # FS2_BENCH_NO_TIMER=1 (A/B runs): no HIP-event brackets in the timed region
+    trainer.eng.timer = None if os.environ.get("FS2_BENCH_NO_TIMER") else timer
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
