@@ -190,6 +190,62 @@ __global__ void __launch_bounds__(256) adamw_prep_tiles_kernel(const fs2_wprep_d
   }
   __syncthreads();
   T* Wf = (T*)d.Wf;
+  T* Wb = (T*)d.Wb;
+  // 16-byte form: 4 consecutive k per lane for the fp32 streams (p, g, m, v: 80 % of the
+  // bytes) and 4 consecutive o per lane for the transposed image -- when the weight's flat
+  // offset and row pitches keep every quad aligned (all the model's weights); the scalar form
+  // below otherwise.  Same adamw_elem per element either way.
+  const bool vec = sizeof(T) == 2 && (base & 3) == 0 && (KC & 3) == 0 && (d.ldf & 3) == 0 &&
+                   (!d.Wb || ((d.ldb & 3) == 0 && (d.O & 3) == 0));
+  if (vec) {
+    // all 4 quads' loads in flight before the first update (blockDim.x == 256)
+#pragma unroll
+    for (int i = threadIdx.x; i < 64 * 16; i += 256) {
+      const int ol = i >> 4, kl = (i & 15) * 4, o = o0 + ol, k = k0 + kl;
+      if (o >= d.O || k >= d.ldf) continue;
+      f32x4 w = {0.f, 0.f, 0.f, 0.f};
+      if (k < KC) {   // KC % 4 == 0: the quad is all in or all out
+        const long e = base + (long)o * KC + k;
+        f32x4 pi = *(const f32x4*)(pb + e), mi = *(const f32x4*)(mb + e);
+        f32x4 vi = *(const f32x4*)(vb + e);
+        const f32x4 gi = *(const f32x4*)(gb + e);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float pq = pi[q], mq = mi[q], vq = vi[q];
+          adamw_elem(pq, mq, vq, gi[q], a.decay_mul, a.w1, a.beta2, a.omb2, a.step_size,
+                     a.bc2_sqrt, a.eps, a.gscale);
+          pi[q] = pq; mi[q] = mq; vi[q] = vq;
+        }
+        *(f32x4*)(pb + e) = pi;
+        *(f32x4*)(mb + e) = mi;
+        *(f32x4*)(vb + e) = vi;
+        w = pi;
+      }
+      uint2 h;
+      h.x = (unsigned)__builtin_bit_cast(unsigned short, (bf16)w[0]) |
+            ((unsigned)__builtin_bit_cast(unsigned short, (bf16)w[1]) << 16);
+      h.y = (unsigned)__builtin_bit_cast(unsigned short, (bf16)w[2]) |
+            ((unsigned)__builtin_bit_cast(unsigned short, (bf16)w[3]) << 16);
+      *(uint2*)(Wf + (long)o * d.ldf + k) = h;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) tile[ol][kl + q] = w[q];
+    }
+    if (!d.Wb) return;
+    __syncthreads();
+#pragma unroll
+    for (int i = threadIdx.x; i < 64 * 16; i += 256) {
+      const int kl = i >> 4, ol = (i & 15) * 4, o = o0 + ol, k = k0 + kl;
+      if (o >= d.O || k >= KC) continue;   // O % 4 == 0: the quad is all in or all out
+      const int j = jcs[kl] >> 16, c = jcs[kl] & 0xffff;
+      uint2 h;
+      h.x = (unsigned)__builtin_bit_cast(unsigned short, (bf16)tile[ol][kl]) |
+            ((unsigned)__builtin_bit_cast(unsigned short, (bf16)tile[ol + 1][kl]) << 16);
+      h.y = (unsigned)__builtin_bit_cast(unsigned short, (bf16)tile[ol + 2][kl]) |
+            ((unsigned)__builtin_bit_cast(unsigned short, (bf16)tile[ol + 3][kl]) << 16);
+      *(uint2*)(Wb + (long)c * d.ldb + (long)j * d.O + o) = h;
+    }
+    return;
+  }
   for (int i = threadIdx.x; i < 64 * 64; i += blockDim.x) {
     const int ol = i >> 6, kl = i & 63, o = o0 + ol, k = k0 + kl;
     if (o >= d.O || k >= d.ldf) continue;
@@ -207,7 +263,6 @@ __global__ void __launch_bounds__(256) adamw_prep_tiles_kernel(const fs2_wprep_d
   }
   if (!d.Wb) return;
   __syncthreads();
-  T* Wb = (T*)d.Wb;
   for (int i = threadIdx.x; i < 64 * 64; i += blockDim.x) {
     const int kl = i >> 6, ol = i & 63, o = o0 + ol, k = k0 + kl;
     if (o >= d.O || k >= KC) continue;
