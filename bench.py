@@ -452,8 +452,10 @@ def main():
                 "frac": (wach / MFMA_BF16_PEAK_TFLOPS) if wach else None,
                 "traffic": wtraffic, "traffic_source": wtraffic_src,
                 "launches": wn, "avg_ms": wms, "flop_per_launch": kflop,
-                "timing": "HIP events on the weight-gradient side stream around the GEMM launch, "
-                          "concurrent with the main stream's conv1 data gradient"},
+                "timing": "HIP events on the weight-gradient side stream around the GEMM launch; "
+                          "it is enqueued beside the main stream's conv1 data gradient (a "
+                          "persistent kernel holding one block per CU), so the duration includes "
+                          "its wait for CUs (DESIGN.md 6.4 has the standalone time)"},
             "hip_graph": graphed,
             # the step-level roofline on VALID frames -- frames/s x the train FLOPs
             # of one mel frame at T_phon=200, T_mel=1000 (338.8 MFLOP at default dims) / peak
