@@ -1713,7 +1713,18 @@ __device__ __forceinline__ int ps_sw(int row) { return (row >> 1) & 7; }
 // CM: 0 plain, 1 reflect "same" conv, 4 padded-domain conv (dgrad).  EO: 1 = a bf16 [M][N]
 // epilogue operand (the ReLU gate OR the residual; plain A, 256 x 192 tiles), loaded into
 // registers in the tile's last K-tile ahead of that iteration's DMA.
-template <int CM, int WN, int EO = 0>
+// BT: 1 = conv_mode 6, the K-major weight gradient over channel-major padded images
+// (layout.hip): B row n = (tap j, channel c) reads image row c shifted by j - P columns, i.e.
+// a per-lane constant source offset; the source is then only 2-byte aligned, which the
+// LDS-DMA takes (tools/micro/dma_unaligned.hip).  The resource base sits BT_GUARD elements
+// before B so the first row's negative shifts stay in range (the caller allocates that guard).
+// Split-K (BT only): work unit u = (split s, tile), s = u / tiles; split s covers K-tiles
+// [s * nk, (s + 1) * nk) of K = split_k * k_per_split and stores its fp32 partial to
+// C + s * split_stride (caller sums the slices).  The launch gives every unit its own block
+// (units <= grid), so a block's unit, K base and output slice are fixed at entry -- per-tile
+// unit arithmetic in the loop spilled SGPRs into VGPR lanes and corrupted the accumulators.
+constexpr int BT_GUARD = 64;
+template <int CM, int WN, int EO = 0, int BT = 0>
 __global__ void __launch_bounds__(BNT, 1) gemm_ps_kernel(GemmP p) {
   constexpr int BN = 4 * WN, NJ = WN / 16;
   constexpr int AIMG = 256 * 128;
@@ -1732,15 +1743,23 @@ __global__ void __launch_bounds__(BNT, 1) gemm_ps_kernel(GemmP p) {
   char* const epl = smem + 2 * SLOT + wave * EPW;
   const int li = lane & 15, lg = lane >> 4;
   const int ntile = p.tiles_m * p.tiles_n;
+  const int nsplit = BT && p.split_k > 1 ? p.split_k : 1;   // compile-time 1 unless BT
+  const int nunit = ntile * nsplit;   // BT: <= gridDim.x, one unit per block
   const int G = gridDim.x;
   const int xcd = blockIdx.x & 7, local = blockIdx.x >> 3;
   const int nbx = (G - xcd + 7) >> 3;
-  const int c0 = (int)((long)ntile * xcd / 8), c1 = (int)((long)ntile * (xcd + 1) / 8);
+  const int c0 = (int)((long)nunit * xcd / 8), c1 = (int)((long)nunit * (xcd + 1) / 8);
   const int mine = local < c1 - c0 ? (c1 - c0 - local + nbx - 1) / nbx : 0;
-  const int nk = (p.K + 63) / 64;
+  const int nk = nsplit > 1 ? p.k_per_split / 64 : (p.K + 63) / 64;
   const int total = mine * nk;
   if (total == 0) return;
-  const i32x4 rsA = make_rsrc(p.A), rsB = make_rsrc(p.B), rsC = make_rsrc(p.C);
+  // BT: this block's unit (split bt_sp, tile bt_tile), fixed for the whole launch
+  const int bt_unit = c0 + local;
+  const int bt_sp = BT && nsplit > 1 ? __builtin_amdgcn_readfirstlane(bt_unit / ntile) : 0;
+  const int bt_tile = BT ? bt_unit - bt_sp * ntile : 0;
+  const int bt_kb = BT ? bt_sp * nk * 64 : 0;
+  const i32x4 rsA = make_rsrc(p.A), rsC = make_rsrc(p.C);
+  const i32x4 rsB = make_rsrc(BT ? p.B - BT_GUARD * 2 : p.B);
   static_assert(EO == 0 || (CM == 0 && WN == 48), "epilogue operands: plain 256 x 192 only");
   constexpr int EL = EO ? 8 * (WN / 16) : 0;   // operand loads per wave in a tile's last K-tile
   const i32x4 rsE = make_rsrc(EO ? (p.gate ? (const void*)p.gate : (const void*)p.residual)
@@ -1769,7 +1788,7 @@ __global__ void __launch_bounds__(BNT, 1) gemm_ps_kernel(GemmP p) {
     blc[q] = (lane & 7) ^ ps_sw(brow[q]);
   }
   // A stream (units of iteration g + 1): tile ordinal, k-tile, tap, row info, lane offsets
-  int a_t = 0, a_kt = -1, a_tap = 0, a_c = 0;
+  int a_t = 0, a_kt = -1, a_tap = 0, a_c = 0, a_kb = 0;
   int abt[4], at_[4], aoff[4];
   bool aval[4];
   auto a_point = [&]() {   // lane offsets of the current tap (conv) / row (plain)
@@ -1792,8 +1811,9 @@ __global__ void __launch_bounds__(BNT, 1) gemm_ps_kernel(GemmP p) {
   };
   auto a_advance = [&]() {  // to the next iteration of the A stream
     if (++a_kt == nk) { a_kt = 0; ++a_t; }
-    if (a_kt == 0) {
-      const int tile = c0 + local + a_t * nbx;
+    if (a_kt == 0 && (!BT || a_t == 0)) {
+      const int tile = BT ? bt_tile : c0 + local + a_t * nbx;
+      a_kb = bt_kb;
       const int tm = tile / p.tiles_n;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -1816,7 +1836,7 @@ __global__ void __launch_bounds__(BNT, 1) gemm_ps_kernel(GemmP p) {
     }
   };
   auto issue_a = [&](int unit, char* slot) {
-    const int k0 = a_kt * 64;
+    const int k0 = a_kb + a_kt * 64;
     const int soff = __builtin_amdgcn_readfirstlane((CM ? a_c * 64 : k0) * 2);   // uniform by construction
     const bool kin = k0 + 64 <= K;
 #pragma unroll
@@ -1827,11 +1847,11 @@ __global__ void __launch_bounds__(BNT, 1) gemm_ps_kernel(GemmP p) {
     }
   };
   // B stream (units of iteration g + 2)
-  int b_t = 0, b_kt = -1;
+  int b_t = 0, b_kt = -1, b_kb = 0;
   int boff[2 + NB1];
   auto b_advance = [&]() {
     if (++b_kt == nk) { b_kt = 0; ++b_t; }
-    if (b_kt == 0) {
+    if (!BT && b_kt == 0) {   // BT: one tile per block, offsets set below
       const int tile = c0 + local + b_t * nbx;
       const int tn = tile - (tile / p.tiles_n) * p.tiles_n;
 #pragma unroll
@@ -1841,8 +1861,19 @@ __global__ void __launch_bounds__(BNT, 1) gemm_ps_kernel(GemmP p) {
       }
     }
   };
+  if constexpr (BT) {   // the block's one tile: row = (tap j, channel c) reads image row c
+    b_kb = bt_kb;       // shifted j - P columns
+    const int tn = bt_tile - (bt_tile / p.tiles_n) * p.tiles_n;
+#pragma unroll
+    for (int q = 0; q < 2 + NB1; ++q) {
+      const int row = tn * BN + brow[q];
+      const int j = row / p.conv_c, c = row - j * p.conv_c;
+      boff[q] = row < p.N ? (int)(((long)c * p.ldb + blc[q] * 8 + j - p.conv_p + BT_GUARD) * 2)
+                          : BUF_OOB;
+    }
+  }
   auto issue_b = [&](int unit, char* slot) {
-    const int k0 = b_kt * 64;
+    const int k0 = b_kb + b_kt * 64;
     const bool kin = k0 + 64 <= K;
 #pragma unroll
     for (int q = unit * 2; q < (unit ? 2 + NB1 : 2); ++q) {
@@ -1862,7 +1893,7 @@ __global__ void __launch_bounds__(BNT, 1) gemm_ps_kernel(GemmP p) {
   // iteration, so the ring's counted waits retire them long before the epilogue reads them --
   // no vmcnt(0) drain of the ring per tile (global loads there cost ~5-10 us per tile)
   auto issue_epi = [&](int tt) {
-    const int tile = c0 + local + tt * nbx;
+    const int tile = BT ? bt_tile : c0 + local + tt * nbx;
     const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
     const int n = tn * BN + wc * WN + 4 * lane;
     const bool bok = p.bias && lane < WN / 4 && n < p.nvalid;
@@ -1927,7 +1958,7 @@ __global__ void __launch_bounds__(BNT, 1) gemm_ps_kernel(GemmP p) {
       if (ph == 0 && first) issue_epi(t);
       if constexpr (EO && ph == 0) {
         if (last) {   // older than this iteration's DMA: the epilogue waits for them, not it
-          const int tile = c0 + local + t * nbx;
+          const int tile = c0 + local + t * nbx;   // EO: no split, unit == tile
           const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
           const int mb = tm * 256 + wr * 128, nb = tn * BN + wc * WN;
 #pragma unroll
@@ -1983,9 +2014,10 @@ __global__ void __launch_bounds__(BNT, 1) gemm_ps_kernel(GemmP p) {
       if (ph == 3 && last && !(XFLAGS(p) & 32)) {   // flag 32: timing only, no epilogue
         // ---- tile epilogue, straight from the accumulators; operands from the wave's LDS
         // area (landed: retired by the counted waits since the tile's first K-tile) ----
-        const int tile = c0 + local + t * nbx;
+        const int tile = BT ? bt_tile : c0 + local + t * nbx;
         const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
         const int mb = tm * 256 + wr * 128, nb = tn * BN + wc * WN;
+        const int soc = BT ? (int)(bt_sp * p.split_stride * 4) : 0;
         f32x4 bv[NJ];
 #pragma unroll
         for (int j = 0; j < NJ; ++j) bv[j] = *(const f32x4*)(epl + (16 * j + 4 * lg) * 4);
@@ -2036,8 +2068,12 @@ __global__ void __launch_bounds__(BNT, 1) gemm_ps_kernel(GemmP p) {
               const f32x4 v = fin(i, j);
               const int n = nb + 16 * j + 4 * lg;
               const bool ok = rowok && n < p.nvalid && !nost;
+              // the slice offset goes into voffset, soffset stays 0: with an SGPR soffset
+              // LLVM assumes no VMEM-store-data hazard and inserts no wait before the next
+              // write of the store's data VGPRs -- on gfx950 the store then read the NEXT
+              // fragment's values in lanes 12-15 of each row group (tools/km_debug.py)
               llvm_raw_buffer_store_v4i32(__builtin_bit_cast(i32x4, v), rsC,
-                                          ok ? (int)(((long)m * p.ldc + n) * 4) : BUF_OOB, 0, 0);
+                                          ok ? (int)(((long)m * p.ldc + n) * 4) + soc : BUF_OOB, 0, 0);
             }
             continue;
           }
@@ -2132,6 +2168,19 @@ int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
     // persistent 256 x 256 / 256 x 192 kernel: long-K K-major GEMMs without gate / residual
     // operands (FS2_GEMM_NO_PS=1 restores the per-tile kernels for A/B runs)
     static const bool no_ps = getenv_flag("FS2_GEMM_NO_PS");
+    if (p.conv_mode == 6) {
+      if (!p.vec_align) return FS2_EALIGN;
+      GemmP q = p;
+      q.g4_flags = getenv_int("FS2_PS_FLAGS", 0);
+      q.tiles_m = (p.M + 255) / 256;
+      q.tiles_n = (p.N + 255) / 256;
+      const int nu = q.tiles_m * q.tiles_n * max(1, p.split_k);
+      if (nu > 1024) return FS2_EINVAL;   // one unit per block (gemm_ps_kernel BT)
+      const int g = (nu + 7) / 8 * 8;
+      hipLaunchKernelGGL((gemm_ps_kernel<0, 64, 0, 1>), dim3(g), dim3(BNT), 0, s, q);
+      FS2_CHECK_LAUNCH();
+      return 0;
+    }
     // FS2_PS_MODES: bit 0 plain, bit 1 reflect conv (fwd), bit 2 padded-domain conv (dgrad).
     // Default 5: in the bench step the unsplit decoder conv1 data gradient gains 0.15-0.2 ms,
     // while the conv1 forward measured 0-0.1 ms slower than gemm256_kernel (A/B runs).
@@ -2350,6 +2399,17 @@ extern "C" int fs2_gemm(const fs2_gemm_desc* d, void* stream) {
     if (p.conv_mode == 4 && !d->a_kmajor) return FS2_EINVAL;
     if (p.conv_mode == 4 && p.K != p.conv_kw * p.conv_c) return FS2_EINVAL;
     if (p.conv_mode == 3 && (d->b_kmajor || p.N != p.conv_kw * p.conv_c)) return FS2_EINVAL;
+    if (p.conv_mode == 6) {   // K-major weight gradient over padded channel-major images
+      if (d->dtype != FS2_BF16 || !d->a_kmajor || !d->b_kmajor || !p.c_fp32 ||
+          p.N != p.conv_kw * p.conv_c || (p.K % 64) || p.bias || p.gate || p.residual ||
+          p.row_scale || p.row_scale_post || p.relu || p.c_conv_kw || batch > 1 || p.accumulate)
+        return FS2_EINVAL;
+      if (p.split_k > 1 && (p.split_stride <= 0 || (p.K % (64 * p.split_k)))) return FS2_EINVAL;
+      const long lim = 0x7fffffffL;
+      if ((long)p.M * p.lda * 2 >= lim || ((long)p.conv_c * p.ldb + 2 * BT_GUARD) * 2 >= lim ||
+          (long)p.split_k * (p.split_stride + (long)p.mvalid * p.ldc) * 4 >= lim)
+        return FS2_EINVAL;
+    }
   }
   if (p.c_conv_kw > 0 && (p.N % p.c_conv_kw)) return FS2_EINVAL;
   int split_req = p.split_k;

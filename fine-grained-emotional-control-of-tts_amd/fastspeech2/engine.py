@@ -71,6 +71,9 @@ _PS_MODES = N.exp_int("FS2_PS_MODES", 5)
 # result no longer depends on atomic ordering.  FS2_NO_WGRAD_BIG_SLICES=1 restores the atomics.
 _BIG_SLICES = not N.exp_flag("FS2_NO_WGRAD_BIG_SLICES")
 _SLICE_TARGET = N.exp_int("FS2_WGRAD_SLICE_TARGET", 240)
+# conv weight gradients with both operands K-major (channel-major padded images, conv_mode 6):
+# FS2_KM_WGRAD=0 restores the MN-major implicit-conv GEMM for A/B runs
+_KM_WGRAD = N.exp_int("FS2_KM_WGRAD", 1)
 # serial mode for per-call-site timing (bench.py --detail runs with the experiments library)
 _NO_SIDE = N.exp_flag("FS2_NO_SIDE_STREAM")
 _NO_AUX = N.exp_flag("FS2_NO_AUX_STREAM")
@@ -121,6 +124,7 @@ class FS2Engine:
         self._wtable = None          # device descriptor table of every GEMM weight image
         self.on_grads_ready = None   # optional callback(tag) for DP overlap
         self.timer = None            # optional KernelTimer: HIP events around tagged launches
+        self._km = {}                # conv_mode-6 images, reused layer after layer (side stream)
 
     def _tic(self, tag):
         if self.timer is not None:
@@ -348,11 +352,61 @@ class FS2Engine:
             self._toc(tag)
         self._side_exit(h)
 
+    def _km_ok(self, O, C, KW, T, n_cols):
+        """conv weight gradients that take the K-major path (conv_mode 6): the FFN conv1
+        (k = 9) and PostNet (k = 5) weights.  tools/km_wgrad_bench.py, B = 32, GEMM + slice sum
+        + both transposes vs the MN-major implicit-conv GEMM: decoder conv1 464 -> 372 us,
+        encoder conv1 115 -> 110, PostNet 218 / 237 / 221 -> 125 / 98 / 75; the k = 3
+        predictor convs lose (58 -> 67: the transposes cost more than the GEMM saves)."""
+        return (self.dt == 1 and _KM_WGRAD and KW >= 5 and n_cols is None and
+                C % 8 == 0 and O % 8 == 0 and (KW - 1) // 2 < T)
+
+    def _km_image(self, key, C, ld):
+        """bf16 [C][ld] image with a zeroed guard of 64 elements before row 0 and after the
+        last row (the tap-shifted reads of conv_mode 6 reach P elements past either end)"""
+        k = (key, C, ld)
+        buf = self._km.get(k)
+        if buf is None:
+            buf = torch.zeros(C * ld + 128, dtype=torch.bfloat16, device=self.dev)
+            self._km[k] = buf
+        return buf[64:64 + C * ld]
+
+    def _wgrad_km(self, dY, lddy, X, ldx, M, T, wname, gemm_tag=None):
+        """grad[O][KW][C] += sum_{b,t} dY[b,t,o] X[b, reflect(t+j-P), c] with both GEMM operands
+        K-major: dY and X are first written channel-major over the padded token domain (T+2P
+        columns per utterance; dY's pad columns zero, X's reflected), where tap j is a constant
+        column shift j - P of X's image (fs2_pad_transpose + conv_mode 6).  Same sum as
+        _wgrad_impl's implicit-conv GEMM (SB Conv1d weight gradient, model.py:241-267)."""
+        O, C, KW = self._wspecs[wname]
+        P = (KW - 1) // 2
+        B = M // T
+        Bt = B * (T + 2 * P)
+        ncol = KW * C
+        tiles = -(-O // 256) * -(-ncol // 256)
+        # one (split, tile) unit per CU; >= 16 K-tiles per unit, <= 25 fp32 slices to sum
+        S = max(1, min(256 // tiles, -(-Bt // 64) // 16, 25))
+        Kp = round_up(Bt, 64 * S)
+        dYT = self._km_image("dy", O, Kp)
+        XT = self._km_image("x", C, Kp)
+        ops.pad_transpose(dY, lddy, B, T, O, P, 0, dYT, Kp, Kp, dt=self.dt)
+        ops.pad_transpose(X, ldx, B, T, C, P, 1, XT, Kp, Kp, dt=self.dt)
+        stride = O * ncol
+        ws = self.ws(S * stride)
+        if gemm_tag:
+            self._tic(gemm_tag)
+        ops.gemm(O, ncol, Kp, dYT, Kp, XT, Kp, ws, ncol, dt=self.dt, conv=(6, T, KW, C),
+                 c_fp32=1, split_k=S, split_stride=stride if S > 1 else 0)
+        if gemm_tag:
+            self._toc(gemm_tag)
+        ops.sum_slices(ws, S, stride, stride, self.grads[wname], accumulate=1)
+
     def _wgrad_impl(self, dY, lddy, X, ldx, M, T, wname, n_cols=None, gemm_tag=None):
         """grad[O][KW][C] += sum_m dY[m][o] * X[reflect(t+j-P)][c]   (fp32, accumulate).
         ``gemm_tag``: HIP events around the GEMM launch alone (bench.py's roofline entry for
         the FFN conv1 weight gradient), on the stream it runs on (the side stream)."""
         O, C, KW = self._wspecs[wname]
+        if self._km_ok(O, C, KW, T, n_cols) and lddy % 8 == 0 and ldx % 8 == 0:
+            return self._wgrad_km(dY, lddy, X, ldx, M, T, wname, gemm_tag)
         Ncols = n_cols or KW * C
         K = round_up(M, self.epc)
         tiles = -(-O // 128) * -(-Ncols // 128)

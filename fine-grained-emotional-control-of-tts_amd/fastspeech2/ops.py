@@ -66,6 +66,11 @@ def conv_fold(Xpad, B, T, P, C, out, ldo, *, dt, residual=None, ldr=0, row_scale
                                _p(row_scale), _p(row_scale_post), dt, _s()), "fs2_conv_fold")
 
 
+def pad_transpose(X, ldx, B, T, C, P, reflect, out, ldo, ncols, *, dt):
+    _chk(N.lib().fs2_pad_transpose(_p(X), ldx, B, T, C, P, reflect, _p(out), ldo, ncols, dt, _s()),
+         "fs2_pad_transpose")
+
+
 def sum_slices(ws, nslices, stride, n, out, accumulate=1):
     _chk(N.lib().fs2_sum_slices(_p(ws), nslices, stride, n, _p(out), accumulate, _s()),
          "fs2_sum_slices")

@@ -53,6 +53,12 @@ typedef struct fs2_gemm_desc {
    *      utterance: the data gradient in the padded domain, finished by fs2_conv_fold
    *   5: A fwd   A(m=(b,t), k=(j,c)) = X[b, t+j-P, c], 0 outside [0,T): zero-padded "same"
    *      conv (torch nn.Conv1d(padding=k//2), IntensityExtractor FFN, rank_model/model.py:23-24)
+   *   6: B wgrad, K-major over padded channel-major images (fs2_pad_transpose):
+   *      B(k, n=(j,c)) = B[c*ldb + k + j - P] (b_kmajor; k runs over the padded token domain,
+   *      T+2P columns per utterance; A = the zero-padded channel-major dY image, so products
+   *      across utterances vanish).  B must have 64 readable elements before it and P after
+   *      each row end; K % 64 == 0; fp32 output, split-K only as split_stride slices with
+   *      K % (64 * split_k) == 0, no epilogue operations
    * P = (conv_kw-1)/2, conv_c = channels per tap, conv_t = tokens per utterance.          */
   int conv_mode, conv_t, conv_kw, conv_c;
   void* C; int64_t ldc; int c_fp32;           /* output; c_fp32: float output else dtype     */
@@ -88,6 +94,14 @@ int fs2_conv_fold(const float* Xpad, int nsplit, int64_t split_stride, int B, in
 /* out[i] (+)= sum_{s < nslices} ws[s*stride + i], i < n (fp32; n, stride multiples of 4,
  * 16-byte aligned): the sum of split-K weight-gradient slices written by fs2_gemm with
  * split_stride (no atomics; fixed summation order)                                         */
+/* channel-major padded image for conv_mode 6 (backward of the SB Conv1d weights, App. A.1;
+ * model.py:241-267 FFN conv1): out[c][b*(T+2P) + i] = X[b*T + reflect(i-P)][c] (reflect = 1)
+ * or X[b*T + i-P][c] inside [0,T) and 0 outside (reflect = 0), i in [0, T+2P); columns
+ * [B*(T+2P), ncols) are written as 0.  X bf16 [B*T][ldx]; out bf16 [C][ldo]; C, ldx, ldo,
+ * ncols multiples of 8, ldo >= ncols >= B*(T+2P), both pointers 16-byte aligned.          */
+int fs2_pad_transpose(const void* X, int64_t ldx, int B, int T, int C, int P, int reflect,
+                      void* out, int64_t ldo, int ncols, int dtype, void* stream);
+
 int fs2_sum_slices(const float* ws, int nslices, int64_t stride, int64_t n, float* out,
                    int accumulate, void* stream);
 

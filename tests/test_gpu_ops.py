@@ -487,6 +487,59 @@ def test_wgrad_conv3_slices(cuda, Bn, T, O, Cin, KW, ns):
     assert rel(ws.sum(0), ref) < 2e-2
 
 
+@pytest.mark.parametrize("Bn,T,O,Cin,KW,S", [(32, 977, 1536, 384, 9, 3), (32, 200, 1536, 384, 9, 3),
+                                             (4, 77, 600, 72, 9, 1), (3, 130, 520, 128, 5, 2),
+                                             (2, 50, 1024, 80, 5, 4)])
+def test_wgrad_kmajor_padded_images(cuda, Bn, T, O, Cin, KW, S):
+    """conv_mode 6 (the engine's FFN conv1 weight gradient): fs2_pad_transpose writes dY
+    (zero pads) and X (reflect pads) channel-major over the padded token domain, exactly the
+    torch construction; the K-major GEMM over them (gemm_ps_kernel<0, 64, 0, 1>, tap j = a
+    column shift j - P, 2-byte-aligned LDS-DMA sources, split-K fp32 slices) equals the fp32
+    reference of the same bf16 values (rel 1e-3: both sum exact bf16 products in fp32).  Shapes:
+    decoder / encoder FFN conv1, ragged M / N / K (tile edges, utterance boundaries inside
+    K-tiles, odd T), one slice, four slices."""
+    from fastspeech2 import ops
+    torch.manual_seed(T + O + S)
+    P = (KW - 1) // 2
+    M = Bn * T
+    Tp = T + 2 * P
+    X = torch.randn(Bn, T, Cin, device=cuda).to(torch.bfloat16)
+    G = torch.randn(M, O, device=cuda).to(torch.bfloat16)
+    idx = torch.arange(T, device=cuda)
+    cols = []
+    for j in range(KW):
+        src = idx + j - P
+        src = torch.where(src < 0, -src, src)
+        src = torch.where(src >= T, 2 * (T - 1) - src, src)
+        cols.append(X[:, src, :].float())
+    ref = G.float().t() @ torch.cat(cols, dim=2).reshape(M, KW * Cin)
+    Kp = ops.round_up(Bn * Tp, 64 * S)
+    # images with zeroed 64-element guards before row 0 and after the last row
+    gy = torch.full((O * Kp + 128,), float("nan"), device=cuda).to(torch.bfloat16)
+    gx = torch.zeros(Cin * Kp + 128, device=cuda).to(torch.bfloat16)
+    dYT, XT = gy[64:64 + O * Kp], gx[64:64 + Cin * Kp]
+    ops.pad_transpose(G, O, Bn, T, O, P, 0, dYT, Kp, Kp, dt=1)
+    ops.pad_transpose(X, Cin, Bn, T, Cin, P, 1, XT, Kp, Kp, dt=1)
+    ipad = torch.arange(-P, T + P, device=cuda)
+    rpad = torch.where(ipad < 0, -ipad, ipad)
+    rpad = torch.where(rpad >= T, 2 * (T - 1) - rpad, rpad)
+    xi = torch.zeros(Cin, Kp, device=cuda, dtype=torch.bfloat16)
+    xi[:, :Bn * Tp] = X[:, rpad, :].reshape(Bn * Tp, Cin).t()
+    gi = torch.zeros(Bn, Tp, O, device=cuda, dtype=torch.bfloat16)
+    gi[:, P:P + T] = G.reshape(Bn, T, O)
+    yi = torch.zeros(O, Kp, device=cuda, dtype=torch.bfloat16)
+    yi[:, :Bn * Tp] = gi.reshape(Bn * Tp, O).t()
+    assert torch.equal(XT.reshape(Cin, Kp), xi)
+    assert torch.equal(dYT.reshape(O, Kp), yi)
+    stride = O * KW * Cin
+    ws = torch.full((S, O, KW * Cin), float("nan"), device=cuda)
+    ops.gemm(O, KW * Cin, Kp, dYT, Kp, XT, Kp, ws, KW * Cin, dt=1, conv=(6, T, KW, Cin),
+             c_fp32=1, split_k=S, split_stride=stride if S > 1 else 0)
+    torch.cuda.synchronize()
+    assert torch.isfinite(ws).all()
+    assert rel(ws.sum(0), ref) < 1e-3
+
+
 @pytest.mark.parametrize("dt,code", [(torch.float32, 0), (torch.bfloat16, 1)])
 def test_add3_mask_rows(cuda, dt, code):
     """fs2_add3_mask_rows: X = (X + Y + Z) * keep[row] in fp32 with one rounding, row pitch > D."""
@@ -505,7 +558,7 @@ def test_add3_mask_rows(cuda, dt, code):
 @pytest.mark.parametrize("M,N,K,c32", [(1000, 1536, 2048, 0), (31264, 1536, 3456, 0),
                                         (700, 384, 4096, 1), (300, 200, 2056, 1),
                                         (6400, 1536, 3456, 0), (2000, 384, 8192, 1),
-                                        (5000, 700, 3000, 1)])
+                                        (5000, 700, 3000, 1), (10752, 1536, 2048, 1)])
 def test_gemm_persistent_long_k(cuda, M, N, K, c32):
     """Long-K K-major GEMMs take the persistent 256 x 256 / 256 x 192 kernel (gemm_ps_kernel):
     both tile widths, partial row / column tiles, a partial last K-tile (K = 2056), bf16 and
