@@ -446,8 +446,10 @@ def main():
                                     "timed region" if graphed else
                                     "HIP events on the engine stream over the timed region")},
             "roofline_conv1_wgrad": {
-                "bound": "mfma", "kernel": "decoder FFN conv1 (k=9) weight gradient, implicit "
-                                           "reflect-conv B operand, 3 split-K fp32 planes",
+                "bound": "mfma", "kernel": "decoder FFN conv1 (k=9) weight gradient: K-major GEMM "
+                                           "over channel-major padded dY / X images (conv_mode 6, "
+                                           "gemm_ps_kernel<0, 64, 0, 1>), 3 split-K fp32 slices; "
+                                           "the two image transposes are separate launches",
                 "achieved": wach, "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": (wach / MFMA_BF16_PEAK_TFLOPS) if wach else None,
                 "traffic": wtraffic, "traffic_source": wtraffic_src,

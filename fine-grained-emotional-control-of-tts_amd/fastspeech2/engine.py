@@ -342,14 +342,19 @@ class FS2Engine:
                       row_scale_post=epi.get("row_scale_post"), nsplit=split,
                       split_stride=Mp * C)
 
-    def _wgrad(self, dY, lddy, X, ldx, M, T, wname, n_cols=None, gemm_tag=None):
+    def _wgrad(self, dY, lddy, X, ldx, M, T, wname, n_cols=None, gemm_tag=None, bias=None):
+        """weight gradient on the side stream; ``bias``: also the bias gradient (column sums of
+        dY) -- fused into the K-major path's dY transpose, else an fs2_colsum pass"""
         h = self._side_enter(dY, X)
         tag = self._dtag("wgrad", wname, T)
         if tag:
             self._tic(tag)
-        self._wgrad_impl(dY, lddy, X, ldx, M, T, wname, n_cols, gemm_tag)
+        done = self._wgrad_impl(dY, lddy, X, ldx, M, T, wname, n_cols, gemm_tag, bias)
         if tag:
             self._toc(tag)
+        if bias is not None and not done:
+            O = self._wspecs[wname][0]
+            ops.colsum(dY, lddy, M, O, self.grads[bias], dt=self.dt, ws=self.ws(ops.colsum_ws(M, O)))
         self._side_exit(h)
 
     def _km_ok(self, O, C, KW, T, n_cols):
@@ -371,7 +376,7 @@ class FS2Engine:
             self._km[k] = buf
         return buf[64:64 + C * ld]
 
-    def _wgrad_km(self, dY, lddy, X, ldx, M, T, wname, gemm_tag=None):
+    def _wgrad_km(self, dY, lddy, X, ldx, M, T, wname, gemm_tag=None, bias=None):
         """grad[O][KW][C] += sum_{b,t} dY[b,t,o] X[b, reflect(t+j-P), c] with both GEMM operands
         K-major: dY and X are first written channel-major over the padded token domain (T+2P
         columns per utterance; dY's pad columns zero, X's reflected), where tap j is a constant
@@ -388,7 +393,9 @@ class FS2Engine:
         Kp = round_up(Bt, 64 * S)
         dYT = self._km_image("dy", O, Kp)
         XT = self._km_image("x", C, Kp)
-        ops.pad_transpose(dY, lddy, B, T, O, P, 0, dYT, Kp, Kp, dt=self.dt)
+        ws = self.ws(max(ops.pad_transpose_ws(Kp, O), 1))
+        ops.pad_transpose(dY, lddy, B, T, O, P, 0, dYT, Kp, Kp, dt=self.dt,
+                          colsum=self.grads[bias] if bias is not None else None, ws=ws)
         ops.pad_transpose(X, ldx, B, T, C, P, 1, XT, Kp, Kp, dt=self.dt)
         stride = O * ncol
         ws = self.ws(S * stride)
@@ -399,14 +406,15 @@ class FS2Engine:
         if gemm_tag:
             self._toc(gemm_tag)
         ops.sum_slices(ws, S, stride, stride, self.grads[wname], accumulate=1)
+        return True
 
-    def _wgrad_impl(self, dY, lddy, X, ldx, M, T, wname, n_cols=None, gemm_tag=None):
+    def _wgrad_impl(self, dY, lddy, X, ldx, M, T, wname, n_cols=None, gemm_tag=None, bias=None):
         """grad[O][KW][C] += sum_m dY[m][o] * X[reflect(t+j-P)][c]   (fp32, accumulate).
         ``gemm_tag``: HIP events around the GEMM launch alone (bench.py's roofline entry for
         the FFN conv1 weight gradient), on the stream it runs on (the side stream)."""
         O, C, KW = self._wspecs[wname]
         if self._km_ok(O, C, KW, T, n_cols) and lddy % 8 == 0 and ldx % 8 == 0:
-            return self._wgrad_km(dY, lddy, X, ldx, M, T, wname, gemm_tag)
+            return self._wgrad_km(dY, lddy, X, ldx, M, T, wname, gemm_tag, bias)
         Ncols = n_cols or KW * C
         K = round_up(M, self.epc)
         tiles = -(-O // 128) * -(-Ncols // 128)
@@ -537,8 +545,8 @@ class FS2Engine:
         self._wgrad(dY, D, ctx["Hc"], F, M, T, w2)
         self._dgrad(dY, D, M, T, w2, dHc, F, gate=ctx["Hc"], ldg=F)
         self._wgrad(dHc, F, ctx["X1"], D, M, T, w1,
-                    gemm_tag="ffn_conv1_wgrad." + prefix.split(".")[0])
-        self._bias_grad(dHc, F, M, F, prefix + "pos_ffn.0.conv.bias")
+                    gemm_tag="ffn_conv1_wgrad." + prefix.split(".")[0],
+                    bias=prefix + "pos_ffn.0.conv.bias")
         self._dgrad(dHc, F, M, T, w1, dX1, D, residual=ds2, ldr=D)
         del dY, dHc, ds2
         lnws = self.ws(ops.ln_ws(M, D))
@@ -752,9 +760,8 @@ class FS2Engine:
                 return dmel
             dprev = self.empty(M, E)
             self._dgrad(dx, E, M, T, name + ".conv.weight", dprev, E)
-            self._wgrad(dx, E, xin, ldx, M, T, name + ".conv.weight")
-            if i != bias_done:
-                self._bias_grad(dx, E, M, E, name + ".conv.bias")
+            self._wgrad(dx, E, xin, ldx, M, T, name + ".conv.weight",
+                        bias=name + ".conv.bias" if i != bias_done else None)
             dx = dprev
 
     # ------------------------------------------------------------------ full forward

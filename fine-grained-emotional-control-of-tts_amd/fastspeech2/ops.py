@@ -66,9 +66,13 @@ def conv_fold(Xpad, B, T, P, C, out, ldo, *, dt, residual=None, ldr=0, row_scale
                                _p(row_scale), _p(row_scale_post), dt, _s()), "fs2_conv_fold")
 
 
-def pad_transpose(X, ldx, B, T, C, P, reflect, out, ldo, ncols, *, dt):
-    _chk(N.lib().fs2_pad_transpose(_p(X), ldx, B, T, C, P, reflect, _p(out), ldo, ncols, dt, _s()),
-         "fs2_pad_transpose")
+def pad_transpose(X, ldx, B, T, C, P, reflect, out, ldo, ncols, *, dt, colsum=None, ws=None):
+    _chk(N.lib().fs2_pad_transpose(_p(X), ldx, B, T, C, P, reflect, _p(out), ldo, ncols,
+                                   _p(colsum), _p(ws), dt, _s()), "fs2_pad_transpose")
+
+
+def pad_transpose_ws(ncols, C):
+    return -(-ncols // 64) * C
 
 
 def sum_slices(ws, nslices, stride, n, out, accumulate=1):

@@ -98,9 +98,12 @@ int fs2_conv_fold(const float* Xpad, int nsplit, int64_t split_stride, int B, in
  * model.py:241-267 FFN conv1): out[c][b*(T+2P) + i] = X[b*T + reflect(i-P)][c] (reflect = 1)
  * or X[b*T + i-P][c] inside [0,T) and 0 outside (reflect = 0), i in [0, T+2P); columns
  * [B*(T+2P), ncols) are written as 0.  X bf16 [B*T][ldx]; out bf16 [C][ldo]; C, ldx, ldo,
- * ncols multiples of 8, ldo >= ncols >= B*(T+2P), both pointers 16-byte aligned.          */
+ * ncols multiples of 8, ldo >= ncols >= B*(T+2P), both pointers 16-byte aligned.
+ * colsum (optional, reflect = 0 only): colsum[c] += sum_t X[t][c] -- the conv bias gradient
+ * (K13 bias), replacing an fs2_colsum pass; workspace >= ceil(ncols/64) * C floats.        */
 int fs2_pad_transpose(const void* X, int64_t ldx, int B, int T, int C, int P, int reflect,
-                      void* out, int64_t ldo, int ncols, int dtype, void* stream);
+                      void* out, int64_t ldo, int ncols, float* colsum, float* workspace,
+                      int dtype, void* stream);
 
 int fs2_sum_slices(const float* ws, int nslices, int64_t stride, int64_t n, float* out,
                    int accumulate, void* stream);

@@ -493,7 +493,7 @@ def test_wgrad_conv3_slices(cuda, Bn, T, O, Cin, KW, ns):
 def test_wgrad_kmajor_padded_images(cuda, Bn, T, O, Cin, KW, S):
     """conv_mode 6 (the engine's FFN conv1 weight gradient): fs2_pad_transpose writes dY
     (zero pads) and X (reflect pads) channel-major over the padded token domain, exactly the
-    torch construction; the K-major GEMM over them (gemm_ps_kernel<0, 64, 0, 1>, tap j = a
+    torch construction, and dY's column sums (the fused bias gradient, rel 1e-5); the K-major GEMM over them (gemm_ps_kernel<0, 64, 0, 1>, tap j = a
     column shift j - P, 2-byte-aligned LDS-DMA sources, split-K fp32 slices) equals the fp32
     reference of the same bf16 values (rel 1e-3: both sum exact bf16 products in fp32).  Shapes:
     decoder / encoder FFN conv1, ragged M / N / K (tile edges, utterance boundaries inside
@@ -518,7 +518,10 @@ def test_wgrad_kmajor_padded_images(cuda, Bn, T, O, Cin, KW, S):
     gy = torch.full((O * Kp + 128,), float("nan"), device=cuda).to(torch.bfloat16)
     gx = torch.zeros(Cin * Kp + 128, device=cuda).to(torch.bfloat16)
     dYT, XT = gy[64:64 + O * Kp], gx[64:64 + Cin * Kp]
-    ops.pad_transpose(G, O, Bn, T, O, P, 0, dYT, Kp, Kp, dt=1)
+    bias = torch.full((O,), 0.25, device=cuda)                # the fused column sum accumulates
+    pws = torch.empty(ops.pad_transpose_ws(Kp, O), device=cuda)
+    ops.pad_transpose(G, O, Bn, T, O, P, 0, dYT, Kp, Kp, dt=1, colsum=bias, ws=pws)
+    assert rel(bias - 0.25, G.float().sum(0)) < 1e-5
     ops.pad_transpose(X, Cin, Bn, T, Cin, P, 1, XT, Kp, Kp, dt=1)
     ipad = torch.arange(-P, T + P, device=cuda)
     rpad = torch.where(ipad < 0, -ipad, ipad)

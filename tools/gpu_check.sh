@@ -21,9 +21,9 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/pro
   > $O/prof_bench.json 2> $O/prof.err || { echo "rocprof failed"; tail -20 $O/prof.err; exit 1; }
 python $R/tools/rocprof_summary.py stats $O/prof 13 $O/kernel_stats.txt | head -40
 python $R/tools/rocprof_summary.py kernel $O/prof "gemm256_kernel<true, true, 1" 377856 100 | tee $O/roofline_kernel_trace.txt
-# second roofline kernel: the decoder FFN conv1 weight gradient (X grid 84 x 512, 3 split-K
-# planes in z; the encoder's runs < 300 us even beside the data gradient)
-python $R/tools/rocprof_summary.py kernel $O/prof "gemm256_kernel<false, false, 0, 1>" 43008 300 | tee $O/wgrad_kernel_trace.txt
+# second roofline kernel: the decoder FFN conv1 weight gradient (conv_mode 6 on the persistent
+# kernel: 84 tiles x 3 splits -> 256 blocks of 512; the encoder's, same grid, runs < 200 us)
+python $R/tools/rocprof_summary.py kernel $O/prof "gemm_ps_kernel<0, 64, 0, 1>" 131072 200 | tee $O/wgrad_kernel_trace.txt
 python $R/tools/rocprof_summary.py gaps $O/prof adamw_prep_tiles 10 $O/gaps.json | tail -3
 if [ "$3" == "pmc" ]; then
   for C in FETCH_SIZE WRITE_SIZE; do
@@ -31,11 +31,18 @@ if [ "$3" == "pmc" ]; then
       > $O/pmc_$C.log 2>&1 || { echo "pmc $C failed"; tail -20 $O/pmc_$C.log; exit 1; }
   done
   python $R/tools/rocprof_summary.py traffic $O/pmc_FETCH_SIZE $O/pmc_WRITE_SIZE "gemm256_kernel<true, true, 1" 377856 100 $O/roofline_traffic.json
-  # (counter-collection Grid_Size is the whole grid: x 43008 times z 3)
-  python $R/tools/rocprof_summary.py traffic $O/pmc_FETCH_SIZE $O/pmc_WRITE_SIZE "gemm256_kernel<false, false, 0, 1>" 129024 300 $O/wgrad_traffic.json
+  python $R/tools/rocprof_summary.py traffic $O/pmc_FETCH_SIZE $O/pmc_WRITE_SIZE "gemm_ps_kernel<0, 64, 0, 1>" 131072 200 $O/wgrad_traffic.json
   python $R/tools/rocprof_summary.py traffic $O/pmc_FETCH_SIZE $O/pmc_WRITE_SIZE "gemm_ps_kernel<4, 48, 0>" 126976 200 $O/ps_dgrad_traffic.json
 fi
 if [ "$4" == "detail" ]; then
   cd $R && timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-extractor --no-fp32-leg --no-config2-leg --detail > $O/detail.json 2> $O/detail.txt || { echo "detail failed"; tail -20 $O/detail.txt; exit 1; }
   grep -v amdgpu.ids $O/detail.txt | head -60
+fi
+if [ "$5" == "serial" ]; then
+  # per-kernel totals with the weight-gradient and predictor streams off (experiments library):
+  # the standalone work of the step, free of the in-step CU contention between streams
+  cd /tmp && FS2_HIP_LIB=$R/fine-grained-emotional-control-of-tts_amd/fastspeech2/libfs2_hip_exp.so FS2_NO_SIDE_STREAM=1 FS2_NO_AUX_STREAM=1 \
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/sprof -o run -- python $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-extractor --no-fp32-leg --no-config2-leg \
+    > $O/sprof_bench.json 2> $O/sprof.err || { echo "serial rocprof failed"; tail -20 $O/sprof.err; exit 1; }
+  python $R/tools/rocprof_summary.py stats $O/sprof 13 $O/serial_kernel_stats.txt | head -45
 fi
