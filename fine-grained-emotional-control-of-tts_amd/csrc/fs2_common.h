@@ -13,6 +13,19 @@ typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
 
 #define FS2_WAVE 64
 
+// FS2_* A/B switches: read from the environment only in the experiments build
+// (make experiments, -DFS2_EXPERIMENTS, used by tools/); the product library compiles every
+// switch to its default.
+#ifdef FS2_EXPERIMENTS
+#include <cstdlib>
+inline int fs2_exp_int(const char* name, int dflt) {
+  const char* v = std::getenv(name);
+  return v && v[0] ? std::atoi(v) : dflt;
+}
+#else
+constexpr int fs2_exp_int(const char*, int dflt) { return dflt; }
+#endif
+
 __device__ __forceinline__ float to_f(float x) { return x; }
 __device__ __forceinline__ float to_f(bf16 x) { return (float)x; }
 template <typename T> __device__ __forceinline__ T from_f(float x);

@@ -165,7 +165,7 @@ __global__ void __launch_bounds__(256) ln_fwd_rows_kernel(LnFwdP p) {
 
 // rows per wave of the bf16 LayerNorm forward (FS2_LN_FWD_ROWS: 1 = ln_fwd_vec_kernel)
 int ln_fwd_rows() {
-  static const int r = [] { const char* v = std::getenv("FS2_LN_FWD_ROWS"); return v && v[0] ? std::atoi(v) : 2; }();
+  static const int r = fs2_exp_int("FS2_LN_FWD_ROWS", 2);
   return r;
 }
 
@@ -770,15 +770,15 @@ __global__ void __launch_bounds__(256) sum_slices_kernel(const float* ws, int ns
 // rows per LayerNorm-backward block (4 waves): 32, or 16 when 32 leaves fewer than 512 blocks
 // (ln_bench, M = 6400: 20.0 -> 16.9 us; M = 31264: 38.5 vs 41.4 us with 16); FS2_LN_RPB forces
 int ln_rpb(int M) {
-  static const int r = [] { const char* v = std::getenv("FS2_LN_RPB"); return v && v[0] ? std::max(4, std::atoi(v)) : 0; }();
-  if (r) return r;
+  static const int r = fs2_exp_int("FS2_LN_RPB", 0);
+  if (r) return std::max(4, r);
   return (M + 31) / 32 >= 512 ? 32 : 16;
 }
 int ln_blocks(int M) { return min(8192, max(1, (M + ln_rpb(M) - 1) / ln_rpb(M))); }
 // rows in flight per wave in the bf16 LayerNorm backward (FS2_LN_ROWS=1 selects the one-row
 // kernel for A/B runs)
 int ln_rows_r() {
-  static const int r = [] { const char* v = std::getenv("FS2_LN_ROWS"); return v ? std::atoi(v) : 4; }();
+  static const int r = fs2_exp_int("FS2_LN_ROWS", 4);
   return r;
 }
 // ---- token-major -> channel-major padded images for the K-major weight gradient (conv_mode 6)
@@ -1010,7 +1010,7 @@ extern "C" int fs2_conv_fold(const float* Xpad, int nsplit, int64_t split_stride
     return FS2_EINVAL;
   const dim3 g((unsigned)((n / 4 + 255) / 256)), b(256);
   hipStream_t s = (hipStream_t)stream;
-  static const bool no8 = [] { const char* v = std::getenv("FS2_FOLD8"); return v && v[0] == '0'; }();
+  static const bool no8 = fs2_exp_int("FS2_FOLD8", 1) == 0;
   const bool v8 = !no8 && dtype == FS2_BF16 && C % 8 == 0 && a16(out) && ldo % 8 == 0 &&
                   (!residual || (a16(residual) && ldr % 8 == 0)) && a16(Xpad) &&
                   (nsplit == 1 || split_stride % 4 == 0) && n / 8 < (1L << 31);

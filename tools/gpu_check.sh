@@ -32,7 +32,7 @@ if [ "$3" == "pmc" ]; then
   done
   python $R/tools/rocprof_summary.py traffic $O/pmc_FETCH_SIZE $O/pmc_WRITE_SIZE "gemm256_kernel<true, true, 1" 377856 100 $O/roofline_traffic.json
   python $R/tools/rocprof_summary.py traffic $O/pmc_FETCH_SIZE $O/pmc_WRITE_SIZE "gemm_ps_kernel<0, 64, 0, 1>" 131072 200 $O/wgrad_traffic.json
-  python $R/tools/rocprof_summary.py traffic $O/pmc_FETCH_SIZE $O/pmc_WRITE_SIZE "gemm_ps_kernel<4, 48, 0>" 126976 200 $O/ps_dgrad_traffic.json
+  python $R/tools/rocprof_summary.py traffic $O/pmc_FETCH_SIZE $O/pmc_WRITE_SIZE "gemm_ps_kernel<4, 48, 0, 0>" 126976 200 $O/ps_dgrad_traffic.json
 fi
 if [ "$4" == "detail" ]; then
   cd $R && timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-extractor --no-fp32-leg --no-config2-leg --detail > $O/detail.json 2> $O/detail.txt || { echo "detail failed"; tail -20 $O/detail.txt; exit 1; }
