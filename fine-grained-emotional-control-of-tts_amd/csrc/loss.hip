@@ -31,11 +31,14 @@ struct LossP {
   float* part_mel;   // [2][B][nch] chunk sums of squared mel / postnet errors
   int nch;
   float* stats;      // [8][B] ymax, ymin, hmax, hmin, cnt_hmax, cnt_hmin, S1, S2
+  float* mm_part;    // [B][MMCH][4] chunk max / min of target and prediction
+  float* cnt_part;   // [B][MMCH][2] chunk tie counts of the prediction's max / min
   float* ssim_part;  // [B][nblk_pix]
   float* dmap;       // [3][B][npix]
   float* dnmap;      // [B][Tm][NM]
   float* scal;       // [4]
   int npix, nblk_pix;
+  int vec;           // every mel operand 16-byte aligned (vectorised MSE pass)
 };
 
 __device__ __forceinline__ float block_sum(float v, float* sh) {
@@ -93,13 +96,34 @@ __global__ void __launch_bounds__(256) mse_kernel(LossP p) {
   const float cm = 2.f * p.w_mel / ((float)L * NM * B), cp = 2.f * p.w_post / ((float)L * NM * B);
   float s_mel = 0.f, s_post = 0.f;
   const int i0 = blockIdx.y * LOSS_CHUNK, i1 = min(Tm * NM, i0 + LOSS_CHUNK);
-  for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
-    const bool valid = (i / NM) < L;
-    const float y = mt[i];
-    const float d1 = to_f(mo[i]) - y, d2 = to_f(po[i]) - y;
-    if (valid) { s_mel += d1 * d1; s_post += d2 * d2; }
-    dmo[i] = from_f<T>(valid ? cm * d1 : 0.f);
-    dpo[i] = from_f<T>(valid ? cp * d2 : 0.f);
+  constexpr int V = Vec<T>::N;   // 16-byte accesses: 8 bf16 / 4 fp32 elements per lane
+  if (p.vec && NM % V == 0) {    // a lane's V elements share one mel frame (one validity test)
+    for (int i = i0 + threadIdx.x * V; i < i1; i += blockDim.x * V) {
+      const bool valid = (i / NM) < L;
+      float y[V], a[V], c[V], g1[V], g2[V];
+#pragma unroll
+      for (int e = 0; e < V; e += 4) vload<float>(y + e, mt + i + e);
+      vload<T>(a, mo + i);
+      vload<T>(c, po + i);
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        const float d1 = a[e] - y[e], d2 = c[e] - y[e];
+        if (valid) { s_mel += d1 * d1; s_post += d2 * d2; }
+        g1[e] = valid ? cm * d1 : 0.f;
+        g2[e] = valid ? cp * d2 : 0.f;
+      }
+      vstore<T>(dmo + i, g1);
+      vstore<T>(dpo + i, g2);
+    }
+  } else {
+    for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+      const bool valid = (i / NM) < L;
+      const float y = mt[i];
+      const float d1 = to_f(mo[i]) - y, d2 = to_f(po[i]) - y;
+      if (valid) { s_mel += d1 * d1; s_post += d2 * d2; }
+      dmo[i] = from_f<T>(valid ? cm * d1 : 0.f);
+      dpo[i] = from_f<T>(valid ? cp * d2 : 0.f);
+    }
   }
   s_mel = block_sum(s_mel, sh);
   s_post = block_sum(s_post, sh);
@@ -142,24 +166,50 @@ __global__ void __launch_bounds__(256) mse_kernel(LossP p) {
 }
 
 // ---- 2: masked min / max of target and prediction -----------------------------------------
+// Two passes over MMCH chunks per utterance (grid MMCH x B; one block per utterance left 224 of
+// the 256 CUs idle: 83 us): chunk extrema, then every chunk block combines the MMCH partials
+// in a fixed order and counts its ties to the prediction's extrema; finalize_kernel sums the
+// tie counts.  Same values as one pass over the utterance (max / min are order-free).
+constexpr int MMCH = 16;
 template <typename T>
-__global__ void __launch_bounds__(256) minmax_kernel(LossP p) {
+__global__ void __launch_bounds__(256) minmax_part_kernel(LossP p) {
   __shared__ float sh[8];
-  const int b = blockIdx.x, Tm = p.Tm, NM = p.NM, B = p.B;
+  const int c = blockIdx.x, b = blockIdx.y, Tm = p.Tm, NM = p.NM;
   const int L = (int)min((int64_t)Tm, p.mel_len[b]);
+  const int n = L * NM, per = (n + MMCH - 1) / MMCH;
+  const int i0 = c * per, i1 = min(n, i0 + per);
   const T* h = (const T*)p.mel_out + (long)b * Tm * NM;
   const float* y = p.mel_tgt + (long)b * Tm * NM;
   float ymx = -INFINITY, ymn = INFINITY, hmx = -INFINITY, hmn = INFINITY;
-  for (int i = threadIdx.x; i < L * NM; i += blockDim.x) {
+  for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
     const float yv = y[i], hv = to_f(h[i]);
     ymx = fmaxf(ymx, yv); ymn = fminf(ymn, yv); hmx = fmaxf(hmx, hv); hmn = fminf(hmn, hv);
   }
   ymx = block_max(ymx, sh); ymn = block_min(ymn, sh);
   hmx = block_max(hmx, sh); hmn = block_min(hmn, sh);
+  if (threadIdx.x == 0) {
+    float* o = p.mm_part + ((long)b * MMCH + c) * 4;
+    o[0] = ymx; o[1] = ymn; o[2] = hmx; o[3] = hmn;
+  }
+}
+template <typename T>
+__global__ void __launch_bounds__(256) minmax_count_kernel(LossP p) {
+  __shared__ float sh[8];
+  const int c = blockIdx.x, b = blockIdx.y, Tm = p.Tm, NM = p.NM, B = p.B;
+  const int L = (int)min((int64_t)Tm, p.mel_len[b]);
+  const float* q = p.mm_part + (long)b * MMCH * 4;
+  float ymx = -INFINITY, ymn = INFINITY, hmx = -INFINITY, hmn = INFINITY;
+  for (int k = 0; k < MMCH; ++k) {
+    ymx = fmaxf(ymx, q[4 * k]); ymn = fminf(ymn, q[4 * k + 1]);
+    hmx = fmaxf(hmx, q[4 * k + 2]); hmn = fminf(hmn, q[4 * k + 3]);
+  }
   const bool has_pad = L < Tm;  // masked_fill(~mask, 0) contributes zeros to the max
   if (has_pad) { ymx = fmaxf(ymx, 0.f); hmx = fmaxf(hmx, 0.f); }
+  const int n = L * NM, per = (n + MMCH - 1) / MMCH;
+  const int i0 = c * per, i1 = min(n, i0 + per);
+  const T* h = (const T*)p.mel_out + (long)b * Tm * NM;
   float cmx = 0.f, cmn = 0.f;
-  for (int i = threadIdx.x; i < L * NM; i += blockDim.x) {
+  for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
     const float hv = to_f(h[i]);
     cmx += (hv == hmx) ? 1.f : 0.f;
     cmn += (hv == hmn) ? 1.f : 0.f;
@@ -167,23 +217,49 @@ __global__ void __launch_bounds__(256) minmax_kernel(LossP p) {
   cmx = block_sum(cmx, sh);
   cmn = block_sum(cmn, sh);
   if (threadIdx.x == 0) {
-    if (has_pad && hmx == 0.f) cmx += (float)(Tm - L) * NM;
-    float* st = p.stats;
-    st[0 * B + b] = ymx; st[1 * B + b] = ymn; st[2 * B + b] = hmx; st[3 * B + b] = hmn;
-    st[4 * B + b] = cmx; st[5 * B + b] = cmn; st[6 * B + b] = 0.f; st[7 * B + b] = 0.f;
+    float* o = p.cnt_part + ((long)b * MMCH + c) * 2;
+    o[0] = cmx; o[1] = cmn;
+    if (c == 0) {
+      float* st = p.stats;
+      st[0 * B + b] = ymx; st[1 * B + b] = ymn; st[2 * B + b] = hmx; st[3 * B + b] = hmn;
+      st[6 * B + b] = 0.f; st[7 * B + b] = 0.f;
+    }
   }
 }
 
+// per-utterance min-max normalisation constants, read once per block
+struct NormC {
+  int L;
+  float ymn, yden, hmn, hden;
+  __device__ NormC(const LossP& p, int b) {
+    L = (int)min((int64_t)p.Tm, p.mel_len[b]);
+    const float* st = p.stats;
+    const int B = p.B;
+    ymn = st[1 * B + b]; yden = st[0 * B + b] - ymn + 1e-8f;
+    hmn = st[3 * B + b]; hden = st[2 * B + b] - hmn + 1e-8f;
+  }
+};
 template <typename T>
-__device__ __forceinline__ void norm_xy(const LossP& p, int b, int t, int f, float& X, float& Y) {
-  const int L = (int)min((int64_t)p.Tm, p.mel_len[b]);
-  if (t >= L) { X = 0.f; Y = 0.f; return; }
+__device__ __forceinline__ void norm_xy(const LossP& p, const NormC& nc, int b, int t, int f,
+                                        float& X, float& Y) {
+  if (t >= nc.L) { X = 0.f; Y = 0.f; return; }
   const long i = ((long)b * p.Tm + t) * p.NM + f;
-  const float* st = p.stats;
-  const int B = p.B;
-  X = (p.mel_tgt[i] - st[1 * B + b]) / (st[0 * B + b] - st[1 * B + b] + 1e-8f);
-  Y = (to_f(((const T*)p.mel_out)[i]) - st[3 * B + b]) / (st[2 * B + b] - st[3 * B + b] + 1e-8f);
+  X = (p.mel_tgt[i] - nc.ymn) / nc.yden;
+  Y = (to_f(((const T*)p.mel_out)[i]) - nc.hmn) / nc.hden;
 }
+
+// (row, column) walk of a rows x W index space by 256 threads without a division per element
+struct Walk {
+  int r, c, dr, dc, W;
+  __device__ Walk(int W_) : W(W_) {
+    r = (int)threadIdx.x / W; c = (int)threadIdx.x - r * W;
+    dr = 256 / W; dc = 256 - dr * W;
+  }
+  __device__ __forceinline__ void next() {
+    c += dc; r += dr;
+    if (c >= W) { c -= W; ++r; }
+  }
+};
 
 // ---- 3: SSIM map and its partial derivatives wrt the prediction's local statistics --------
 // Separable Gaussian: a block takes SSIM_TI output rows of one utterance, stages the
@@ -201,16 +277,17 @@ __global__ void __launch_bounds__(256) ssim_map_kernel(LossP p) {
   if (threadIdx.x < WIN) w1[threadIdx.x] = gauss1(threadIdx.x);
   const int b = blockIdx.y, i0 = blockIdx.x * SSIM_TI;
   const int NM = p.NM, OW = NM - (WIN - 1), OH = p.Tm - (WIN - 1);
-  for (int idx = threadIdx.x; idx < SSIM_R * NM; idx += blockDim.x) {
-    const int r = idx / NM, f = idx - r * NM, t = i0 + r;
+  const NormC nc(p, b);
+  for (Walk w(NM); w.r < SSIM_R; w.next()) {
+    const int r = w.r, f = w.c, t = i0 + r;
     float X = 0.f, Y = 0.f;
-    if (t < p.Tm) norm_xy<T>(p, b, t, f, X, Y);
+    if (t < p.Tm) norm_xy<T>(p, nc, b, t, f, X, Y);
     xs[r][f] = X;
     ys[r][f] = Y;
   }
   __syncthreads();
-  for (int idx = threadIdx.x; idx < SSIM_R * OW; idx += blockDim.x) {
-    const int r = idx / OW, j = idx - r * OW;
+  for (Walk wk(OW); wk.r < SSIM_R; wk.next()) {
+    const int r = wk.r, j = wk.c;
     float mx = 0.f, my = 0.f, exx = 0.f, eyy = 0.f, exy = 0.f;
 #pragma unroll
     for (int dj = 0; dj < WIN; ++dj) {
@@ -222,8 +299,8 @@ __global__ void __launch_bounds__(256) ssim_map_kernel(LossP p) {
   __syncthreads();
   float ss = 0.f;
   const long plane = (long)p.B * p.npix;
-  for (int idx = threadIdx.x; idx < SSIM_TI * OW; idx += blockDim.x) {
-    const int ti = idx / OW, j = idx - ti * OW, i = i0 + ti;
+  for (Walk wk(OW); wk.r < SSIM_TI; wk.next()) {
+    const int ti = wk.r, j = wk.c, i = i0 + ti;
     if (i >= OH) continue;
     float a = 0.f, bb = 0.f, exx = 0.f, eyy = 0.f, exy = 0.f;
 #pragma unroll
@@ -273,20 +350,28 @@ __global__ void __launch_bounds__(256) finalize_kernel(LossP p) {
     }
     p.per_b[0 * B + b] = sm / ((float)L * p.NM);
     p.per_b[1 * B + b] = sp / ((float)L * p.NM);
+    float cmx = 0.f, cmn = 0.f;   // tie counts of the prediction's extrema, fixed order
+    for (int c = 0; c < MMCH; ++c) {
+      cmx += p.cnt_part[((long)b * MMCH + c) * 2];
+      cmn += p.cnt_part[((long)b * MMCH + c) * 2 + 1];
+    }
+    if (L < p.Tm && p.stats[2 * B + b] == 0.f) cmx += (float)(p.Tm - L) * p.NM;   // zero pads
+    p.stats[4 * B + b] = cmx;
+    p.stats[5 * B + b] = cmn;
   }
   __syncthreads();
+  // utterance means of the five terms: fixed-order block sums (B <= 256) instead of a serial
+  // thread-0 loop of 5 B dependent loads
+  __shared__ float fsh[8];
+  float t[5];
+  for (int k = 0; k < 5; ++k)
+    t[k] = block_sum(threadIdx.x < B ? p.per_b[k * B + threadIdx.x] : 0.f, fsh) / (float)B;
   if (threadIdx.x != 0) return;
   const float ssim_val = (float)(tot / ((double)B * p.npix));
   float l_ssim = 1.f - ssim_val;
   float gate = 1.f;
   if (l_ssim > 1.f) { l_ssim = 1.f; gate = 0.f; }
   if (l_ssim < 0.f) { l_ssim = 0.f; gate = 0.f; }
-  float t[5];
-  for (int k = 0; k < 5; ++k) {
-    float s = 0.f;
-    for (int b = 0; b < B; ++b) s += p.per_b[k * B + b];
-    t[k] = s / (float)B;
-  }
   const float ssim_w = l_ssim * p.w_ssim, mel_w = t[0] * p.w_mel, post_w = t[1] * p.w_post;
   const float dur_w = t[2] * p.w_dur, pi_w = t[3] * p.w_pitch, en_w = t[4] * p.w_energy;
   p.loss_out[0] = ssim_w + mel_w + post_w + dur_w + pi_w + en_w;
@@ -312,8 +397,8 @@ __global__ void __launch_bounds__(256) ssim_grad_kernel(LossP p) {
   const int OH = Tm - (WIN - 1), OW = NM - (WIN - 1);
   const long plane = (long)B * p.npix;
   const float* Db = p.dmap + (long)b * p.npix;
-  for (int idx = threadIdx.x; idx < SSIM_R * OW; idx += blockDim.x) {
-    const int r = idx / OW, j = idx - r * OW, i = t0 - (WIN - 1) + r;
+  for (Walk wk(OW); wk.r < SSIM_R; wk.next()) {
+    const int r = wk.r, j = wk.c, i = t0 - (WIN - 1) + r;
     const bool ok = i >= 0 && i < OH;
     const long o = (long)i * OW + j;
     dsm[0][r][j] = ok ? Db[o] : 0.f;
@@ -321,8 +406,8 @@ __global__ void __launch_bounds__(256) ssim_grad_kernel(LossP p) {
     dsm[2][r][j] = ok ? Db[2 * plane + o] : 0.f;
   }
   __syncthreads();
-  for (int idx = threadIdx.x; idx < SSIM_R * NM; idx += blockDim.x) {
-    const int r = idx / NM, f = idx - r * NM;
+  for (Walk wk(NM); wk.r < SSIM_R; wk.next()) {
+    const int r = wk.r, f = wk.c;
     float u = 0.f, v = 0.f, w = 0.f;
 #pragma unroll
     for (int dj = 0; dj < WIN; ++dj) {
@@ -335,10 +420,11 @@ __global__ void __launch_bounds__(256) ssim_grad_kernel(LossP p) {
   }
   __syncthreads();
   const float g = p.scal[0];
-  const int L = (int)min((int64_t)Tm, p.mel_len[b]);
+  const NormC nc(p, b);
+  const int L = nc.L;
   float s1 = 0.f, s2 = 0.f;
-  for (int idx = threadIdx.x; idx < SSIM_TI * NM; idx += blockDim.x) {
-    const int tt = idx / NM, f = idx - tt * NM, t = t0 + tt;
+  for (Walk wk(NM); wk.r < SSIM_TI; wk.next()) {
+    const int tt = wk.r, f = wk.c, t = t0 + tt;
     if (t >= Tm) continue;
     float U = 0.f, V = 0.f, W = 0.f;
 #pragma unroll
@@ -348,7 +434,7 @@ __global__ void __launch_bounds__(256) ssim_grad_kernel(LossP p) {
       U += w * hsm[0][r][f]; V += w * hsm[1][r][f]; W += w * hsm[2][r][f];
     }
     float X, Y;
-    norm_xy<T>(p, b, t, f, X, Y);
+    norm_xy<T>(p, nc, b, t, f, X, Y);
     float dn = 0.f;
     if (t < L) dn = g * (U + 2.f * Y * V + X * W);
     const long q = (long)t * NM + f;
@@ -356,7 +442,7 @@ __global__ void __launch_bounds__(256) ssim_grad_kernel(LossP p) {
     if (t < L) {
       const float hv = to_f(((const T*)p.mel_out)[(long)b * Tm * NM + q]);
       s1 += dn;
-      s2 += dn * (hv - p.stats[3 * B + b]);
+      s2 += dn * (hv - nc.hmn);
     }
   }
   s1 = block_sum(s1, sh);
@@ -396,7 +482,8 @@ __global__ void ssim_apply_kernel(LossP p) {
 template <typename T>
 int run_loss(LossP& p, hipStream_t s) {
   hipLaunchKernelGGL(mse_kernel<T>, dim3(p.B, p.nch), dim3(256), 0, s, p);
-  hipLaunchKernelGGL(minmax_kernel<T>, dim3(p.B), dim3(256), 0, s, p);
+  hipLaunchKernelGGL(minmax_part_kernel<T>, dim3(MMCH, p.B), dim3(256), 0, s, p);
+  hipLaunchKernelGGL(minmax_count_kernel<T>, dim3(MMCH, p.B), dim3(256), 0, s, p);
   hipLaunchKernelGGL(ssim_map_kernel<T>, dim3(p.nblk_pix, p.B), dim3(256), 0, s, p);
   hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(256), 0, s, p);
   const unsigned nq = (unsigned)(((long)p.Tm * p.NM + 255) / 256);
@@ -416,6 +503,8 @@ void carve(LossP& p, float* ws) {
   p.per_b = w; w += 5L * B;
   p.part_mel = w; w += 2L * B * p.nch;
   p.stats = w; w += 8L * B;
+  p.mm_part = w; w += 4L * B * MMCH;
+  p.cnt_part = w; w += 2L * B * MMCH;
   p.scal = w; w += 4;
   p.ssim_part = w; w += (long)B * p.nblk_pix;
   w = (float*)(((uintptr_t)w + 15) & ~(uintptr_t)15);
@@ -429,7 +518,8 @@ extern "C" int64_t fs2_loss_workspace_floats(int B, int Tm, int NM) {
   const long npix = (long)(Tm - (WIN - 1)) * (NM - (WIN - 1));
   const long nblk = (Tm - (WIN - 1) + SSIM_TI - 1) / SSIM_TI;
   const long nch = ((long)Tm * NM + LOSS_CHUNK - 1) / LOSS_CHUNK;
-  return 5L * B + 2L * B * nch + 8L * B + 4 + B * nblk + 4 + 3L * B * npix + (long)B * Tm * NM;
+  return 5L * B + 2L * B * nch + 8L * B + 6L * B * MMCH + 4 + B * nblk + 4 + 3L * B * npix +
+         (long)B * Tm * NM;
 }
 
 extern "C" int fs2_loss_fwd_bwd(const fs2_loss_desc* d, void* stream) {
@@ -437,6 +527,7 @@ extern "C" int fs2_loss_fwd_bwd(const fs2_loss_desc* d, void* stream) {
   if (d->B <= 0) return 0;
   if (d->Tm < WIN || d->NM < WIN) return FS2_EINVAL;  // SSIM: kernel larger than input
   if (d->NM > SSIM_MAXW) return FS2_EINVAL;           // SSIM LDS tiles
+  if (d->B > 256) return FS2_EINVAL;                  // finalize_kernel: one thread per utterance
   if (!d->mel_out || !d->postnet_out || !d->log_dur || !d->pitch_pred || !d->energy_pred ||
       !d->mel_tgt || !d->dur_tgt || !d->pitch_avg || !d->energy_avg || !d->mel_len ||
       !d->phon_len || !d->loss_out || !d->d_mel_out || !d->d_postnet_out || !d->d_log_dur ||
@@ -453,6 +544,10 @@ extern "C" int fs2_loss_fwd_bwd(const fs2_loss_desc* d, void* stream) {
   p.loss_out = d->loss_out; p.d_mel = d->d_mel_out; p.d_post = d->d_postnet_out;
   p.d_dur = d->d_log_dur; p.d_pitch = d->d_pitch; p.d_energy = d->d_energy;
   carve(p, d->workspace);
+  {
+    const auto al = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
+    p.vec = al(p.mel_out) && al(p.post_out) && al(p.mel_tgt) && al(p.d_mel) && al(p.d_post);
+  }
   hipStream_t s = (hipStream_t)stream;
   if (d->dtype == FS2_BF16) return run_loss<bf16>(p, s);
   if (d->dtype == FS2_F32) return run_loss<float>(p, s);

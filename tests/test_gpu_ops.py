@@ -292,15 +292,19 @@ def test_avg_over_durations_bit_exact(cuda, golden_dir):
     np.testing.assert_array_equal(out.cpu().numpy(), g["avg"])
 
 
-@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
-def test_fused_loss_vs_oracle(cuda, dt):
+@pytest.mark.parametrize("dt,B,Tp,ties", [(torch.float32, 3, 20, False), (torch.bfloat16, 3, 20, False),
+                                          (torch.float32, 4, 60, True), (torch.bfloat16, 4, 60, True)])
+def test_fused_loss_vs_oracle(cuda, dt, B, Tp, ties):
+    """fs2_loss_fwd_bwd vs LossOracle (loss.py:101-186).  ``ties``: predictions clamped so
+    their max / min repeat many times across the min-max kernels' 16 chunks per utterance --
+    the SSIM normalisation gradient is split over every tie (torch amax / amin semantics)."""
     from fastspeech2.loss import fused_loss
     from oracle.fs2_oracle import LossOracle
-    torch.manual_seed(4)
-    B, Tp, NM = 3, 20, 80
+    torch.manual_seed(4 + Tp)
+    NM = 80
     d = torch.randint(1, 6, (B, Tp))
-    d[1, 15:] = 0
-    d[2, 9:] = 0
+    d[1, Tp * 3 // 4:] = 0
+    d[2, Tp // 2 - 1:] = 0
     mel_len = d.sum(1)
     Tm = int(mel_len.max())
     phon_len = (d > 0).sum(1)
@@ -308,6 +312,8 @@ def test_fused_loss_vs_oracle(cuda, dt):
     for b in range(B):
         tgt[b, mel_len[b]:] = 0
     mel = (torch.randn(B, Tm, NM) * 2 - 4)
+    if ties:
+        mel = mel.clamp(-6.0, -2.5)
     post = mel + 0.1 * torch.randn(B, Tm, NM)
     for b in range(B):
         mel[b, mel_len[b]:] = 0
