@@ -325,6 +325,15 @@ __device__ __forceinline__ void glds_mnmajor(char* lds, const char* base, long l
   }
 }
 
+// ---- fp32 C staging in LDS (cs[row][col ^ cs_swz(row)], 128 floats per row) ----------------
+// An accumulator fragment is written with lanes on 16 rows x 2 column quads per 32-lane half;
+// rows are 512 B apart, so only the swizzle separates their banks.  XOR-ing the column by 4x
+// (row & 15) spreads them over all 16 quads of banks (2-way, the minimum for 32 lanes whose
+// column is fixed mod 4; the old (row >> 2 & 1) << 4 left 8-way: 22 % of the 256 x 128
+// weight-gradient kernel's LDS cycles were conflicts, profiles/r03s2_gemm_lds_pmc.json), and
+// keeps every aligned 4-float group contiguous for the 16-byte epilogue reads.
+__device__ __forceinline__ int cs_swz(int row) { return (row & 15) << 2; }
+
 // ---- fragment readers -------------------------------------------------------------------
 typedef __attribute__((ext_vector_type(4))) short s16x4;
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
@@ -583,7 +592,7 @@ __global__ void __launch_bounds__(NT) gemm_kernel(GemmP p) {
       for (int r = 0; r < 4; ++r) {
         const int row = wm * 64 + i * 16 + (lane >> 4) * 4 + r;
         const int col = wn * 64 + j * 16 + (lane & 15);
-        cs[row * 128 + (col ^ (((row >> 2) & 1) << 4))] = acc[i][j][r];
+        cs[row * 128 + (col ^ cs_swz(row))] = acc[i][j][r];
       }
   __syncthreads();
   const int c8 = (tid & 15) * 8;
@@ -593,7 +602,7 @@ __global__ void __launch_bounds__(NT) gemm_kernel(GemmP p) {
     const int row = (tid >> 4) + 16 * pass;
     const int m = m0 + row;
     if (m >= p.mvalid || n >= p.nvalid) continue;
-    const int sw = ((row >> 2) & 1) << 4;
+    const int sw = cs_swz(row);
     const f32x4 lo = *(const f32x4*)&cs[row * 128 + (c8 ^ sw)];
     const f32x4 hi = *(const f32x4*)&cs[row * 128 + ((c8 + 4) ^ sw)];
     float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
@@ -753,7 +762,7 @@ __device__ __forceinline__ void epilogue_256x128(const GemmP& p, const float* cs
       const int row = idx >> 7, col = idx & 127;
       const int m = m0 + row, n = n0 + col;
       if (m >= p.mvalid || n >= p.nvalid) continue;
-      float v = cs[row * 128 + (col ^ (((row >> 2) & 1) << 4))];
+      float v = cs[row * 128 + (col ^ cs_swz(row))];
       long c2 = n;
       if (cc > 0) { const int jj = n / cc; c2 = (long)(n - jj * cc) * p.c_conv_kw + jj; }
       const long off = (long)m * p.ldc + c2;
@@ -770,7 +779,7 @@ __device__ __forceinline__ void epilogue_256x128(const GemmP& p, const float* cs
     const int row = (tid >> 4) + 32 * pass;
     const int m = m0 + row;
     if (m >= p.mvalid || n >= p.nvalid) continue;
-    const int sw = ((row >> 2) & 1) << 4;
+    const int sw = cs_swz(row);
     const f32x4 lo = *(const f32x4*)&cs[row * 128 + (c8 ^ sw)];
     const f32x4 hi = *(const f32x4*)&cs[row * 128 + ((c8 + 4) ^ sw)];
     float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
@@ -1065,7 +1074,7 @@ __global__ void __launch_bounds__(BNT) gemm_big_kernel(GemmP p) {
       for (int r = 0; r < 4; ++r) {
         const int row = wm * 64 + i * 16 + (lane & 15);
         const int col = wn * 64 + j * 16 + (lane >> 4) * 4 + r;
-        cs[row * 128 + (col ^ (((row >> 2) & 1) << 4))] = acc[i][j][r];
+        cs[row * 128 + (col ^ cs_swz(row))] = acc[i][j][r];
       }
   __syncthreads();
   epilogue_256x128(p, cs, m0, n0, Cb, Rb, tid);
@@ -1409,7 +1418,7 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256_kernel(GemmP p) {
           for (int r = 0; r < 4; ++r) {
             const int row = wr * 128 + i * 16 + (lane >> 4) * 4 + r;
             const int col = (wc & 1) * 64 + j * 16 + (lane & 15);
-            cs[row * 128 + (col ^ (((row >> 2) & 1) << 4))] = acc[i][j][r];
+            cs[row * 128 + (col ^ cs_swz(row))] = acc[i][j][r];
           }
     }
     __syncthreads();
