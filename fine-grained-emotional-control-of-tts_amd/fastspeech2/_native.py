@@ -121,7 +121,8 @@ SIGNATURES = {
     "fs2_softmax_fwd": (I, [P, P, I, I, I, I, I, I, Fl, Fl, U32, U32, P, P, I, P]),
     "fs2_softmax_bwd": (I, [P, P, I, I, I, I, I, Fl, Fl, U32, U32, P, I, P]),
     "fs2_embed_fwd": (I, [P, P, P, I, I, I, I, P, P, I, P]),
-    "fs2_embed_bwd": (I, [P, P, P, I, I, I, P, I, P]),
+    "fs2_embed_bwd": (I, [P, P, P, I, I, I, P, P, I, P]),
+    "fs2_embed_bwd_workspace_floats": (I64, [I, I]),
     "fs2_keypad_from_tokens": (I, [P, I, I, P, P]),
     "fs2_keypad_from_lengths": (I, [P, I, I, P, P, P]),
     "fs2_concat_fwd": (I, [P, P, P, P, I, I, I, I, P, I, I, P]),

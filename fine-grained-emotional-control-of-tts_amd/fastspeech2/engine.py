@@ -994,6 +994,7 @@ class FS2Engine:
                                ctx["p_enc"], seed)
             notify(f"encoder.layers.{i}")
         ops.embed_bwd(ctx["tokens"], dX, keep_p, Mp, D, c.n_char,
-                      G["encPreNet.token_embedding.Embedding.weight"], dt=self.dt)
+                      G["encPreNet.token_embedding.Embedding.weight"], dt=self.dt,
+                      ws=self.ws(ops.embed_bwd_ws(D, c.n_char)))
         self.side_join()
         notify("prenet")

@@ -149,9 +149,13 @@ def embed_fwd(tokens, table, pe, pad_idx, B, T, D, X, keep, *, dt):
                                dt, _s()), "fs2_embed_fwd")
 
 
-def embed_bwd(tokens, dX, keep, M, D, V, dtable, *, dt):
-    _chk(N.lib().fs2_embed_bwd(_p(tokens), _p(dX), _p(keep), M, D, V, _p(dtable), dt, _s()),
-         "fs2_embed_bwd")
+def embed_bwd(tokens, dX, keep, M, D, V, dtable, *, dt, ws):
+    _chk(N.lib().fs2_embed_bwd(_p(tokens), _p(dX), _p(keep), M, D, V, _p(dtable), _p(ws), dt,
+                               _s()), "fs2_embed_bwd")
+
+
+def embed_bwd_ws(D, V):
+    return N.lib().fs2_embed_bwd_workspace_floats(D, V)
 
 
 def keypad_from_tokens(tokens, pad_idx, M, key_pad):

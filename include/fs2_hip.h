@@ -180,9 +180,12 @@ int64_t fs2_attn_workspace_floats(int B, int H, int T);
  * ------------------------------------------------------------------------------------------ */
 int fs2_embed_fwd(const int64_t* tokens, const float* table, const float* pe, int pad_idx,
                   int B, int T, int D, void* X, float* keep, int dtype, void* stream);
-/* dTable[v] (+)= sum_{m: tok[m]==v} dX[m] * keep[m]   (deterministic, one block per row)   */
+/* dTable[v] (+)= sum_{m: tok[m]==v} dX[m] * keep[m]   (deterministic: token-chunk partials in
+ * per-wave LDS accumulators, summed in a fixed order); V <= 128;
+ * workspace >= fs2_embed_bwd_workspace_floats(D, V) floats                                 */
 int fs2_embed_bwd(const int64_t* tokens, const void* dX, const float* keep, int M, int D,
-                  int V, float* dtable, int dtype, void* stream);
+                  int V, float* dtable, float* workspace, int dtype, void* stream);
+int64_t fs2_embed_bwd_workspace_floats(int D, int V);
 
 /* key padding masks: from tokens (tok==pad) or from lengths (t >= len)                    */
 int fs2_keypad_from_tokens(const int64_t* tokens, int pad_idx, int M, uint8_t* key_pad,

@@ -830,3 +830,55 @@ def test_weight_prep_batched_layouts(cuda):
     for Wf, Wb, rf, rb in refs:
         assert torch.equal(Wf, rf)
         assert torch.equal(Wb, rb)
+
+
+@pytest.mark.parametrize("dt,code", [(torch.float32, 0), (torch.bfloat16, 1)])
+@pytest.mark.parametrize("B,T,V", [(32, 200, 95), (3, 37, 128), (1, 5, 7)])
+def test_embedding_fwd_bwd(cuda, dt, code, B, T, V):
+    """fs2_embed_fwd (table row + positional encoding, pad rows zero) and fs2_embed_bwd (token
+    rows scatter-added into the table gradient through per-wave LDS accumulators, fixed-order
+    combine) against torch: forward exact up to the output rounding, backward rel 1e-5 (fp32
+    sums of the same values in another order).  Bench shape (B*T_p = 6400, V = 95 = n_char),
+    a ragged one with V at the kernel's limit, a tiny one; pad tokens (id 0) are masked."""
+    from fastspeech2 import ops
+    torch.manual_seed(B * T + V)
+    D = 384
+    M = B * T
+    tok = torch.randint(0, V, (B, T), device=cuda)
+    tok[:, T - T // 4:] = 0
+    table = torch.randn(V, D, device=cuda)
+    pe = torch.randn(T, D, device=cuda)
+    X = torch.empty(M, D, device=cuda, dtype=dt)
+    keep = torch.empty(M, device=cuda)
+    ops.embed_fwd(tok, table, pe, 0, B, T, D, X, keep, dt=code)
+    k_ref = (tok.reshape(-1) != 0).float()
+    ref = (table[tok.reshape(-1)] + pe.repeat(B, 1)) * k_ref[:, None]
+    assert torch.equal(keep, k_ref)
+    assert rel(X, ref.to(dt)) < (1e-6 if dt == torch.float32 else 1e-2)
+    dX = torch.randn(M, D, device=cuda).to(dt)
+    dtab = torch.full((V, D), 0.5, device=cuda)
+    ws = torch.empty(ops.embed_bwd_ws(D, V), device=cuda)
+    ops.embed_bwd(tok.reshape(-1), dX, keep, M, D, V, dtab, dt=code, ws=ws)
+    g = torch.zeros(V, D, device=cuda).index_add_(0, tok.reshape(-1), dX.float() * keep[:, None])
+    assert rel(dtab - 0.5, g) < 1e-5
+
+
+@pytest.mark.parametrize("dt,code", [(torch.float32, 0), (torch.bfloat16, 1)])
+@pytest.mark.parametrize("M,D,ldu", [(6400, 384, 384), (999, 256, 264)])
+def test_rowdot_bwd(cuda, dt, code, M, D, ldu):
+    """fs2_rowdot_bwd (the variance predictors' 384 -> 1 head): du = dy * scale * w per row,
+    dw / db = fixed-order column partials; against torch fp32 on the same values."""
+    from fastspeech2 import ops
+    torch.manual_seed(M + D)
+    u = torch.randn(M, ldu, device=cuda).to(dt)
+    dy = torch.randn(M, device=cuda).to(dt)
+    w = torch.randn(D, device=cuda)
+    scale = 0.7
+    du = torch.empty(M, D, device=cuda, dtype=dt)
+    dw, db = torch.zeros(D, device=cuda), torch.zeros(1, device=cuda)
+    ws = torch.empty(256 * (D + 1), device=cuda)
+    ops.rowdot_bwd(dy, u, ldu, w, scale, M, D, du, dw, db, dt=code, ws=ws)
+    g = dy.float() * scale
+    assert rel(du, (g[:, None] * w[None, :]).to(dt)) < (1e-6 if dt == torch.float32 else 1e-2)
+    assert rel(dw, (g[:, None] * u[:, :D].float()).sum(0)) < 1e-5
+    assert abs(db.item() - g.sum().item()) <= 1e-4 * max(1.0, abs(g.sum().item()))
