@@ -200,8 +200,16 @@ def ptr(t):
     return t.data_ptr()
 
 
+_raw_stream = torch._C._cuda_getCurrentRawStream
+_cur_dev = torch._C._cuda_getDevice
+
+
 def stream_ptr():
-    return torch.cuda.current_stream().cuda_stream
+    """torch's current HIP stream on the current device, as a raw pointer.  (The C accessors:
+    torch.cuda.current_stream() builds a Stream object and re-checks lazy init and the device
+    index on every call -- ~5 us, 700+ times a step, which was a quarter of the host's
+    enqueue time.)"""
+    return _raw_stream(_cur_dev())
 
 
 def check(rc, name):

@@ -143,7 +143,7 @@ class FS2Engine:
     def ws(self, n):
         """scratch buffer of the CURRENT stream (the weight-gradient side stream has its own)"""
         n = int(n)
-        key = torch.cuda.current_stream(self.dev).cuda_stream
+        key = N.stream_ptr()
         buf = self._ws if key == self._ws_key else self._ws_other.get(key)
         if buf is None or buf.numel() < n:
             buf = torch.empty(max(int(n * 1.25) + 1024, 1 << 20), dtype=torch.float32,

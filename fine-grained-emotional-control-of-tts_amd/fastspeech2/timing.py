@@ -5,12 +5,19 @@ records with a system-scope release, i.e. an L2 write-back and invalidate betwee
 kernels it separates, which measured ~6 us of idle GPU on each side of every bracketed launch
 (24 brackets per bench step ~ 0.3 ms).  Timing-only events need no such fence
 (hip_runtime_api.h: "can be used for events that are only being used to measure timing").
-FS2_TIMER_EVENTS=torch restores torch.cuda.Event for A/B runs."""
+FS2_TIMER_EVENTS=torch restores torch.cuda.Event for A/B runs.
+
+Events are pooled: creating a HIP event costs far more host time than recording one (the
+bench's 40 brackets a step added ~4.6 ms of host enqueue time when each record created its
+event), so ``reserve(n)`` creates them before a timed region and ``reset()`` returns recorded
+events to the pool once their times have been read."""
 
 import ctypes
 import os
 
 import torch
+
+from . import _native as N
 
 _HIP_EVENT_DISABLE_SYSTEM_FENCE = 0x20000000
 _hip = None
@@ -40,8 +47,8 @@ class _NoFenceEvent:
             raise RuntimeError("hipEventCreateWithFlags failed")
         self.h = h
 
-    def record(self, stream):
-        if _lib().hipEventRecord(self.h, ctypes.c_void_p(stream.cuda_stream)):
+    def record(self, stream_ptr):
+        if _lib().hipEventRecord(self.h, ctypes.c_void_p(stream_ptr)):
             raise RuntimeError("hipEventRecord failed")
 
     def elapsed_time(self, end):
@@ -59,24 +66,45 @@ class KernelTimer:
     def __init__(self):
         self.pending = {}
         self.pairs = {}
+        self.free = []
         self.torch_events = os.environ.get("FS2_TIMER_EVENTS", "nofence") == "torch"
 
     def _event(self):
+        return self.free.pop() if self.free else self._event_new()
+
+    def _record(self, e):
         if self.torch_events:
-            return torch.cuda.Event(enable_timing=True)
-        return _NoFenceEvent()
+            e.record(torch.cuda.current_stream())
+        else:
+            e.record(N.stream_ptr())
 
     def start(self, tag):
         e = self._event()
-        e.record(torch.cuda.current_stream())
+        self._record(e)
         self.pending[tag] = e
 
     def stop(self, tag):
         e = self._event()
-        e.record(torch.cuda.current_stream())
+        self._record(e)
         self.pairs.setdefault(tag, []).append((self.pending.pop(tag), e))
 
+    def n_events(self):
+        return 2 * sum(len(p) for p in self.pairs.values()) + len(self.pending)
+
+    def reserve(self, n):
+        """create events until n are pooled (outside a timed region)"""
+        while len(self.free) < n:
+            self.free.append(self._event_new())
+
+    def _event_new(self):
+        return torch.cuda.Event(enable_timing=True) if self.torch_events else _NoFenceEvent()
+
     def reset(self):
+        """drop the recorded pairs (after their times were read); their events are reused"""
+        for prs in self.pairs.values():
+            for a, b in prs:
+                self.free += (a, b)
+        self.free += list(self.pending.values())
         self.pending, self.pairs = {}, {}
 
     def summary(self):
