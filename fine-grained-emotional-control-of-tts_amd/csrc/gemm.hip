@@ -72,6 +72,7 @@ struct GemmP {
   int tiles_m, tiles_n;
   int vec_ok;
   int vec_align;  // vector epilogue possible if K were not split
+  int c_row_t, c_row_pad;  // >0: output row m stored at m + (m / c_row_t) * c_row_pad (ps kernel)
 };
 
 __device__ __forceinline__ u32x4 add_bf16x8(u32x4 a, u32x4 b) {
@@ -2069,8 +2070,10 @@ __global__ void __launch_bounds__(BNT, 1) gemm_ps_kernel(GemmP p) {
         };
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-          const int m = mb + 16 * i + li;
-          const bool rowok = m < p.mvalid;
+          const int m0 = mb + 16 * i + li;
+          const bool rowok = m0 < p.mvalid;
+          // padded-domain output rows (c_row_t): one division per fragment row
+          const int m = p.c_row_t ? m0 + (m0 / p.c_row_t) * p.c_row_pad : m0;
           if (c32) {   // a lane's 4 consecutive fp32 columns: one 16-byte store per fragment
 #pragma unroll
             for (int j = 0; j < NJ; ++j) {
@@ -2171,8 +2174,10 @@ int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
     // kernels for A/B runs); 32-bit buffer offsets must cover A, B, C and the gate/residual
     static const bool no_pk = getenv_flag("FS2_GEMM_NO_PK");
     const long lim = 0x7fffffffL;
+    const long crows = p.c_row_t ? p.mvalid + ((long)p.mvalid / p.c_row_t + 1) * p.c_row_pad
+                                 : p.mvalid;
     const bool pk_fits = (long)p.M * p.lda * 2 < lim && (long)p.N * p.ldb * 2 < lim &&
-                         (long)p.mvalid * p.ldc * (p.c_fp32 ? 4 : 2) < lim &&
+                         crows * p.ldc * (p.c_fp32 ? 4 : 2) < lim &&
                          (long)p.mvalid * (p.gate ? p.ldg : p.ldr) * 2 < lim;
     // persistent 256 x 256 / 256 x 192 kernel: long-K K-major GEMMs without gate / residual
     // operands (FS2_GEMM_NO_PS=1 restores the per-tile kernels for A/B runs)
@@ -2213,10 +2218,14 @@ int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
     const bool ps_w192 = ps_op ||
                          (long)((ps_t192 + 255) / 256) * 192 < (long)((ps_t256 + 255) / 256) * 256;
     const int ps_nt = ps_w192 ? ps_t192 : ps_t256;
-    const bool ps_k = p.K >= 2048 || (p.K >= max(ps_min_k, 128) && ps_nt >= ps_short_tiles);
-    if (!no_ps && ak && bk && ps_on && batch == 1 && p.split_k <= 1 && p.vec_ok &&
+    // a padded-domain output (c_row_t) exists only on this kernel: it takes every such GEMM
+    const bool ps_k = p.K >= 2048 || (p.K >= max(ps_min_k, 128) && ps_nt >= ps_short_tiles) ||
+                      (p.c_row_t && p.K >= 128);
+    const bool ps_go = !no_ps && ak && bk && ps_on && batch == 1 && p.split_k <= 1 && p.vec_ok &&
         !p.accumulate && !(p.gate && p.residual) && (!ps_op || cm_ps == 0) && p.relu <= 1 && ps_k &&
-        p.N >= 128 && pk_fits) {
+        p.N >= 128 && pk_fits;
+    if (p.c_row_t && !ps_go) return FS2_EINVAL;
+    if (ps_go) {
       GemmP q = p;
       q.g4_flags = getenv_int("FS2_PS_FLAGS", 0);
       q.tiles_m = ps_tm;
@@ -2387,6 +2396,11 @@ extern "C" int fs2_gemm(const fs2_gemm_desc* d, void* stream) {
   p.tiles_m = (p.M + BM - 1) / BM;
   p.tiles_n = (p.N + BN - 1) / BN;
   const int batch = d->batch > 1 ? d->batch : 1;
+  p.c_row_t = d->c_row_t > 0 ? d->c_row_t : 0;
+  p.c_row_pad = p.c_row_t ? d->c_row_pad : 0;
+  if (p.c_row_t && (p.c_row_pad < 0 || d->dtype != FS2_BF16 || !d->a_kmajor || !d->b_kmajor ||
+                    p.conv_mode || batch > 1 || p.split_k > 1 || p.accumulate || p.c_conv_kw))
+    return FS2_EINVAL;
 
   // ---- argument checks (host) ----
   if (!p.A || !p.B || !p.C) return FS2_EINVAL;

@@ -76,7 +76,7 @@ __global__ void weight_prep_kernel(const float* W, int O, int C, int KW, int okc
     float v = 0.f;
     if (col < KW * C) {
       const int j = col / C, c = col - j * C;
-      v = okc ? W[(long)o * KW * C + col] : W[((long)o * C + c) * KW + j];
+      v = (okc & 1) ? W[(long)o * KW * C + col] : W[((long)o * C + c) * KW + j];
     }
     Wf[i] = from_f<T>(v);
   }
@@ -86,12 +86,18 @@ __global__ void weight_prep_kernel(const float* W, int O, int C, int KW, int okc
       const int c = (int)(i / ldb), col = (int)(i - (long)c * ldb);
       float v = 0.f;
       if (col < KW * O) {
-        const int j = col / O, o = col - j * O;
-        v = okc ? W[((long)o * KW + j) * C + c] : W[((long)o * C + c) * KW + j];
+        const int jb = col / O, o = col - jb * O;
+        const int j = (okc & 2) ? KW - 1 - jb : jb;   // bit 1: Wb's taps reversed
+        v = (okc & 1) ? W[((long)o * KW + j) * C + c] : W[((long)o * C + c) * KW + j];
       }
       Wb[i] = from_f<T>(v);
     }
   }
+}
+
+// tap index of Wb (w_okc bit 1: taps reversed)
+__device__ __forceinline__ int wb_tap(const fs2_wprep_desc& d, int j) {
+  return (d.w_okc & 2) ? d.KW - 1 - j : j;
 }
 
 // one block per 64x64 tile (o, k = j*C + c) of one weight's forward image; the weight is found
@@ -130,7 +136,7 @@ __global__ void __launch_bounds__(256) weight_prep_batched_kernel(const fs2_wpre
     float v = 0.f;
     if (k < KC) {
       const int j = jcs[kl] >> 16, c = jcs[kl] & 0xffff;
-      v = d.w_okc ? d.W[(long)o * KC + k] : d.W[((long)o * d.C + c) * d.KW + j];
+      v = (d.w_okc & 1) ? d.W[(long)o * KC + k] : d.W[((long)o * d.C + c) * d.KW + j];
     }
     Wf[(long)o * d.ldf + k] = from_f<T>(v);
     tile[ol][kl] = v;
@@ -142,7 +148,7 @@ __global__ void __launch_bounds__(256) weight_prep_batched_kernel(const fs2_wpre
   for (int i = threadIdx.x; i < 64 * 64; i += blockDim.x) {
     const int kl = i >> 6, ol = i & 63, o = o0 + ol, k = k0 + kl;
     if (o >= d.O || k >= KC) continue;
-    const int j = jcs[kl] >> 16, c = jcs[kl] & 0xffff;
+    const int j = wb_tap(d, jcs[kl] >> 16), c = jcs[kl] & 0xffff;
     Wb[(long)c * d.ldb + (long)j * d.O + o] = from_f<T>(tile[ol][kl]);
   }
 }
@@ -236,7 +242,7 @@ __global__ void __launch_bounds__(256) adamw_prep_tiles_kernel(const fs2_wprep_d
     for (int i = threadIdx.x; i < 64 * 16; i += 256) {
       const int kl = i >> 4, ol = (i & 15) * 4, o = o0 + ol, k = k0 + kl;
       if (o >= d.O || k >= KC) continue;   // O % 4 == 0: the quad is all in or all out
-      const int j = jcs[kl] >> 16, c = jcs[kl] & 0xffff;
+      const int j = wb_tap(d, jcs[kl] >> 16), c = jcs[kl] & 0xffff;
       uint2 h;
       h.x = (unsigned)__builtin_bit_cast(unsigned short, (bf16)tile[ol][kl]) |
             ((unsigned)__builtin_bit_cast(unsigned short, (bf16)tile[ol + 1][kl]) << 16);
@@ -266,7 +272,7 @@ __global__ void __launch_bounds__(256) adamw_prep_tiles_kernel(const fs2_wprep_d
   for (int i = threadIdx.x; i < 64 * 64; i += blockDim.x) {
     const int kl = i >> 6, ol = i & 63, o = o0 + ol, k = k0 + kl;
     if (o >= d.O || k >= KC) continue;
-    const int j = jcs[kl] >> 16, c = jcs[kl] & 0xffff;
+    const int j = wb_tap(d, jcs[kl] >> 16), c = jcs[kl] & 0xffff;
     Wb[(long)c * d.ldb + (long)j * d.O + o] = from_f<T>(tile[ol][kl]);
   }
 }

@@ -63,6 +63,7 @@ class GemmDesc(ctypes.Structure):
         ("sA1", ctypes.c_int64), ("sA2", ctypes.c_int64), ("sB1", ctypes.c_int64),
         ("sB2", ctypes.c_int64), ("sC1", ctypes.c_int64), ("sC2", ctypes.c_int64),
         ("sR1", ctypes.c_int64), ("sR2", ctypes.c_int64), ("conv_dil", ctypes.c_int),
+        ("c_row_t", ctypes.c_int), ("c_row_pad", ctypes.c_int),
     ]
 
 

@@ -74,6 +74,8 @@ _SLICE_TARGET = N.exp_int("FS2_WGRAD_SLICE_TARGET", 240)
 # conv weight gradients with both operands K-major (channel-major padded images, conv_mode 6):
 # FS2_KM_WGRAD=0 restores the MN-major implicit-conv GEMM for A/B runs
 _KM_WGRAD = N.exp_int("FS2_KM_WGRAD", 1)
+# decoder FFN conv1 data gradient over the zero-padded dY image (engine._pad_dgrad)
+_PAD_DGRAD = N.exp_int("FS2_PAD_DGRAD", 1)
 # serial mode for per-call-site timing (bench.py --detail runs with the experiments library)
 _NO_SIDE = N.exp_flag("FS2_NO_SIDE_STREAM")
 _NO_AUX = N.exp_flag("FS2_NO_AUX_STREAM")
@@ -261,8 +263,10 @@ class FS2Engine:
                     self.w[name] = (self.empty(O, ldf), self.empty(C, ldb))
                 Wf, Wb = self.w[name]
                 W = self.params[name]
-                # conv weights are [O][KW][C] in the flat buffer (model._kw_major)
-                entries.append((W, O, C, KW, int(KW > 1), Wf, ldf, Wb, ldb))
+                # conv weights are [O][KW][C] in the flat buffer (model._kw_major); the FFN
+                # conv1 data-gradient image has its taps reversed on the padded-dY path
+                okc = int(KW > 1) | (2 if self._pad_dgrad(name) else 0)
+                entries.append((W, O, C, KW, okc, Wf, ldf, Wb, ldb))
                 self._wentries[name] = entries[-1]
             self._wtable = ops.weight_prep_table(entries)
         ops.weight_prep_batched(*self._wtable, dt=self.dt)
@@ -321,6 +325,32 @@ class FS2Engine:
         if tag:
             self._toc(tag)
 
+    def _pad_dgrad(self, wname):
+        """FFN conv1 data gradients over a zero-padded token-major dY image (bf16): the
+        producing conv2 data gradient writes dY into the image (fs2_gemm c_row_t), and with the
+        weight image's taps reversed the shift conv is a plain K-major GEMM whose A rows
+        overlap, A(m, k) = image[m * O + k] (tools/dgrad_probe.py, B = 32: decoder 417 -> 339
+        us, encoder 83 -> 76) -- no per-K-tile tap offsets or row bounds in the loader."""
+        # decoder only: the encoder's conv2 data gradient (M = 6400) runs faster on the per-tile
+        # kernels than on the persistent one the padded output needs
+        if self.dt != 1 or not _PAD_DGRAD or not wname.startswith("decoder.") or \
+                ".pos_ffn.0." not in wname:
+            return False
+        O, C, KW = self._wspecs[wname]
+        return KW > 1 and self._km_ok(O, C, KW, KW, None)
+
+    def _dy_image(self, B, T, P, F):
+        """zero-padded token-major image for a k = 2P+1 conv data gradient: 2P zero rows, then
+        per utterance T data rows and 2P zero rows (the last P are the end guard); returns
+        (image from its first row, data view from the first utterance's row 0).  Token (b, t)
+        sits at data row b*T + t remapped to b*(T+2P) + t (fs2_gemm c_row = (T, 2P)).  The pad
+        rows are zeroed here (one fill) through a view starting T rows before the image."""
+        L = T + 2 * P
+        buf = self.empty((B + 1) * L, F)
+        buf.view(B + 1, L, F)[:, T:].zero_()
+        img = buf[T:]
+        return img, img[2 * P:]
+
     def _dgrad_impl(self, dY, lddy, M, T, wname, out, ldo, n_out=None, **epi):
         O, C, KW = self._wspecs[wname]
         _, Wb = self.w[wname]
@@ -334,22 +364,31 @@ class FS2Engine:
         Mp = B * (T + 2 * P)
         split = dgrad_split(Mp, C, KW * O, self.dt)
         Xpad = torch.empty(split, Mp, C, dtype=torch.float32, device=self.dev)
-        ops.gemm(Mp, C, KW * O, dY, lddy, Wb, KW * O, Xpad, C, dt=self.dt, conv=(4, T, KW, O),
-                 c_fp32=1, split_k=split, split_stride=Mp * C if split > 1 else 0)
+        if isinstance(dY, tuple):
+            # padded dY image (_dy_image): row m of the padded domain reads image rows
+            # m .. m + 2P, i.e. A(m, k) = image[m * O + k] against the tap-reversed Wb
+            img = dY[0]
+            ops.gemm(Mp, C, KW * O, img, O, Wb, KW * O, Xpad, C, dt=self.dt, c_fp32=1,
+                     split_k=split, split_stride=Mp * C if split > 1 else 0)
+        else:
+            ops.gemm(Mp, C, KW * O, dY, lddy, Wb, KW * O, Xpad, C, dt=self.dt, conv=(4, T, KW, O),
+                     c_fp32=1, split_k=split, split_stride=Mp * C if split > 1 else 0)
         assert set(epi) <= {"residual", "ldr", "row_scale", "row_scale_post"}, epi
         ops.conv_fold(Xpad, B, T, P, C, out, ldo, dt=self.dt, residual=epi.get("residual"),
                       ldr=epi.get("ldr", 0), row_scale=epi.get("row_scale"),
                       row_scale_post=epi.get("row_scale_post"), nsplit=split,
                       split_stride=Mp * C)
 
-    def _wgrad(self, dY, lddy, X, ldx, M, T, wname, n_cols=None, gemm_tag=None, bias=None):
+    def _wgrad(self, dY, lddy, X, ldx, M, T, wname, n_cols=None, gemm_tag=None, bias=None,
+               dy_img=None):
         """weight gradient on the side stream; ``bias``: also the bias gradient (column sums of
-        dY) -- fused into the K-major path's dY transpose, else an fs2_colsum pass"""
-        h = self._side_enter(dY, X)
+        dY) -- fused into the K-major path's dY transpose, else an fs2_colsum pass; ``dy_img``:
+        dY lives in a zero-padded image (_dy_image), read from there"""
+        h = self._side_enter(dY, X, dy_img)
         tag = self._dtag("wgrad", wname, T)
         if tag:
             self._tic(tag)
-        done = self._wgrad_impl(dY, lddy, X, ldx, M, T, wname, n_cols, gemm_tag, bias)
+        done = self._wgrad_impl(dY, lddy, X, ldx, M, T, wname, n_cols, gemm_tag, bias, dy_img)
         if tag:
             self._toc(tag)
         if bias is not None and not done:
@@ -376,7 +415,7 @@ class FS2Engine:
             self._km[k] = buf
         return buf[64:64 + C * ld]
 
-    def _wgrad_km(self, dY, lddy, X, ldx, M, T, wname, gemm_tag=None, bias=None):
+    def _wgrad_km(self, dY, lddy, X, ldx, M, T, wname, gemm_tag=None, bias=None, dy_img=None):
         """grad[O][KW][C] += sum_{b,t} dY[b,t,o] X[b, reflect(t+j-P), c] with both GEMM operands
         K-major: dY and X are first written channel-major over the padded token domain (T+2P
         columns per utterance; dY's pad columns zero, X's reflected), where tap j is a constant
@@ -394,8 +433,15 @@ class FS2Engine:
         dYT = self._km_image("dy", O, Kp)
         XT = self._km_image("x", C, Kp)
         ws = self.ws(max(ops.pad_transpose_ws(Kp, O), 1))
-        ops.pad_transpose(dY, lddy, B, T, O, P, 0, dYT, Kp, Kp, dt=self.dt,
-                          colsum=self.grads[bias] if bias is not None else None, ws=ws)
+        colsum = self.grads[bias] if bias is not None else None
+        if dy_img is not None:
+            # the padded dY image already holds the zero pad rows: a plain transpose of its
+            # utterance rows (from image row P: T + 2P rows per utterance)
+            ops.pad_transpose(dy_img[P:], lddy, B, T + 2 * P, O, 0, 0, dYT, Kp, Kp,
+                              dt=self.dt, colsum=colsum, ws=ws)
+        else:
+            ops.pad_transpose(dY, lddy, B, T, O, P, 0, dYT, Kp, Kp, dt=self.dt, colsum=colsum,
+                              ws=ws)
         ops.pad_transpose(X, ldx, B, T, C, P, 1, XT, Kp, Kp, dt=self.dt)
         stride = O * ncol
         ws = self.ws(S * stride)
@@ -408,13 +454,16 @@ class FS2Engine:
         ops.sum_slices(ws, S, stride, stride, self.grads[wname], accumulate=1)
         return True
 
-    def _wgrad_impl(self, dY, lddy, X, ldx, M, T, wname, n_cols=None, gemm_tag=None, bias=None):
+    def _wgrad_impl(self, dY, lddy, X, ldx, M, T, wname, n_cols=None, gemm_tag=None, bias=None,
+                    dy_img=None):
         """grad[O][KW][C] += sum_m dY[m][o] * X[reflect(t+j-P)][c]   (fp32, accumulate).
         ``gemm_tag``: HIP events around the GEMM launch alone (bench.py's roofline entry for
         the FFN conv1 weight gradient), on the stream it runs on (the side stream)."""
         O, C, KW = self._wspecs[wname]
         if self._km_ok(O, C, KW, T, n_cols) and lddy % 8 == 0 and ldx % 8 == 0:
-            return self._wgrad_km(dY, lddy, X, ldx, M, T, wname, gemm_tag, bias)
+            return self._wgrad_km(dY, lddy, X, ldx, M, T, wname, gemm_tag, bias, dy_img)
+        if dy_img is not None:
+            raise RuntimeError(f"{wname}: a padded dY image needs the K-major weight gradient")
         Ncols = n_cols or KW * C
         K = round_up(M, self.epc)
         tiles = -(-O // 128) * -(-Ncols // 128)
@@ -536,19 +585,26 @@ class FS2Engine:
                    dbeta=G[prefix + "norm2.norm.bias"], dcol=G[prefix + "pos_ffn.2.conv.bias"])
         w2 = prefix + "pos_ffn.2.conv.weight"
         w1 = prefix + "pos_ffn.0.conv.weight"
-        dHc = self.empty(M, F)
+        pad = self._pad_dgrad(w1)
+        if pad:   # conv2's data gradient lands in the zero-padded image conv1's reads
+            P1 = (self._wspecs[w1][2] - 1) // 2
+            img, dHc = self._dy_image(B, T, P1, F)
+            crow = {"c_row": (T, 2 * P1)}
+        else:
+            img, crow = None, {}
+            dHc = self.empty(M, F)
         dX1 = self.empty(M, D)
         # weight gradients enqueued as soon as their operands exist (the side stream waits for
         # everything queued on main so far): conv2's before its data gradient, conv1's right
         # after dHc, so the two big conv1 GEMMs overlap instead of the conv1 weight gradient
         # holding every CU while main's out-projection waits behind it
         self._wgrad(dY, D, ctx["Hc"], F, M, T, w2)
-        self._dgrad(dY, D, M, T, w2, dHc, F, gate=ctx["Hc"], ldg=F)
+        self._dgrad(dY, D, M, T, w2, dHc, F, gate=ctx["Hc"], ldg=F, **crow)
         self._wgrad(dHc, F, ctx["X1"], D, M, T, w1,
                     gemm_tag="ffn_conv1_wgrad." + prefix.split(".")[0],
-                    bias=prefix + "pos_ffn.0.conv.bias")
-        self._dgrad(dHc, F, M, T, w1, dX1, D, residual=ds2, ldr=D)
-        del dY, dHc, ds2
+                    bias=prefix + "pos_ffn.0.conv.bias", dy_img=img)
+        self._dgrad((img,) if pad else dHc, F, M, T, w1, dX1, D, residual=ds2, ldr=D)
+        del dY, dHc, ds2, img
         lnws = self.ws(ops.ln_ws(M, D))
         ds1, dAo = self.empty(M, D), self.empty(M, D)
         ops.ln_bwd(dX1, D, ctx["s1"], D, ctx["mean1"], ctx["rstd1"], P[prefix + "norm1.norm.weight"],

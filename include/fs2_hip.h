@@ -79,6 +79,12 @@ typedef struct fs2_gemm_desc {
   int batch, batch_div;
   int64_t sA1, sA2, sB1, sB2, sC1, sC2, sR1, sR2;
   int conv_dil;         /* dilation of conv modes 1 / 5 (tap j reads row t + (j-P)*dil); 0 = 1 */
+  /* c_row_t > 0: output row m is stored at C row m + (m / c_row_t) * c_row_pad -- a token-major
+   * result written into a padded token domain (c_row_pad zero rows between utterances, which
+   * the caller keeps zero), e.g. the FFN conv2 data gradient straight into the zero-padded dY
+   * image of the conv1 data gradient below.  bf16, both K-major, no split / batch / conv; runs
+   * on the persistent 256-row kernel (FS2_EINVAL where that kernel does not apply).          */
+  int c_row_t, c_row_pad;
 } fs2_gemm_desc;
 
 int fs2_gemm(const fs2_gemm_desc* d, void* stream);
@@ -281,7 +287,10 @@ int fs2_adamw(float* param, const float* grad, float* exp_avg, float* exp_avg_sq
 
 /* master weight W (fp32) -> fwd copy Wf[O][KW][C] and dgrad copy Wb[C][KW][O] in dtype, each
  * with row pitch padded to ldf / ldb elements (zeros in the pad).  W is stored torch-style
- * [O][C][KW] (w_okc = 0) or [O][KW][C] (w_okc = 1, the flat-buffer layout of conv weights). */
+ * [O][C][KW] (w_okc bit 0 clear) or [O][KW][C] (bit 0 set, the flat-buffer layout of conv
+ * weights).  w_okc bit 1: Wb's taps reversed, Wb[C][KW-1-j][O] -- the order in which the conv
+ * data gradient over a zero-padded token-major dY image is a plain K-major GEMM whose A rows
+ * overlap (A(m, k) = image[m*O + k], lda = O). */
 int fs2_weight_prep(const float* W, int O, int C, int KW, int w_okc, void* Wf, int ldf, void* Wb,
                     int ldb, int dtype, void* stream);
 

@@ -832,6 +832,81 @@ def test_weight_prep_batched_layouts(cuda):
         assert torch.equal(Wb, rb)
 
 
+def test_weight_prep_reversed_taps(cuda):
+    """w_okc bit 1: the data-gradient image Wb with its taps reversed, Wb[c][(KW-1-j)*O + o],
+    in fs2_weight_prep_batched, fs2_weight_prep and the fused AdamW image pass (zero step:
+    decay 1, step size 0), exactly the bf16 rounding of the expected image."""
+    from fastspeech2 import ops
+    torch.manual_seed(13)
+    O, C, KW = 136, 72, 9
+    W = torch.randn(O, KW, C, device=cuda)
+    ldf = ops.round_up(KW * C, 8)
+    ref_b = W.flip(1).permute(2, 1, 0).reshape(C, KW * O).to(torch.bfloat16)
+    ref_f = torch.zeros(O, ldf, device=cuda)
+    ref_f[:, :KW * C] = W.reshape(O, KW * C)
+    ref_f = ref_f.to(torch.bfloat16)
+    Wf = torch.full((O, ldf), float("nan"), device=cuda).to(torch.bfloat16)
+    Wb = torch.full((C, KW * O), float("nan"), device=cuda).to(torch.bfloat16)
+    table = ops.weight_prep_table([(W, O, C, KW, 3, Wf, ldf, Wb, KW * O)])
+    ops.weight_prep_batched(*table, dt=1)
+    torch.cuda.synchronize()
+    assert torch.equal(Wf, ref_f) and torch.equal(Wb, ref_b)
+    Wb.fill_(float("nan"))
+    ops.weight_prep(W, O, C, KW, Wf, ldf, Wb, KW * O, dt=1, w_okc=3)
+    torch.cuda.synchronize()
+    assert torch.equal(Wb, ref_b)
+
+
+@pytest.mark.parametrize("B,T,O,C,KW", [(32, 977, 1536, 384, 9), (3, 37, 256, 128, 9),
+                                         (2, 50, 192, 256, 5)])
+def test_conv_dgrad_padded_image(cuda, B, T, O, C, KW):
+    """The FFN conv1 data gradient over a zero-padded token-major dY image: (1) a gated GEMM
+    writes its rows into the image's data rows (fs2_gemm c_row = (T, 2P)), leaving the zero
+    pad rows untouched; (2) the plain K-major GEMM over the image with overlapping A rows
+    (lda = O) against the tap-reversed Wb equals the shift-conv GEMM (conv_mode 4) over
+    token-major dY with the natural Wb -- the same products in another K order (fp32 rel
+    1e-5).  Decoder shape, a ragged small one, a k = 5 one."""
+    from fastspeech2 import ops
+    torch.manual_seed(B * T + KW)
+    P = (KW - 1) // 2
+    M = B * T
+    L = T + 2 * P
+    Mp = B * L
+    bf = torch.bfloat16
+    # (1) gated GEMM (the conv2 data gradient: M x O from K = C2) into the padded image
+    C2 = 384
+    A = (torch.randn(M, C2, device=cuda) * 0.5).to(bf)
+    W2 = (torch.randn(O, C2, device=cuda) * 0.05).to(bf)
+    G = torch.randn(M, O, device=cuda).to(bf)
+    buf = torch.full(((B + 1) * L, O), float("nan"), device=cuda, dtype=bf)
+    buf.view(B + 1, L, O)[:, T:] = 0
+    img = buf[T:]
+    ops.gemm(M, O, C2, A, C2, W2, C2, img[2 * P:], O, dt=1, gate=G, ldg=O, c_row=(T, 2 * P))
+    dY = torch.empty(M, O, device=cuda, dtype=bf)
+    ops.gemm(M, O, C2, A, C2, W2, C2, dY, O, dt=1, gate=G, ldg=O)
+    torch.cuda.synchronize()
+    data = img[2 * P:2 * P + Mp].view(B, L, O)
+    # (the padded write always runs on the persistent kernel; small unpadded shapes may not)
+    assert rel(data[:, :T].reshape(M, O), dY) < (1e-6 if M >= 31264 else 1e-2)
+    assert not data[:, T:].float().abs().gt(0).any()          # pad rows still zero
+    assert not img[:2 * P].float().abs().gt(0).any()
+    # (2) data gradient: plain GEMM over the image vs conv_mode 4
+    Wm = torch.randn(O, KW, C, device=cuda) * 0.05
+    ldf = ops.round_up(KW * C, 8)
+    Wf = torch.empty(O, ldf, device=cuda, dtype=bf)
+    Wb = torch.empty(C, KW * O, device=cuda, dtype=bf)
+    Wr = torch.empty(C, KW * O, device=cuda, dtype=bf)
+    ops.weight_prep(Wm, O, C, KW, Wf, ldf, Wb, KW * O, dt=1, w_okc=1)
+    ops.weight_prep(Wm, O, C, KW, Wf, ldf, Wr, KW * O, dt=1, w_okc=3)
+    X4 = torch.empty(Mp, C, device=cuda)
+    X0 = torch.empty(Mp, C, device=cuda)
+    ops.gemm(Mp, C, KW * O, dY, O, Wb, KW * O, X4, C, dt=1, conv=(4, T, KW, O), c_fp32=1)
+    ops.gemm(Mp, C, KW * O, img, O, Wr, KW * O, X0, C, dt=1, c_fp32=1)
+    torch.cuda.synchronize()
+    assert torch.isfinite(X0).all()
+    assert rel(X0, X4) < 1e-5
+
+
 @pytest.mark.parametrize("dt,code", [(torch.float32, 0), (torch.bfloat16, 1)])
 @pytest.mark.parametrize("B,T,V", [(32, 200, 95), (3, 37, 128), (1, 5, 7)])
 def test_embedding_fwd_bwd(cuda, dt, code, B, T, V):
