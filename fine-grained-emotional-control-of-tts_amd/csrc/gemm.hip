@@ -2071,9 +2071,18 @@ __global__ void __launch_bounds__(BNT, 1) gemm_ps_kernel(GemmP p) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           const int m0 = mb + 16 * i + li;
-          const bool rowok = m0 < p.mvalid;
+          bool rowok = m0 < p.mvalid;
           // padded-domain output rows (c_row_t): one division per fragment row
-          const int m = p.c_row_t ? m0 + (m0 / p.c_row_t) * p.c_row_pad : m0;
+          int m = m0;
+          if (p.c_row_t) {
+            if (p.c_row_pad >= 0) {
+              m = m0 + (m0 / p.c_row_t) * p.c_row_pad;
+            } else {   // drop the pad rows of a padded-domain result
+              const int L = p.c_row_t - p.c_row_pad, u = m0 / L;
+              rowok = rowok && m0 - u * L < p.c_row_t;
+              m = m0 + u * p.c_row_pad;
+            }
+          }
           if (c32) {   // a lane's 4 consecutive fp32 columns: one 16-byte store per fragment
 #pragma unroll
             for (int j = 0; j < NJ; ++j) {
@@ -2174,8 +2183,9 @@ int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
     // kernels for A/B runs); 32-bit buffer offsets must cover A, B, C and the gate/residual
     static const bool no_pk = getenv_flag("FS2_GEMM_NO_PK");
     const long lim = 0x7fffffffL;
-    const long crows = p.c_row_t ? p.mvalid + ((long)p.mvalid / p.c_row_t + 1) * p.c_row_pad
-                                 : p.mvalid;
+    const long crows = p.c_row_t && p.c_row_pad > 0
+                           ? p.mvalid + ((long)p.mvalid / p.c_row_t + 1) * p.c_row_pad
+                           : p.mvalid;
     const bool pk_fits = (long)p.M * p.lda * 2 < lim && (long)p.N * p.ldb * 2 < lim &&
                          crows * p.ldc * (p.c_fp32 ? 4 : 2) < lim &&
                          (long)p.mvalid * (p.gate ? p.ldg : p.ldr) * 2 < lim;
@@ -2398,7 +2408,7 @@ extern "C" int fs2_gemm(const fs2_gemm_desc* d, void* stream) {
   const int batch = d->batch > 1 ? d->batch : 1;
   p.c_row_t = d->c_row_t > 0 ? d->c_row_t : 0;
   p.c_row_pad = p.c_row_t ? d->c_row_pad : 0;
-  if (p.c_row_t && (p.c_row_pad < 0 || d->dtype != FS2_BF16 || !d->a_kmajor || !d->b_kmajor ||
+  if (p.c_row_t && (d->dtype != FS2_BF16 || !d->a_kmajor || !d->b_kmajor ||
                     p.conv_mode || batch > 1 || p.split_k > 1 || p.accumulate || p.c_conv_kw))
     return FS2_EINVAL;
 

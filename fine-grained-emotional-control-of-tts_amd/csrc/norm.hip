@@ -855,6 +855,27 @@ __global__ void __launch_bounds__(256) pad_transpose_kernel(const bf16* X, long 
   }
 }
 
+// token-major padded image (conv forward over the padded domain, fs2_pad_rows):
+// out row b*(T+2P) + i = X row b*T + reflect(i-P) (reflect) or zero outside [0,T); rows past
+// B*(T+2P) zero.  One thread per 16-byte chunk, 32-bit indices (host-checked).
+__global__ void __launch_bounds__(256) pad_rows_kernel(const bf16* X, long ldx, int B, int T,
+                                                       int C8, int P, int reflect, bf16* out,
+                                                       long ldo, unsigned n8) {
+  const unsigned idx = blockIdx.x * 256u + threadIdx.x;
+  if (idx >= n8) return;
+  const unsigned r = idx / (unsigned)C8;
+  const int c = (int)(idx - r * (unsigned)C8) * 8;
+  const unsigned L = (unsigned)(T + 2 * P);
+  const unsigned b = r / L;
+  const int i = (int)(r - b * L) - P;
+  u32x4 v = {0u, 0u, 0u, 0u};
+  if ((int)b < B) {
+    const int t = reflect ? reflect_idx(i, T) : i;
+    if (t >= 0 && t < T) v = *(const u32x4*)(X + ((long)b * T + t) * ldx + c);
+  }
+  *(u32x4*)(out + (long)r * ldo + c) = v;
+}
+
 int colsum_blocks(int M) { return min(512, max(1, (M + 63) / 64)); }
 bool a16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
@@ -1054,5 +1075,22 @@ extern "C" int fs2_pad_transpose(const void* X, int64_t ldx, int B, int T, int C
                        (int)grid.x, C, 1, colsum, nullptr, nullptr, 1);
     FS2_CHECK_LAUNCH();
   }
+  return 0;
+}
+
+extern "C" int fs2_pad_rows(const void* X, int64_t ldx, int B, int T, int C, int P, int reflect,
+                            int tail, void* out, int64_t ldo, int dtype, void* stream) {
+  if (B <= 0 || T <= 0 || C <= 0) return 0;
+  if (dtype != FS2_BF16 || !X || !out || P < 0 || tail < 0 || (reflect && P >= T))
+    return FS2_EINVAL;
+  if ((C % 8) || (ldx % 8) || (ldo % 8) || ldo < C || ldx < C || !a16(X) || !a16(out))
+    return FS2_EALIGN;
+  const long rows = (long)B * (T + 2 * P) + tail;
+  const long n8 = rows * (C / 8);
+  if (n8 >= 0x7fffffffL || rows * ldo >= 0x7fffffffL) return FS2_EINVAL;
+  hipLaunchKernelGGL(pad_rows_kernel, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, (const bf16*)X, (long)ldx, B, T, C / 8, P, reflect,
+                     (bf16*)out, (long)ldo, (unsigned)n8);
+  FS2_CHECK_LAUNCH();
   return 0;
 }

@@ -76,6 +76,8 @@ _SLICE_TARGET = N.exp_int("FS2_WGRAD_SLICE_TARGET", 240)
 _KM_WGRAD = N.exp_int("FS2_KM_WGRAD", 1)
 # decoder FFN conv1 data gradient over the zero-padded dY image (engine._pad_dgrad)
 _PAD_DGRAD = N.exp_int("FS2_PAD_DGRAD", 1)
+# FFN conv1 forward over a reflect-padded X image (engine._pad_fwd)
+_PAD_FWD = N.exp_int("FS2_PAD_FWD", 1)
 # serial mode for per-call-site timing (bench.py --detail runs with the experiments library)
 _NO_SIDE = N.exp_flag("FS2_NO_SIDE_STREAM")
 _NO_AUX = N.exp_flag("FS2_NO_AUX_STREAM")
@@ -313,9 +315,26 @@ class FS2Engine:
         tag = self._dtag("fwd", wname, T)
         if tag:
             self._tic(tag)
-        ops.gemm(M, O, K, X, ldx, Wf, K, out, ldo, dt=self.dt, conv=conv, **epi)
+        if isinstance(X, tuple):
+            # reflect-padded X image (_pad_fwd): the conv over the padded domain is a plain
+            # K-major GEMM with overlapping rows, A(m, k=(j,c)) = image[m*C + k]; the pad rows'
+            # results are dropped by the epilogue (c_row = (T, -2P))
+            P = (KW - 1) // 2
+            Mp = (M // T) * (T + 2 * P)
+            ops.gemm(Mp, O, K, X[0], C, Wf, K, out, ldo, dt=self.dt, c_row=(T, -2 * P), **epi)
+        else:
+            ops.gemm(M, O, K, X, ldx, Wf, K, out, ldo, dt=self.dt, conv=conv, **epi)
         if tag:
             self._toc(tag)
+
+    def _pad_fwd(self, wname, M, T):
+        """FFN conv1 forward over a reflect-padded token-major X image (fs2_pad_rows + a plain
+        GEMM whose A rows overlap, 2P dropped rows per utterance): tools/fwd_probe.py, B = 32:
+        decoder 374 -> 305 us, encoder 100 -> 89 (the implicit conv's per-K-tile reflect rows
+        and tap offsets are gone from the loader)"""
+        O, C, KW = self._wspecs[wname]
+        return (self.dt == 1 and _PAD_FWD and KW > 1 and C % 64 == 0 and (KW - 1) // 2 < T and
+                self.w[wname][0].shape[1] == KW * C)
 
     def _dgrad(self, dY, lddy, M, T, wname, out, ldo, n_out=None, **epi):
         tag = self._dtag("dgrad", wname, T)
@@ -549,13 +568,20 @@ class FS2Engine:
                    mean1, rstd1, M, D, dt=self.dt, seed=seed, r=Ao, ldr=D, p_r=p_drop, salt_r=s_r1,
                    s_out=s1)
         del Ao
-        F = self._wspecs[prefix + "pos_ffn.0.conv.weight"][0]
+        w1 = prefix + "pos_ffn.0.conv.weight"
+        F, _, KW1 = self._wspecs[w1]
         Hc = self.empty(M, F)
+        X1in = X1
+        if self._pad_fwd(w1, M, T):
+            P1 = (KW1 - 1) // 2
+            img = self.empty(B * (T + 2 * P1) + 2 * P1, D)
+            ops.pad_rows(X1, D, B, T, D, P1, 1, 2 * P1, img, D, dt=self.dt)
+            X1in = (img,)
         tag = "ffn_conv1_fwd." + prefix.split(".")[0]
         self._tic(tag)
-        self._fwd(X1, D, M, T, prefix + "pos_ffn.0.conv.weight", Hc, F,
-                  bias=P[prefix + "pos_ffn.0.conv.bias"], relu=1)
+        self._fwd(X1in, D, M, T, w1, Hc, F, bias=P[prefix + "pos_ffn.0.conv.bias"], relu=1)
         self._toc(tag)
+        del X1in
         Y = self.empty(M, D)
         self._fwd(Hc, F, M, T, prefix + "pos_ffn.2.conv.weight", Y, D,
                   bias=P[prefix + "pos_ffn.2.conv.bias"])

@@ -73,6 +73,11 @@ def pad_transpose(X, ldx, B, T, C, P, reflect, out, ldo, ncols, *, dt, colsum=No
                                    _p(colsum), _p(ws), dt, _s()), "fs2_pad_transpose")
 
 
+def pad_rows(X, ldx, B, T, C, P, reflect, tail, out, ldo, *, dt):
+    _chk(N.lib().fs2_pad_rows(_p(X), ldx, B, T, C, P, reflect, tail, _p(out), ldo, dt, _s()),
+         "fs2_pad_rows")
+
+
 def pad_transpose_ws(ncols, C):
     return -(-ncols // 64) * C
 

@@ -79,11 +79,14 @@ typedef struct fs2_gemm_desc {
   int batch, batch_div;
   int64_t sA1, sA2, sB1, sB2, sC1, sC2, sR1, sR2;
   int conv_dil;         /* dilation of conv modes 1 / 5 (tap j reads row t + (j-P)*dil); 0 = 1 */
-  /* c_row_t > 0: output row m is stored at C row m + (m / c_row_t) * c_row_pad -- a token-major
-   * result written into a padded token domain (c_row_pad zero rows between utterances, which
-   * the caller keeps zero), e.g. the FFN conv2 data gradient straight into the zero-padded dY
-   * image of the conv1 data gradient below.  bf16, both K-major, no split / batch / conv; runs
-   * on the persistent 256-row kernel (FS2_EINVAL where that kernel does not apply).          */
+  /* c_row_t > 0, c_row_pad > 0: output row m is stored at C row m + (m / c_row_t) * c_row_pad
+   * -- a token-major result written into a padded token domain (c_row_pad zero rows between
+   * utterances, which the caller keeps zero), e.g. the FFN conv2 data gradient straight into
+   * the zero-padded dY image of the conv1 data gradient.  c_row_pad < 0: the inverse -- rows m
+   * of a padded domain (L = c_row_t - c_row_pad rows per utterance) with m mod L < c_row_t are
+   * stored at m - (m / L) * (-c_row_pad), the others dropped (a conv forward over the padded
+   * domain, fs2_pad_rows).  bf16, both K-major, no split / batch / conv; runs on the
+   * persistent 256-row kernel (FS2_EINVAL where that kernel does not apply).                */
   int c_row_t, c_row_pad;
 } fs2_gemm_desc;
 
@@ -113,6 +116,17 @@ int fs2_pad_transpose(const void* X, int64_t ldx, int B, int T, int C, int P, in
 
 int fs2_sum_slices(const float* ws, int nslices, int64_t stride, int64_t n, float* out,
                    int accumulate, void* stream);
+
+/* token-major padded image for a conv forward over the padded token domain (SB Conv1d
+ * "same"+reflect, App. A.1; model.py:241-267 FFN conv1): out row b*(T+2P) + i = X row
+ * b*T + reflect(i-P) (reflect = 1) or X row b*T + i-P inside [0,T) and zero outside
+ * (reflect = 0), i in [0, T+2P); then `tail` zero rows (the guard the overlapping-row GEMM
+ * reads past the last utterance).  With it the conv is a plain K-major GEMM over the padded
+ * domain, A(m, k=(j,c)) = out[m*ldo + k] (lda = ldo = C), whose rows m with
+ * m mod (T+2P) >= T are dropped by fs2_gemm's c_row (T, -2P).  bf16; C, ldx, ldo multiples
+ * of 8, 16-byte aligned pointers. */
+int fs2_pad_rows(const void* X, int64_t ldx, int B, int T, int C, int P, int reflect, int tail,
+                 void* out, int64_t ldo, int dtype, void* stream);
 
 /* column sums: out[n] (+)= sum_m X[m][n]   (bias gradients; SB Linear/Conv1d bias, K16) */
 int fs2_colsum(const void* X, int64_t ldx, int M, int N, int dtype, float* out, int accumulate,

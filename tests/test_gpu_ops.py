@@ -907,6 +907,39 @@ def test_conv_dgrad_padded_image(cuda, B, T, O, C, KW):
     assert rel(X0, X4) < 1e-5
 
 
+@pytest.mark.parametrize("B,T,C,O,KW", [(32, 977, 384, 1536, 9), (32, 200, 384, 1536, 9),
+                                         (3, 37, 128, 256, 9), (2, 50, 192, 320, 5)])
+def test_conv_fwd_padded_image(cuda, B, T, C, O, KW):
+    """The FFN conv1 forward over the padded token domain: fs2_pad_rows writes the
+    reflect-padded token-major image (checked exactly against torch's reflect pad), then a
+    plain K-major GEMM with overlapping rows (lda = C) drops each utterance's 2P pad rows in
+    its epilogue (c_row = (T, -2P)) -- equal to the implicit reflect conv (conv_mode 1) with
+    bias + ReLU (bf16 outputs, rel 1e-2: two kernels, one sum order).  Every token row is
+    written (NaN-filled output)."""
+    from fastspeech2 import ops
+    torch.manual_seed(B + T + KW)
+    P = (KW - 1) // 2
+    M, L = B * T, T + 2 * P
+    bf = torch.bfloat16
+    X = (torch.randn(M, C, device=cuda) * 0.5).to(bf)
+    img = torch.full((B * L + 2 * P, C), float("nan"), device=cuda, dtype=bf)
+    ops.pad_rows(X, C, B, T, C, P, 1, 2 * P, img, C, dt=1)
+    ref_img = F.pad(X.float().view(B, T, C).transpose(1, 2), (P, P), mode="reflect")
+    torch.cuda.synchronize()
+    assert torch.equal(img[:B * L].float().view(B, L, C), ref_img.transpose(1, 2))
+    assert not img[B * L:].float().abs().gt(0).any()
+    W = (torch.randn(O, KW * C, device=cuda) * 0.05).to(bf)
+    bias = torch.randn(O, device=cuda)
+    Y1 = torch.full((M, O), float("nan"), device=cuda, dtype=bf)
+    Y0 = torch.full((M, O), float("nan"), device=cuda, dtype=bf)
+    ops.gemm(M, O, KW * C, X, C, W, KW * C, Y1, O, dt=1, conv=(1, T, KW, C), bias=bias, relu=1)
+    ops.gemm(B * L, O, KW * C, img, C, W, KW * C, Y0, O, dt=1, bias=bias, relu=1,
+             c_row=(T, -2 * P))
+    torch.cuda.synchronize()
+    assert torch.isfinite(Y0.float()).all()
+    assert rel(Y0, Y1) < 1e-2
+
+
 @pytest.mark.parametrize("dt,code", [(torch.float32, 0), (torch.bfloat16, 1)])
 @pytest.mark.parametrize("B,T,V", [(32, 200, 95), (3, 37, 128), (1, 5, 7)])
 def test_embedding_fwd_bwd(cuda, dt, code, B, T, V):
