@@ -450,7 +450,7 @@ def main():
                                    + (", single speaker" if args.single_speaker else ""),
                        "global_batch": args.batch * world, "seq_len": Tm,
                        "valid_mel_frames_per_step": frames_all, "parallelism": f"dp{world}"},
-            "roofline": {"bound": "mfma", "kernel": "decoder FFN conv1 (k=9) implicit-GEMM fwd",
+            "roofline": {"bound": "mfma", "kernel": "decoder FFN conv1 (k=9) fwd: K-major GEMM with overlapping A rows over the reflect-padded X image (gemm_ps_kernel<0, 64, 0, 0>, bias + ReLU, pad rows dropped); the image copy (fs2_pad_rows) is a separate launch",
                          "achieved": achieved, "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": (achieved / MFMA_BF16_PEAK_TFLOPS) if achieved else None,
                          "traffic": traffic, "traffic_source": traffic_src,
