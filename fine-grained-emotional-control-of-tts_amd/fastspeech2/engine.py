@@ -129,6 +129,7 @@ class FS2Engine:
         self.on_grads_ready = None   # optional callback(tag) for DP overlap
         self.timer = None            # optional KernelTimer: HIP events around tagged launches
         self._km = {}                # conv_mode-6 images, reused layer after layer (side stream)
+        self._img = {}               # per-layer zero-padded dY images (_dy_image)
 
     def _tic(self, tag):
         if self.timer is not None:
@@ -350,24 +351,32 @@ class FS2Engine:
         weight image's taps reversed the shift conv is a plain K-major GEMM whose A rows
         overlap, A(m, k) = image[m * O + k] (tools/dgrad_probe.py, B = 32: decoder 417 -> 339
         us, encoder 83 -> 76) -- no per-K-tile tap offsets or row bounds in the loader."""
-        # decoder only: the encoder's conv2 data gradient (M = 6400) runs faster on the per-tile
-        # kernels than on the persistent one the padded output needs
-        if self.dt != 1 or not _PAD_DGRAD or not wname.startswith("decoder.") or \
-                ".pos_ffn.0." not in wname:
+        if self.dt != 1 or not _PAD_DGRAD or ".pos_ffn.0." not in wname:
             return False
+        if _PAD_DGRAD == 2 and not wname.startswith("decoder."):
+            return False     # A/B: decoder only
         O, C, KW = self._wspecs[wname]
         return KW > 1 and self._km_ok(O, C, KW, KW, None)
 
-    def _dy_image(self, B, T, P, F):
+    def _dy_image(self, key, B, T, P, F):
         """zero-padded token-major image for a k = 2P+1 conv data gradient: 2P zero rows, then
         per utterance T data rows and 2P zero rows (the last P are the end guard); returns
         (image from its first row, data view from the first utterance's row 0).  Token (b, t)
-        sits at data row b*T + t remapped to b*(T+2P) + t (fs2_gemm c_row = (T, 2P)).  The pad
-        rows are zeroed here (one fill) through a view starting T rows before the image."""
+        sits at data row b*T + t remapped to b*(T+2P) + t (fs2_gemm c_row = (T, 2P)).  One
+        buffer per layer (``key``), kept across steps: only its data rows are ever written, so
+        its pad rows -- zeroed through a view starting T rows before the image -- need zeroing
+        only when the batch shape changes (stream order keeps the reuse safe: the next step's
+        main-stream work follows this step's side-stream join)."""
         L = T + 2 * P
-        buf = self.empty((B + 1) * L, F)
-        buf.view(B + 1, L, F)[:, T:].zero_()
-        img = buf[T:]
+        n = (B + 1) * L * F
+        shape = (B, T, P, F)
+        ent = self._img.get(key)
+        if ent is None or ent[0] != shape:
+            buf = ent[1] if ent is not None and ent[1].numel() >= n else \
+                torch.empty(n, dtype=self.adt, device=self.dev)
+            buf[:n].view(B + 1, L, F)[:, T:].zero_()
+            ent = self._img[key] = (shape, buf)
+        img = ent[1][:n].view((B + 1) * L, F)[T:]
         return img, img[2 * P:]
 
     def _dgrad_impl(self, dY, lddy, M, T, wname, out, ldo, n_out=None, **epi):
@@ -614,7 +623,7 @@ class FS2Engine:
         pad = self._pad_dgrad(w1)
         if pad:   # conv2's data gradient lands in the zero-padded image conv1's reads
             P1 = (self._wspecs[w1][2] - 1) // 2
-            img, dHc = self._dy_image(B, T, P1, F)
+            img, dHc = self._dy_image(prefix, B, T, P1, F)
             crow = {"c_row": (T, 2 * P1)}
         else:
             img, crow = None, {}
