@@ -83,6 +83,17 @@ _NO_SIDE = N.exp_flag("FS2_NO_SIDE_STREAM")
 _NO_AUX = N.exp_flag("FS2_NO_AUX_STREAM")
 
 
+def eff_split(K, ns, bk):
+    """the split-K slice count fs2_gemm actually uses for ``ns`` requested slices of K (it
+    rounds the K-tiles per slice up, which can leave trailing slices empty -- those it zeroes
+    with a memset so a consumer summing all ``ns`` stays right).  Requesting this count instead
+    skips the memset launch."""
+    if ns <= 1:
+        return 1
+    nkt = -(-K // bk)
+    return -(-nkt // -(-nkt // ns))
+
+
 def wgrad_slices(O, Ncols, ldc, K, dt, n_cu=256):
     """Split-K slice count for a weight gradient with a small output: enough 256x128 tiles x
     slices to fill the 256 CUs once, each slice >= 8 K-tiles; slices are fp32 planes summed in
@@ -504,6 +515,7 @@ class FS2Engine:
         if ns == 1 and _BIG_SLICES and self.dt == 1 and Ncols == ldc and O * ldc > 600_000:
             tiles = -(-O // 256) * -(-Ncols // 256)
             ns = max(1, min(-(-_SLICE_TARGET // tiles), (K // 64) // 8))
+        ns = eff_split(K, ns, _BK[self.dt])
         if ns > 1:
             # small outputs: split-K slices into fp32 planes, summed in a fixed order -- instead
             # of tens of fp32 atomics landing on every output element
