@@ -204,16 +204,18 @@ def secondary_legs(cfg_all, args, rank, world):
     return out
 
 
-def pmc_traffic(kind="roofline"):
-    """HBM bytes per launch of a roofline kernel from the newest committed PMC summary
-    (profiles/r*_<kind>_traffic.json, written by tools/rocprof_summary.py traffic from two
-    separate rocprofv3 --pmc passes of this same bench command)."""
+def pmc_traffic(kind="roofline", kernel=None):
+    """HBM bytes per launch of a roofline kernel from the newest committed PMC summary of that
+    kernel (profiles/r*_<kind>_traffic.json whose kernel_substr is ``kernel``, written by
+    tools/rocprof_summary.py traffic from two separate rocprofv3 --pmc passes of this same
+    bench command)."""
     import glob
     hits = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{kind}_traffic.json")))
-    if not hits:
-        return None, None
-    d = json.load(open(hits[-1]))
-    return d["hbm_bytes_per_launch"], os.path.relpath(hits[-1], ROOT)
+    for h in reversed(hits):
+        d = json.load(open(h))
+        if kernel is None or d.get("kernel_substr", "").startswith(kernel):
+            return d["hbm_bytes_per_launch"], os.path.relpath(h, ROOT)
+    return None, None
 
 
 def detail_table(ks, eng, B, steps, elapsed):
@@ -424,13 +426,15 @@ def main():
         n, ms = ks.get("ffn_conv1_fwd.decoder", (0, float("nan")))
         kflop = 2.0 * (args.batch * Tm) * F * (KW * D)
         achieved = kflop / (ms * 1e-3) / 1e12 if n else None
-        traffic, traffic_src = pmc_traffic() if not args.scaled else (None, None)
+        traffic, traffic_src = (pmc_traffic("roofline", "gemm256_kernel<true, true, 1")
+                                if not args.scaled else (None, None))
         # second entry: the decoder FFN conv1 weight gradient, the largest GEMM bucket of the
         # step (2 M F 9D per launch like the forward); it runs on the side stream beside the
         # main stream's conv1 data gradient, so its duration is the shared-GPU one
         wn, wms = ks.get("ffn_conv1_wgrad.decoder", (0, float("nan")))
         wach = kflop / (wms * 1e-3) / 1e12 if wn else None
-        wtraffic, wtraffic_src = (pmc_traffic("wgrad") if not args.scaled else (None, None))
+        wtraffic, wtraffic_src = (pmc_traffic("wgrad", "gemm_ps_kernel<0, 64, 0, 1>")
+                                  if not args.scaled else (None, None))
         step_ms = elapsed / args.steps * 1e3
         step_tflops = train_flops(c, args.batch, Tp, Tm) * world / (step_ms * 1e-3) / 1e12
         fpf = train_flops(c, 1, 200, 1000) / 1000.0
@@ -450,7 +454,7 @@ def main():
                                    + (", single speaker" if args.single_speaker else ""),
                        "global_batch": args.batch * world, "seq_len": Tm,
                        "valid_mel_frames_per_step": frames_all, "parallelism": f"dp{world}"},
-            "roofline": {"bound": "mfma", "kernel": "decoder FFN conv1 (k=9) fwd: K-major GEMM with overlapping A rows over the reflect-padded X image (gemm_ps_kernel<0, 64, 0, 0>, bias + ReLU, pad rows dropped); the image copy (fs2_pad_rows) is a separate launch",
+            "roofline": {"bound": "mfma", "kernel": "decoder FFN conv1 (k=9) implicit-GEMM fwd (gemm256_kernel<true, true, 1, 0>, reflect conv in the loader, bias + ReLU epilogue)",
                          "achieved": achieved, "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": (achieved / MFMA_BF16_PEAK_TFLOPS) if achieved else None,
                          "traffic": traffic, "traffic_source": traffic_src,

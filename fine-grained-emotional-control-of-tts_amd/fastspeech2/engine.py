@@ -342,9 +342,15 @@ class FS2Engine:
     def _pad_fwd(self, wname, M, T):
         """FFN conv1 forward over a reflect-padded token-major X image (fs2_pad_rows + a plain
         GEMM whose A rows overlap, 2P dropped rows per utterance): tools/fwd_probe.py, B = 32:
-        decoder 374 -> 305 us, encoder 100 -> 89 (the implicit conv's per-K-tile reflect rows
-        and tap offsets are gone from the loader)"""
+        decoder 374 -> 305 us, encoder 100 -> 89 standalone (the implicit conv's per-K-tile
+        reflect rows and tap offsets are gone from the loader)"""
         O, C, KW = self._wspecs[wname]
+        # encoder only: the decoder's (M = 31264) measured no faster in the step on the product
+        # library (same box: 315-317 vs 314-315 us for gemm256_kernel's implicit conv) and the
+        # image copy costs 7 us; the encoder's gained 97 -> 91 us.  FS2_PAD_FWD=2 (experiments
+        # build): both.
+        if _PAD_FWD != 2 and not wname.startswith("encoder."):
+            return False
         return (self.dt == 1 and _PAD_FWD and KW > 1 and C % 64 == 0 and (KW - 1) // 2 < T and
                 self.w[wname][0].shape[1] == KW * C)
 
