@@ -2189,6 +2189,11 @@ int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
     const bool pk_fits = (long)p.M * p.lda * 2 < lim && (long)p.N * p.ldb * 2 < lim &&
                          crows * p.ldc * (p.c_fp32 ? 4 : 2) < lim &&
                          (long)p.mvalid * (p.gate ? p.ldg : p.ldr) * 2 < lim;
+    // the large-tile kernels address their operands through 32-bit buffer offsets (per batch
+    // entry); operands beyond 2 GiB take the pointer-based 128x128 kernel instead
+    const long a_rows = ak ? (long)(p.conv_mode ? p.M + 2L * p.conv_p : p.M) : (long)min(p.K, p.kvalid);
+    const long b_rows = bk ? (long)p.N : (long)min(p.K, p.kvalid);
+    const bool big_fits = a_rows * p.lda * 2 < lim && b_rows * p.ldb * 2 < lim;
     // persistent 256 x 256 / 256 x 192 kernel: long-K K-major GEMMs without gate / residual
     // operands (FS2_GEMM_NO_PS=1 restores the per-tile kernels for A/B runs)
     static const bool no_ps = getenv_flag("FS2_GEMM_NO_PS");
@@ -2235,6 +2240,12 @@ int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
         !p.accumulate && !(p.gate && p.residual) && (!ps_op || cm_ps == 0) && p.relu <= 1 && ps_k &&
         p.N >= 128 && pk_fits;
     if (p.c_row_t && !ps_go) return FS2_EINVAL;
+    if (!ps_go && !big_fits && p.conv_mode != 6) {
+      if (p.conv_mode == 2) launch4<T, false, true>(p, grid, s, ak, bk);
+      else launch4<T, true, true>(p, grid, s, ak, bk);
+      FS2_CHECK_LAUNCH();
+      return 0;
+    }
     if (ps_go) {
       GemmP q = p;
       q.g4_flags = getenv_int("FS2_PS_FLAGS", 0);

@@ -360,12 +360,15 @@ __global__ void __launch_bounds__(256) finalize_kernel(LossP p) {
     p.stats[5 * B + b] = cmn;
   }
   __syncthreads();
-  // utterance means of the five terms: fixed-order block sums (B <= 256) instead of a serial
-  // thread-0 loop of 5 B dependent loads
+  // utterance means of the five terms: fixed-order block sums (each thread's utterances
+  // b = tid, tid + 256, ... in order) instead of a serial thread-0 loop of 5 B dependent loads
   __shared__ float fsh[8];
   float t[5];
-  for (int k = 0; k < 5; ++k)
-    t[k] = block_sum(threadIdx.x < B ? p.per_b[k * B + threadIdx.x] : 0.f, fsh) / (float)B;
+  for (int k = 0; k < 5; ++k) {
+    float v = 0.f;
+    for (int b = threadIdx.x; b < B; b += 256) v += p.per_b[k * B + b];
+    t[k] = block_sum(v, fsh) / (float)B;
+  }
   if (threadIdx.x != 0) return;
   const float ssim_val = (float)(tot / ((double)B * p.npix));
   float l_ssim = 1.f - ssim_val;
@@ -527,7 +530,6 @@ extern "C" int fs2_loss_fwd_bwd(const fs2_loss_desc* d, void* stream) {
   if (d->B <= 0) return 0;
   if (d->Tm < WIN || d->NM < WIN) return FS2_EINVAL;  // SSIM: kernel larger than input
   if (d->NM > SSIM_MAXW) return FS2_EINVAL;           // SSIM LDS tiles
-  if (d->B > 256) return FS2_EINVAL;                  // finalize_kernel: one thread per utterance
   if (!d->mel_out || !d->postnet_out || !d->log_dur || !d->pitch_pred || !d->energy_pred ||
       !d->mel_tgt || !d->dur_tgt || !d->pitch_avg || !d->energy_avg || !d->mel_len ||
       !d->phon_len || !d->loss_out || !d->d_mel_out || !d->d_postnet_out || !d->d_log_dur ||

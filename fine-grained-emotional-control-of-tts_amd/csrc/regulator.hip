@@ -28,7 +28,8 @@ __global__ void embed_fwd_kernel(const int64_t* tok, const float* table, const f
 // adds each row chunk (lane = column) to its own LDS accumulator row of the token's id; the 4
 // wave accumulators are combined in a fixed order into part[chunk][v][64-column chunk], which
 // embed_bwd_reduce_kernel sums over the chunks in order.  (One block per vocabulary id that
-// rescanned every token took 68 us at M = 6400, V = 95.)
+// rescanned every token took 68 us at M = 6400, V = 95.)  Vocabularies larger than the LDS
+// accumulator take several id windows of EMB_VMAX, one per grid.z (ids v0 .. v0 + EMB_VMAX - 1).
 constexpr int EMB_CH = 16, EMB_VMAX = 128;
 template <typename T>
 __global__ void __launch_bounds__(256) embed_bwd_kernel(const int64_t* tok, const T* dX,
@@ -37,6 +38,7 @@ __global__ void __launch_bounds__(256) embed_bwd_kernel(const int64_t* tok, cons
   __shared__ float acc[4][EMB_VMAX][64];   // 128 KiB
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int d = blockIdx.x * 64 + lane;
+  const int v0 = blockIdx.z * EMB_VMAX, vn = min(EMB_VMAX, V - v0);
   for (int i = threadIdx.x; i < 4 * EMB_VMAX * 64; i += 256) (&acc[0][0][0])[i] = 0.f;
   __syncthreads();
   const int per = (M + EMB_CH - 1) / EMB_CH;
@@ -44,13 +46,13 @@ __global__ void __launch_bounds__(256) embed_bwd_kernel(const int64_t* tok, cons
   const int wper = (c1 - c0 + 3) / 4;
   const int m0 = c0 + w * wper, m1 = min(c1, m0 + wper);
   for (int m = m0; m < m1; ++m) {
-    const int v = (int)tok[m];
-    if (d < D && v >= 0 && v < V) acc[w][v][lane] += to_f(dX[(long)m * D + d]) * keep[m];
+    const int v = (int)tok[m] - v0;
+    if (d < D && v >= 0 && v < vn) acc[w][v][lane] += to_f(dX[(long)m * D + d]) * keep[m];
   }
   __syncthreads();
-  for (int v = w; v < V; v += 4)
+  for (int v = w; v < vn; v += 4)
     if (d < D)
-      part[((long)blockIdx.y * V + v) * D + d] =
+      part[((long)blockIdx.y * V + v0 + v) * D + d] =
           (acc[0][v][lane] + acc[1][v][lane]) + (acc[2][v][lane] + acc[3][v][lane]);
 }
 __global__ void embed_bwd_reduce_kernel(const float* part, int nch, long n, float* dtable) {
@@ -418,9 +420,9 @@ extern "C" int fs2_embed_bwd(const int64_t* tokens, const void* dX, const float*
                              int D, int V, float* dtable, float* workspace, int dtype,
                              void* stream) {
   if (M == 0 || V == 0) return 0;
-  if (!tokens || !dX || !keep || !dtable || !workspace || V > EMB_VMAX) return FS2_EINVAL;
+  if (!tokens || !dX || !keep || !dtable || !workspace || V < 0) return FS2_EINVAL;
   hipStream_t s = (hipStream_t)stream;
-  dim3 grid((D + 63) / 64, EMB_CH);
+  dim3 grid((D + 63) / 64, EMB_CH, (V + EMB_VMAX - 1) / EMB_VMAX);
   DISPATCH_T(dtype,
     hipLaunchKernelGGL(embed_bwd_kernel<bf16>, grid, dim3(256), 0, s, tokens, (const bf16*)dX, keep, M, D, V, workspace),
     hipLaunchKernelGGL(embed_bwd_kernel<float>, grid, dim3(256), 0, s, tokens, (const float*)dX, keep, M, D, V, workspace));

@@ -83,6 +83,16 @@ _NO_SIDE = N.exp_flag("FS2_NO_SIDE_STREAM")
 _NO_AUX = N.exp_flag("FS2_NO_AUX_STREAM")
 
 
+def ps_plain_ok(M, lda, N, ldb, out_rows, ldc, out_bytes):
+    """fs2_gemm can take a padded-domain GEMM (c_row output remap) only on its persistent
+    kernel: plain operands enabled (FS2_GEMM_NO_PS / FS2_PS_MODES bit 0 in the experiments
+    build) and every operand within the kernel's 32-bit buffer offsets -- otherwise the engine
+    keeps the implicit-conv path instead of handing fs2_gemm a call it refuses."""
+    lim = 0x7fffffff
+    return (not _NO_PS and bool(_PS_MODES & 1) and M * lda * 2 < lim and N * ldb * 2 < lim and
+            out_rows * ldc * out_bytes < lim)
+
+
 def eff_split(K, ns, bk):
     """the split-K slice count fs2_gemm actually uses for ``ns`` requested slices of K (it
     rounds the K-tiles per slice up, which can leave trailing slices empty -- those it zeroes
@@ -351,8 +361,10 @@ class FS2Engine:
         # build): both.
         if _PAD_FWD != 2 and not wname.startswith("encoder."):
             return False
-        return (self.dt == 1 and _PAD_FWD and KW > 1 and C % 64 == 0 and (KW - 1) // 2 < T and
-                self.w[wname][0].shape[1] == KW * C)
+        P = (KW - 1) // 2
+        return (self.dt == 1 and _PAD_FWD and KW > 1 and C % 64 == 0 and P < T and
+                self.w[wname][0].shape[1] == KW * C and
+                ps_plain_ok((M // T) * (T + 2 * P), C, O, KW * C, M, O, 2))
 
     def _dgrad(self, dY, lddy, M, T, wname, out, ldo, n_out=None, **epi):
         tag = self._dtag("dgrad", wname, T)
@@ -375,25 +387,44 @@ class FS2Engine:
         O, C, KW = self._wspecs[wname]
         return KW > 1 and self._km_ok(O, C, KW, KW, None)
 
+    def _pad_dgrad_fits(self, wname, B, T):
+        """the padded data gradient's GEMM within the persistent kernel's 32-bit offsets"""
+        O, C, KW = self._wspecs[wname]
+        P = (KW - 1) // 2
+        Mp = B * (T + 2 * P)
+        # the image (Mp + 2P rows of O), the weight image, the fp32 padded-domain output, and
+        # conv2's data gradient written into the image (c_row = (T, 2P))
+        return (ps_plain_ok(Mp + 2 * P, O, C, KW * O, Mp, C, 4) and
+                ps_plain_ok(B * T, O, O, O, Mp + 2 * P, O, 2))
+
     def _dy_image(self, key, B, T, P, F):
         """zero-padded token-major image for a k = 2P+1 conv data gradient: 2P zero rows, then
         per utterance T data rows and 2P zero rows (the last P are the end guard); returns
         (image from its first row, data view from the first utterance's row 0).  Token (b, t)
-        sits at data row b*T + t remapped to b*(T+2P) + t (fs2_gemm c_row = (T, 2P)).  One
-        buffer per layer (``key``), kept across steps: only its data rows are ever written, so
-        its pad rows -- zeroed through a view starting T rows before the image -- need zeroing
-        only when the batch shape changes (stream order keeps the reuse safe: the next step's
-        main-stream work follows this step's side-stream join)."""
+        sits at data row b*T + t remapped to b*(T+2P) + t (fs2_gemm c_row = (T, 2P)).
+
+        Eager steps keep one buffer per layer (``key``) across steps: only its data rows are
+        ever written, so its pad rows -- zeroed through a view starting T rows before the image
+        -- need zeroing only when the batch shape changes (stream order keeps the reuse safe:
+        the next step's main-stream work follows this step's side-stream join).  A step being
+        captured into a HIP graph gets its own image from the graph's memory pool with the
+        pad-row zeroing captured too, so replays of graphs of other shapes (FusedTrainer keeps
+        several) never share or re-lay-out a buffer another graph writes."""
         L = T + 2 * P
         n = (B + 1) * L * F
         shape = (B, T, P, F)
-        ent = self._img.get(key)
-        if ent is None or ent[0] != shape:
-            buf = ent[1] if ent is not None and ent[1].numel() >= n else \
-                torch.empty(n, dtype=self.adt, device=self.dev)
-            buf[:n].view(B + 1, L, F)[:, T:].zero_()
-            ent = self._img[key] = (shape, buf)
-        img = ent[1][:n].view((B + 1) * L, F)[T:]
+        if torch.cuda.is_current_stream_capturing():
+            buf = torch.empty(n, dtype=self.adt, device=self.dev)
+            buf.view(B + 1, L, F)[:, T:].zero_()
+        else:
+            ent = self._img.get(key)
+            if ent is None or ent[0] != shape:
+                buf = ent[1] if ent is not None and ent[1].numel() >= n else \
+                    torch.empty(n, dtype=self.adt, device=self.dev)
+                buf[:n].view(B + 1, L, F)[:, T:].zero_()
+                ent = self._img[key] = (shape, buf)
+            buf = ent[1]
+        img = buf[:n].view((B + 1) * L, F)[T:]
         return img, img[2 * P:]
 
     def _dgrad_impl(self, dY, lddy, M, T, wname, out, ldo, n_out=None, **epi):
@@ -452,13 +483,26 @@ class FS2Engine:
 
     def _km_image(self, key, C, ld):
         """bf16 [C][ld] image with a zeroed guard of 64 elements before row 0 and after the
-        last row (the tap-shifted reads of conv_mode 6 reach P elements past either end)"""
-        k = (key, C, ld)
-        buf = self._km.get(k)
-        if buf is None:
-            buf = torch.zeros(C * ld + 128, dtype=torch.bfloat16, device=self.dev)
-            self._km[k] = buf
-        return buf[64:64 + C * ld]
+        last row (the tap-shifted reads of conv_mode 6 reach P elements past either end).
+        One buffer per (key, C), grown to the largest C*ld seen and re-guarded when ld changes
+        (ld follows the batch's T, so a per-ld cache would grow without bound over an epoch);
+        it lives on the side stream, whose layers use it one after another.  A captured step
+        gets its own zeroed image from the graph's pool (see _dy_image)."""
+        n = C * ld
+        if torch.cuda.is_current_stream_capturing():
+            return torch.zeros(n + 128, dtype=torch.bfloat16, device=self.dev)[64:64 + n]
+        k = (key, C)
+        ent = self._km.get(k)
+        if ent is None or ent[1].numel() < n + 128:
+            buf = torch.zeros(n + 128, dtype=torch.bfloat16, device=self.dev)
+            self._km[k] = (ld, buf)
+        elif ent[0] != ld:
+            buf = ent[1]
+            buf[64 + n:64 + n + 64].zero_()   # the end guard of the new layout
+            self._km[k] = (ld, buf)
+        else:
+            buf = ent[1]
+        return buf[64:64 + n]
 
     def _wgrad_km(self, dY, lddy, X, ldx, M, T, wname, gemm_tag=None, bias=None, dy_img=None):
         """grad[O][KW][C] += sum_{b,t} dY[b,t,o] X[b, reflect(t+j-P), c] with both GEMM operands
@@ -639,6 +683,10 @@ class FS2Engine:
         w2 = prefix + "pos_ffn.2.conv.weight"
         w1 = prefix + "pos_ffn.0.conv.weight"
         pad = self._pad_dgrad(w1)
+        if pad and not self._pad_dgrad_fits(w1, B, T):
+            # the weight images of this conv were built tap-reversed for the padded path
+            raise ValueError(f"{w1}: batch of {B} x {T} tokens exceeds the 32-bit offsets of the "
+                             "padded conv data gradient; split the batch")
         if pad:   # conv2's data gradient lands in the zero-padded image conv1's reads
             P1 = (self._wspecs[w1][2] - 1) // 2
             img, dHc = self._dy_image(prefix, B, T, P1, F)

@@ -22,8 +22,10 @@ Differences, each deliberate:
   and the attention masks tile across the batch (App. B-1), so a sentence's mel can depend on
   the batch it shares.  ``synthesize(..., batched=False)`` runs one sentence per call, which is
   the reference loop exactly;
-* the HiFi-GAN vocoder (speechbrain hub weights) is not available offline and is out of scope
-  (DESIGN.md section 7): the outputs are mel spectrograms.
+* ``synthesize`` returns mel spectrograms; ``vocode`` then decodes them the way the reference
+  does (inference.py:82-83: ``model(...)[0].permute(0, 2, 1)`` -> ``vocoder.decode_batch``) with
+  the HIP HiFi-GAN generator of ``fastspeech2.vocoder`` (architecture only: the
+  speechbrain hub weights are not available offline).
 """
 
 import numpy as np
@@ -100,3 +102,22 @@ def intensity_sweep_batch(phoneme, n_speakers, emotions, levels, intensity_bank,
                 inten.append(get_intensity_rep(s, e, lv, T, intensity_bank, n_emotions)[0])
                 keys.append((s, e, lv))
     return ph, spk, inten, keys
+
+
+@torch.no_grad()
+def vocode(vocoder, mels, n_mels=80):
+    """Waveforms for ``synthesize``'s mels: the list is zero-padded to its longest mel into ONE
+    (B, n_mels, T_max) batch -- the padded ``model(...)[0].permute(0, 2, 1)`` the reference
+    hands to ``vocoder.decode_batch`` (inference.py:82-83) -- and decoded by ``vocoder`` (a
+    ``fastspeech2.vocoder.HifiganGenerator``).  Returns (wav (B, 1, hop * (T_max + 10)),
+    per-sentence valid sample counts hop * T_i)."""
+    dev = next(vocoder.parameters()).device
+    B = len(mels)
+    T = max(1, max(int(m.shape[0]) for m in mels))
+    batch = torch.zeros(B, n_mels, T, dtype=torch.float32, device=dev)
+    for i, m in enumerate(mels):
+        if m.shape[0]:
+            batch[i, :, :m.shape[0]] = m.to(device=dev, dtype=torch.float32).t()
+    wav = vocoder.decode_batch(batch)
+    hop = wav.shape[-1] // (T + 2 * vocoder.hp["inference_padding"])
+    return wav, [hop * int(m.shape[0]) for m in mels]
