@@ -11,7 +11,7 @@
 // the IntensityExtractor's src_key_padding_mask (rank_model/model.py:35,101).  A fully masked row yields NaN, as torch's softmax does.
 //
 // One wave per (z, query) row; scores fp32, probabilities stored in the activation dtype.
-// Dropout: fs2_keep_fast over element index row * round_up(Tk, 2) + k (same draw as flash.hip).
+// Dropout: fs2_attn_keep(dkey, row, k) (fs2_common.h; the same draw as flash.hip).
 #include "fs2_common.h"
 
 namespace {
@@ -51,7 +51,7 @@ __global__ void __launch_bounds__(256) softmax_fwd_kernel(const float* S, const 
     if (pdrow) {
       float q = pv;
       if (p_drop > 0.f && k < Tk)
-        q = fs2_keep_fast(dkey, (uint64_t)row * ((Tk + 1) & ~1) + k, thr) ? pv * inv_keep : 0.f;
+        q = fs2_attn_keep(dkey, (uint32_t)row, (uint32_t)k, thr) ? pv * inv_keep : 0.f;
       pdrow[k] = from_f<T>(q);
     }
   }
@@ -72,7 +72,7 @@ __global__ void __launch_bounds__(256) softmax_bwd_kernel(const float* dPd, cons
   float dot = 0.f;
   for (int k = lane; k < Tk; k += 64) {
     float gv = g[k];
-    if (p_drop > 0.f) gv = fs2_keep_fast(dkey, (uint64_t)row * ((Tk + 1) & ~1) + k, thr) ? gv * inv_keep : 0.f;
+    if (p_drop > 0.f) gv = fs2_attn_keep(dkey, (uint32_t)row, (uint32_t)k, thr) ? gv * inv_keep : 0.f;
     dot += gv * to_f(prow[k]);
   }
   dot = wave_sum(dot);
@@ -81,7 +81,7 @@ __global__ void __launch_bounds__(256) softmax_bwd_kernel(const float* dPd, cons
     float v = 0.f;
     if (k < Tk) {
       float gv = g[k];
-      if (p_drop > 0.f) gv = fs2_keep_fast(dkey, (uint64_t)row * ((Tk + 1) & ~1) + k, thr) ? gv * inv_keep : 0.f;
+      if (p_drop > 0.f) gv = fs2_attn_keep(dkey, (uint32_t)row, (uint32_t)k, thr) ? gv * inv_keep : 0.f;
       v = scale * to_f(prow[k]) * (gv - dot);
     }
     drow[k] = from_f<T>(v);

@@ -23,6 +23,7 @@
 // LDS tiles [rows][dh] bf16 with 16-byte chunk c stored at c ^ (row & 7): conflict-free for
 // both the ds_read_b128 (row-major fragment) and the ds_read_b64_tr_b16 (transposed) reads.
 #include <cstdlib>
+#include <type_traits>
 
 #include "fs2_common.h"
 
@@ -53,6 +54,7 @@ struct AttnP {
   float scale, scale_log2, p_drop, inv_keep;
   uint32_t seed, salt;
   uint32_t thr16;                // dropout threshold (fs2_thr16)
+  int xflags;                    // FS2_ATTN_FLAGS (experiments build only: timing bits, WRONG results)
 };
 
 __device__ __forceinline__ bf16x8 ld_frag(const bf16* g) { return *(const bf16x8*)g; }
@@ -81,6 +83,36 @@ __device__ __forceinline__ bf16x8 lds_tr_frag(const char* t, int rowbytes, int r
   const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a2);
   const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   return __builtin_bit_cast(bf16x8, v);
+}
+
+// The same transposed fragment read through inline asm.  hipcc's waitcnt pass treats a
+// ds_read_tr16_b64 builtin as a read that may alias ANY in-flight LDS-DMA and puts an
+// s_waitcnt vmcnt(0) in front of it -- which drained the next tile's K/V (Q/dO) prefetch in the
+// middle of every tile (profiles/r04_attention_pmc.json: SQ_WAIT_ANY 44-51 % of wave cycles).
+// The asm read is invisible to that pass; its results are retired by lds_wait<N> below.
+__device__ __forceinline__ uint32_t lds_off(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+struct TrFrag { s16x4 lo, hi; };
+__device__ __forceinline__ void lds_tr_frag_issue(TrFrag& f, const char* t, int rowbytes, int rbase,
+                                                  int m0, int lane) {
+  const int li = lane & 15, g = lane >> 4, q = li >> 2, p = li & 3;
+  const int m = m0 + 4 * p;
+  const int c = m >> 3, boff = (m & 7) * 2;
+  const int k1 = rbase + 4 * g + q, k2 = k1 + 16;
+  const char* a1 = t + k1 * rowbytes + ((c ^ (k1 & 7)) << 4) + boff;
+  const char* a2 = t + k2 * rowbytes + ((c ^ (k2 & 7)) << 4) + boff;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(f.lo) : "v"(lds_off(a1)));
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(f.hi) : "v"(lds_off(a2)));
+}
+__device__ __forceinline__ bf16x8 tr_val(const TrFrag& f) {
+  const s16x8 v = {f.lo[0], f.lo[1], f.lo[2], f.lo[3], f.hi[0], f.hi[1], f.hi[2], f.hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+// retire all but the N youngest LDS reads; the fragments named are the ones being consumed
+template <int N>
+__device__ __forceinline__ void lds_wait(TrFrag& a, TrFrag& b) {
+  asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(a.lo), "+v"(a.hi), "+v"(b.lo), "+v"(b.hi) : "n"(N));
 }
 
 // rows [r0, r0 + NR) of a [rows][DH] column block starting at src (row pitch ld) -> LDS tile
@@ -154,74 +186,132 @@ __device__ __forceinline__ bf16x8 pack8(const float* a, const float* b) {
   return r;
 }
 
+// max / sum over the 4 lane groups (lanes l, l ^ 16, l ^ 32, l ^ 48) of a 16x16 C fragment: the
+// gfx950 permlane swaps are VALU ops (the __shfl_xor they replace went through ds_bpermute)
 __device__ __forceinline__ float xg_max(float v) {
-  v = fmaxf(v, __shfl_xor(v, 16, 64));
-  return fmaxf(v, __shfl_xor(v, 32, 64));
+  const auto a = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, v),
+                                                  __builtin_bit_cast(unsigned, v), false, false);
+  v = fmaxf(__builtin_bit_cast(float, (unsigned)a[0]), __builtin_bit_cast(float, (unsigned)a[1]));
+  const auto b = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, v),
+                                                  __builtin_bit_cast(unsigned, v), false, false);
+  return fmaxf(__builtin_bit_cast(float, (unsigned)b[0]), __builtin_bit_cast(float, (unsigned)b[1]));
 }
 __device__ __forceinline__ float xg_sum(float v) {
-  v += __shfl_xor(v, 16, 64);
-  return v + __shfl_xor(v, 32, 64);
+  const auto a = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, v),
+                                                  __builtin_bit_cast(unsigned, v), false, false);
+  v = __builtin_bit_cast(float, (unsigned)a[0]) + __builtin_bit_cast(float, (unsigned)a[1]);
+  const auto b = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, v),
+                                                  __builtin_bit_cast(unsigned, v), false, false);
+  return __builtin_bit_cast(float, (unsigned)b[0]) + __builtin_bit_cast(float, (unsigned)b[1]);
 }
 
-// key-valid flags for (b, h) and the end of the last valid key
-__device__ __forceinline__ int build_kvalid(uint8_t* kval, int* kend_s, const AttnP& p, int b,
-                                            int h) {
+// compile-time loop: f(std::integral_constant<int, I>) for I in [I0, N)
+template <int I, int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
+  }
+}
+
+// XCD-aware block coordinates: blocks are dispatched round-robin over the 8 XCDs in linear
+// order (x fastest), which put the query (or key) blocks of one (b, h) on 8 DIFFERENT XCDs --
+// each XCD's L2 then fetched every K/V (Q/dO) tile of every (b, h) from the Infinity Cache:
+// ~390 MB per decoder forward against 48 MB of K/V.  Remapped (bijectively, as the GEMMs' T1
+// swizzle) so that an XCD's blocks cover whole (b, h) groups, whose tiles its L2 then serves.
+__device__ __forceinline__ void attn_block_coords(int& blk, int& z) {
+  const int nb = gridDim.x, n = nb * gridDim.y;
+  const int orig = blockIdx.x + nb * blockIdx.y;
+  const int xcd = orig & 7, q = n >> 3, r = n & 7;
+  const int id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  z = id / nb;
+  blk = id - z * nb;
+}
+
+// key-valid flags for (b, h); returns the end of the last valid key and sets *kfull to the
+// first masked key (keys below it are all valid: the tiles entirely below it skip the per-key
+// mask -- with the decoder's length masks that is every tile but the last)
+__device__ __forceinline__ int build_kvalid(uint8_t* kval, int* kbuf, const AttnP& p, int b,
+                                            int h, int* kfull) {
   const int b2 = p.tiled ? (b * p.H + h) % p.B : b;
   const uint8_t* k1 = p.kpad + (long)b * p.T;
   const uint8_t* k2 = p.kpad + (long)b2 * p.T;
-  if (threadIdx.x == 0) *kend_s = 0;
-  __syncthreads();
-  int last = 0;
   const int tpad = (p.T + 63) & ~63;   // bytes past T read as masked (word reads of 4 keys)
+  if (threadIdx.x == 0) { kbuf[0] = 0; kbuf[1] = tpad; }
+  __syncthreads();
+  int last = 0, first = tpad;
   for (int j = threadIdx.x; j < tpad; j += blockDim.x) {
     const uint8_t v = j < p.T ? !(k1[j] | k2[j]) : 0;
     kval[j] = v;
     if (v) last = j + 1;
+    else first = min(first, j);
   }
-  atomicMax(kend_s, last);
+  atomicMax(&kbuf[0], last);
+  atomicMin(&kbuf[1], first);
   __syncthreads();
-  return *kend_s;
+  *kfull = kbuf[1];
+  return kbuf[0];
+}
+
+// per-lane dropout constants of a query-owning lane (forward, dQ): the fs2_attn_mix inputs of
+// its row for the pairs (kt, e) of a tile at key 0 -- tile k0 adds (k0 / 2) * FS2_ATTN_KC
+__device__ __forceinline__ void drop_lane_consts(uint32_t (&c)[4][2], uint32_t dkey, uint32_t row,
+                                                 int g) {
+  const uint32_t rh = fs2_attn_rowhash(dkey, row);
+#pragma unroll
+  for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+    for (int e = 0; e < 2; ++e) c[kt][e] = rh + (uint32_t)(kt * 8 + 2 * g + e) * FS2_ATTN_KC;
 }
 
 // ------------------------------------------------------------------------------ forward
 // block: 16 * W8 queries = (W8 / QG) waves x QG 16-query groups; K/V tiles of 64 keys
-// (W8 = 8: 128 queries; W8 = 4 for short sequences, so B*H*ceil(T/64) blocks fill the chip)
+// (W8 = 8: 128 queries; W8 = 4 for short sequences, so B*H*ceil(T/64) blocks fill the chip).
+// Per-element VALU is what bounds this loop (one 16x16x32 MFMA leaves issue room for two VALU
+// instructions): raw scores feed the row max, the scale folds into the exponent's FMA, full
+// tiles skip the key mask, and dropout is one add + one 24-bit multiply round per key pair.
 template <int DH, int QG, int W8 = 8>
 __global__ void __launch_bounds__(W8 * 64 / QG, 1) attn_fwd_kernel(AttnP p) {
   constexpr int NT = W8 * 64 / QG;
   constexpr int NS = DH / 32, ND = DH / 16;
   constexpr int TB = 64 * DH * 2;
   // one LDS array (a second __shared__ object can make hipcc drain the DMA ring early):
-  // [tile buffer 0: 2 tensors | tile buffer 1: 2 tensors | kval | kend]
+  // [tile buffer 0: 2 tensors | tile buffer 1: 2 tensors | kval | kend, kfull]
   __shared__ __attribute__((aligned(16))) char smem[4 * TB + TMAX + 16];
   uint8_t* kval = (uint8_t*)(smem + 4 * TB);
-  int& kend_s = *(int*)(smem + 4 * TB + TMAX);
+  int* kbuf = (int*)(smem + 4 * TB + TMAX);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
-  const int z = blockIdx.y, b = z / p.H, h = z - b * p.H;
+  int blk, z;
+  attn_block_coords(blk, z);
+  const int b = z / p.H, h = z - b * p.H;
   const uint32_t dkey = fs2_drop_key(p.seed, p.salt);
-  const uint64_t T2 = (uint64_t)((p.T + 1) & ~1);   // dropout rows padded to even length
-  const int kend = build_kvalid(kval, &kend_s, p, b, h);
+  const bool drop = p.p_drop > 0.f;
+  int kfull;
+  const int kend = build_kvalid(kval, kbuf, p, b, h, &kfull);
   const bf16* Qb = p.qkv + (long)b * p.T * p.ldq + h * DH;
   const bf16* Kb = Qb + p.D;
   const bf16* Vb = Qb + 2 * p.D;
+  const float c = p.scale_log2;
 
   int qi[QG];
   bf16x8 qf[QG][NS];
+  uint32_t dc[QG][4][2];
 #pragma unroll
   for (int qg = 0; qg < QG; ++qg) {
-    qi[qg] = blockIdx.x * (16 * W8) + wave * 16 * QG + qg * 16 + (lane & 15);
+    qi[qg] = blk * (16 * W8) + wave * 16 * QG + qg * 16 + (lane & 15);
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
       if (qi[qg] < p.T) qf[qg][s] = ld_frag(Qb + (long)qi[qg] * p.ldq + 32 * s + 8 * g);
       else qf[qg][s] = bf16x8{};
     }
+    drop_lane_consts(dc[qg], dkey, (uint32_t)(z * p.T + qi[qg]), g);
   }
   f32x4 oacc[ND][QG];
 #pragma unroll
   for (int d = 0; d < ND; ++d)
 #pragma unroll
     for (int qg = 0; qg < QG; ++qg) oacc[d][qg] = f32x4{0, 0, 0, 0};
-  float mrow[QG], lrow[QG];
+  float mrow[QG], lrow[QG];   // raw-score row max, row sum of exp2(c * (s - max))
 #pragma unroll
   for (int qg = 0; qg < QG; ++qg) { mrow[qg] = -INFINITY; lrow[qg] = 0.f; }
 
@@ -237,9 +327,14 @@ __global__ void __launch_bounds__(W8 * 64 / QG, 1) attn_fwd_kernel(AttnP p) {
   }
   for (int t = 0; t < ntile; ++t) {
     const int k0 = t * 64;
-    const char* Ks = smem + (t & 1) * 2 * TB;
+#ifdef FS2_EXPERIMENTS
+    const int tb = (p.xflags & 2) ? 0 : t;
+#else
+    const int tb = t;
+#endif
+    const char* Ks = smem + (tb & 1) * 2 * TB;
     const char* Vs = Ks + TB;
-    if (t + 1 < ntile) {
+    if (t + 1 < ntile && tb == t) {
       char* nx = smem + ((t + 1) & 1) * 2 * TB;
       dma.issue(nx, rsK, p.ldq, k0 + 64, p.T, wave);
       dma.issue(nx + TB, rsV, p.ldq, k0 + 64, p.T, wave);
@@ -254,55 +349,94 @@ __global__ void __launch_bounds__(W8 * 64 / QG, 1) attn_fwd_kernel(AttnP p) {
     for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
       for (int qg = 0; qg < QG; ++qg) sacc[kt][qg] = f32x4{0, 0, 0, 0};
+    // S^T = K Q^T with the K fragments two 32-dim steps ahead of their MFMAs (a 3-deep register
+    // ring, order pinned by sched_group_barrier): the compiler's own schedule read each fragment
+    // one or two MFMAs ahead, so every MFMA waited out most of an LDS read latency
+    bf16x8 kb[3][4];
 #pragma unroll
-    for (int s = 0; s < NS; ++s)
+    for (int s = 0; s < 2; ++s)
 #pragma unroll
-      for (int kt = 0; kt < 4; ++kt) {
-        const bf16x8 kf = lds_row_frag(Ks, DH * 2, kt * 16 + (lane & 15), 4 * s + g);
+      for (int kt = 0; kt < 4; ++kt) kb[s][kt] = lds_row_frag(Ks, DH * 2, kt * 16 + (lane & 15), 4 * s + g);
+    static_for<0, NS>([&](auto SI) {
+      constexpr int s = decltype(SI)::value;
+      if constexpr (s + 2 < NS) {
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+          kb[(s + 2) % 3][kt] = lds_row_frag(Ks, DH * 2, kt * 16 + (lane & 15), 4 * (s + 2) + g);
+        __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+      }
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
         for (int qg = 0; qg < QG; ++qg)
-          sacc[kt][qg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qg][s], sacc[kt][qg], 0, 0, 0);
-      }
+          sacc[kt][qg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kb[s % 3][kt], qf[qg][s], sacc[kt][qg], 0, 0, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 4 * QG, 0);
+    });
+    const bool full = k0 + 64 <= kfull;
+    const uint32_t tkc = (uint32_t)(k0 >> 1) * FS2_ATTN_KC;
     bf16x8 pf[QG][2];
+#ifdef FS2_EXPERIMENTS
+    if (p.xflags & 1) {
+#pragma unroll
+      for (int qg = 0; qg < QG; ++qg) {
+        float pd[4][4];
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) pd[kt][r] = sacc[kt][qg][r];
+        pf[qg][0] = pack8(pd[0], pd[1]);
+        pf[qg][1] = pack8(pd[2], pd[3]);
+      }
+    } else
+#endif
 #pragma unroll
     for (int qg = 0; qg < QG; ++qg) {
       float v[4][4];
       float mt = -INFINITY;
+      if (full) {
 #pragma unroll
-      for (int kt = 0; kt < 4; ++kt) {
-        const uint32_t kw = *(const uint32_t*)(kval + k0 + kt * 16 + 4 * g);   // keys 4g..4g+3
+        for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const bool ok = (kw >> (8 * r)) & 1u;
-          v[kt][r] = ok ? sacc[kt][qg][r] * p.scale_log2 : -INFINITY;
-          mt = fmaxf(mt, v[kt][r]);
+          for (int r = 0; r < 4; ++r) {
+            v[kt][r] = sacc[kt][qg][r];
+            mt = fmaxf(mt, v[kt][r]);
+          }
+      } else {
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt) {
+          const uint32_t kw = *(const uint32_t*)(kval + k0 + kt * 16 + 4 * g);   // keys 4g..4g+3
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            v[kt][r] = (kw >> (8 * r)) & 1u ? sacc[kt][qg][r] : -INFINITY;
+            mt = fmaxf(mt, v[kt][r]);
+          }
         }
       }
       mt = xg_max(mt);
       const float mnew = fmaxf(mrow[qg], mt);
-      const float alpha = mnew == -INFINITY ? 1.f : fexp2(mrow[qg] - mnew);
+      const float alpha = mnew == -INFINITY ? 1.f : fexp2((mrow[qg] - mnew) * c);
+      const float nmc = mnew == -INFINITY ? 0.f : -mnew * c;
       mrow[qg] = mnew;
       float ls = 0.f;
       float pd[4][4];
-      const uint64_t rowi = ((uint64_t)z * p.T + qi[qg]) * T2;
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float e = v[kt][r] == -INFINITY ? 0.f : fexp2(v[kt][r] - mnew);
+          const float e = fexp2(fmaf(v[kt][r], c, nmc));   // masked: exp2(-inf) = 0
           ls += e;
           pd[kt][r] = e;
         }
-      if (p.p_drop > 0.f) {
+      if (drop) {
+        // key pair (k0 + 16 kt + 4g + 2e) / 2; the 1 / (1 - p) of the kept probabilities is
+        // applied once, to O at the end
 #pragma unroll
         for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-          for (int r = 0; r < 4; r += 2) {
-            const uint64_t idx = rowi + k0 + kt * 16 + 4 * g + r;   // even
-            const uint32_t h = fs2_hash_pair(dkey, idx >> 1);
-            // the 1 / (1 - p) of the kept probabilities is applied once, to O at the end
-            pd[kt][r] = fs2_keep_pair_bit(h, idx, p.thr16) ? pd[kt][r] : 0.f;
-            pd[kt][r + 1] = fs2_keep_pair_bit(h, idx + 1, p.thr16) ? pd[kt][r + 1] : 0.f;
+          for (int e = 0; e < 2; ++e) {
+            const uint32_t hh = fs2_attn_mix(dc[qg][kt][e] + tkc);
+            pd[kt][2 * e] = (hh & 0xffffu) >= p.thr16 ? pd[kt][2 * e] : 0.f;
+            pd[kt][2 * e + 1] = (hh >> 16) >= p.thr16 ? pd[kt][2 * e + 1] : 0.f;
           }
       }
       lrow[qg] = lrow[qg] * alpha + ls;
@@ -313,15 +447,31 @@ __global__ void __launch_bounds__(W8 * 64 / QG, 1) attn_fwd_kernel(AttnP p) {
       pf[qg][0] = pack8(pd[0], pd[1]);
       pf[qg][1] = pack8(pd[2], pd[3]);
     }
+    // O^T += V^T P^T, the V^T fragments (two transposed reads each, asm: see lds_tr_frag_issue)
+    // two output blocks ahead of their MFMAs, retired by counted lgkmcnt waits
+    TrFrag vb[3][2];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the softmax's LDS reads retired
 #pragma unroll
-    for (int d = 0; d < ND; ++d)
+    for (int d = 0; d < 2; ++d)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const bf16x8 vf = lds_tr_frag(Vs, DH * 2, 32 * j, 16 * d, lane);
+      for (int j = 0; j < 2; ++j) lds_tr_frag_issue(vb[d][j], Vs, DH * 2, 32 * j, 16 * d, lane);
+    static_for<0, ND>([&](auto DI) {
+      constexpr int d = decltype(DI)::value;
+      if constexpr (d + 2 < ND) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) lds_tr_frag_issue(vb[(d + 2) % 3][j], Vs, DH * 2, 32 * j, 16 * (d + 2), lane);
+        lds_wait<8>(vb[d % 3][0], vb[d % 3][1]);
+      } else if constexpr (d + 1 < ND) {
+        lds_wait<4>(vb[d % 3][0], vb[d % 3][1]);
+      } else {
+        lds_wait<0>(vb[d % 3][0], vb[d % 3][1]);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int qg = 0; qg < QG; ++qg)
-          oacc[d][qg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[qg][j], oacc[d][qg], 0, 0, 0);
-      }
+          oacc[d][qg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_val(vb[d % 3][j]), pf[qg][j], oacc[d][qg], 0, 0, 0);
+    });
     __builtin_amdgcn_s_barrier();   // every wave is done with buffer t & 1 before t+2 lands
   }
 #pragma unroll
@@ -329,7 +479,7 @@ __global__ void __launch_bounds__(W8 * 64 / QG, 1) attn_fwd_kernel(AttnP p) {
     const float l = xg_sum(lrow[qg]);
     const float inv = p.inv_keep / l;
     if (qi[qg] >= p.T) continue;
-    if (g == 0) p.lse[(long)z * p.T + qi[qg]] = mrow[qg] + log2f(l);
+    if (g == 0) p.lse[(long)z * p.T + qi[qg]] = mrow[qg] * c + log2f(l);
     bf16* orow = p.out + ((long)b * p.T + qi[qg]) * p.ldout + h * DH;
 #pragma unroll
     for (int d = 0; d < ND; ++d) {
@@ -345,33 +495,38 @@ __global__ void __launch_bounds__(W8 * 64 / QG, 1) attn_fwd_kernel(AttnP p) {
 }
 
 // ------------------------------------------------------------------------------ backward dQ
-// block: 16 * W8 queries = (W8 / QG) waves x QG 16-query groups; also writes
-// D = rowsum(dO * O) for the dK/dV kernel
+// block: 16 * W8 queries = (W8 / QG) waves x QG 16-query groups; also writes D = rowsum(dO * O)
+// and the dropout row hash of every query row (workspace) for the dK/dV kernel
 template <int DH, int QG, int W8 = 8>
 __global__ void __launch_bounds__(W8 * 64 / QG, 1) attn_bwd_dq_kernel(AttnP p) {
   constexpr int NT = W8 * 64 / QG;
   constexpr int NS = DH / 32, ND = DH / 16;
   constexpr int TB = 64 * DH * 2;
   // one LDS array (a second __shared__ object can make hipcc drain the DMA ring early):
-  // [tile buffer 0: 2 tensors | tile buffer 1: 2 tensors | kval | kend]
+  // [tile buffer 0: 2 tensors | tile buffer 1: 2 tensors | kval | kend, kfull]
   __shared__ __attribute__((aligned(16))) char smem[4 * TB + TMAX + 16];
   uint8_t* kval = (uint8_t*)(smem + 4 * TB);
-  int& kend_s = *(int*)(smem + 4 * TB + TMAX);
+  int* kbuf = (int*)(smem + 4 * TB + TMAX);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
-  const int z = blockIdx.y, b = z / p.H, h = z - b * p.H;
+  int blk, z;
+  attn_block_coords(blk, z);
+  const int b = z / p.H, h = z - b * p.H;
   const uint32_t dkey = fs2_drop_key(p.seed, p.salt);
-  const uint64_t T2 = (uint64_t)((p.T + 1) & ~1);   // dropout rows padded to even length
-  const int kend = build_kvalid(kval, &kend_s, p, b, h);
+  const bool drop = p.p_drop > 0.f;
+  int kfull;
+  const int kend = build_kvalid(kval, kbuf, p, b, h, &kfull);
   const bf16* Qb = p.qkv + (long)b * p.T * p.ldq + h * DH;
   const bf16* Kb = Qb + p.D;
   const bf16* Vb = Qb + 2 * p.D;
+  const float c = p.scale_log2;
 
   int qi[QG];
   bf16x8 qf[QG][NS], dof[QG][NS];
-  float lse[QG], dsum[QG];
+  float nlse[QG], dsum[QG];
+  uint32_t dc[QG][4][2];
 #pragma unroll
   for (int qg = 0; qg < QG; ++qg) {
-    qi[qg] = blockIdx.x * (16 * W8) + wave * 16 * QG + qg * 16 + (lane & 15);
+    qi[qg] = blk * (16 * W8) + wave * 16 * QG + qg * 16 + (lane & 15);
     const bool in = qi[qg] < p.T;
     float dot = 0.f;
 #pragma unroll
@@ -388,9 +543,14 @@ __global__ void __launch_bounds__(W8 * 64 / QG, 1) attn_bwd_dq_kernel(AttnP p) {
         dof[qg][s] = bf16x8{};
       }
     }
-    lse[qg] = in ? p.lse[(long)z * p.T + qi[qg]] : 0.f;
+    nlse[qg] = in ? -p.lse[(long)z * p.T + qi[qg]] : 0.f;
     dsum[qg] = xg_sum(dot);
-    if (in && g == 0) p.dsum[(long)z * p.T + qi[qg]] = dsum[qg];
+    const uint32_t row = (uint32_t)(z * p.T + qi[qg]);
+    drop_lane_consts(dc[qg], dkey, row, g);
+    if (in && g == 0) {
+      p.dsum[(long)z * p.T + qi[qg]] = dsum[qg];
+      ((uint32_t*)p.dsum)[(long)p.B * p.H * p.T + (long)z * p.T + qi[qg]] = fs2_attn_rowhash(dkey, row);
+    }
   }
   f32x4 qacc[ND][QG];
 #pragma unroll
@@ -439,26 +599,26 @@ __global__ void __launch_bounds__(W8 * 64 / QG, 1) attn_bwd_dq_kernel(AttnP p) {
           pacc[kt][qg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, dof[qg][s], pacc[kt][qg], 0, 0, 0);
         }
       }
+    const bool full = k0 + 64 <= kfull;
+    const uint32_t tkc = (uint32_t)(k0 >> 1) * FS2_ATTN_KC;
     bf16x8 sf[QG][2];
 #pragma unroll
     for (int qg = 0; qg < QG; ++qg) {
       float ds[4][4];
-      const uint64_t rowi = ((uint64_t)z * p.T + qi[qg]) * T2;
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt) {
-        const uint32_t kw = *(const uint32_t*)(kval + k0 + kt * 16 + 4 * g);   // keys 4g..4g+3
+        const uint32_t kw = full ? 0x01010101u : *(const uint32_t*)(kval + k0 + kt * 16 + 4 * g);
 #pragma unroll
-        for (int r = 0; r < 4; r += 2) {
-          const int key = k0 + kt * 16 + 4 * g + r;
-          const uint32_t h = p.p_drop > 0.f ? fs2_hash_pair(dkey, (rowi + key) >> 1) : 0u;
+        for (int e2 = 0; e2 < 2; ++e2) {
+          const uint32_t hh = drop ? fs2_attn_mix(dc[qg][kt][e2] + tkc) : 0u;
 #pragma unroll
           for (int e = 0; e < 2; ++e) {
-            const bool ok = (kw >> (8 * (r + e))) & 1u;
-            const float pr = ok ? fexp2(sacc[kt][qg][r + e] * p.scale_log2 - lse[qg]) : 0.f;
-            float dp = pacc[kt][qg][r + e];
-            if (p.p_drop > 0.f)
-              dp = fs2_keep_pair_bit(h, rowi + key + e, p.thr16) ? dp * p.inv_keep : 0.f;
-            ds[kt][r + e] = pr * (dp - dsum[qg]);
+            const int r = 2 * e2 + e;
+            float pr = fexp2(fmaf(sacc[kt][qg][r], c, nlse[qg]));
+            if (!full) pr = (kw >> (8 * r)) & 1u ? pr : 0.f;
+            float dp = pacc[kt][qg][r];
+            if (drop) dp = ((hh >> (16 * e)) & 0xffffu) >= p.thr16 ? dp * p.inv_keep : 0.f;
+            ds[kt][r] = pr * (dp - dsum[qg]);
           }
         }
       }
@@ -494,32 +654,38 @@ __global__ void __launch_bounds__(W8 * 64 / QG, 1) attn_bwd_dq_kernel(AttnP p) {
 }
 
 // ------------------------------------------------------------------------------ backward dK dV
-// block: W8 waves x 16 keys; query tiles of 64 (Q, dO, lse, D staged in LDS).  Q / dO tiles are
-// double-buffered through LDS-DMA (tile t+1 streams in while tile t computes; the one-buffer
-// version exposed each tile's load); wave 0 streams tile t+1's lse / D rows the same way.
+// block: W8 waves x 16 keys; query tiles of 64 (Q, dO, lse, D and the dropout row hashes staged
+// in LDS).  Q / dO tiles are double-buffered through LDS-DMA (tile t+1 streams in while tile t
+// computes); wave 0 streams tile t+1's lse / D / row-hash rows the same way.  A masked key's
+// lane computes unmasked (finite) values and stores zeros; rows past T read zero Q / dO / lse /
+// D, so their P = 1 multiplies zero dO and their dS is 0 -- no per-element mask.
 template <int DH, int W8 = 8>
 __global__ void __launch_bounds__(W8 * 64, 1) attn_bwd_dkv_kernel(AttnP p) {
   constexpr int NS = DH / 32, ND = DH / 16;
   constexpr int TB = 64 * DH * 2;
   // one LDS array (a second __shared__ object can make hipcc drain the DMA ring early):
-  // [Q 0 | dO 0 | Q 1 | dO 1 | (lse, D) 0 | (lse, D) 1 | kval | kend]
-  __shared__ __attribute__((aligned(16))) char smem[4 * TB + 1024 + TMAX + 16];
+  // [Q 0 | dO 0 | Q 1 | dO 1 | (lse, D, rowhash) 0 | (lse, D, rowhash) 1 | kval | kend, kfull]
+  __shared__ __attribute__((aligned(16))) char smem[4 * TB + 1536 + TMAX + 16];
   float* lsd = (float*)(smem + 4 * TB);
-  uint8_t* kval = (uint8_t*)(smem + 4 * TB + 1024);
-  int& kend_s = *(int*)(smem + 4 * TB + 1024 + TMAX);
+  uint8_t* kval = (uint8_t*)(smem + 4 * TB + 1536);
+  int* kbuf = (int*)(smem + 4 * TB + 1536 + TMAX);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
-  const int z = blockIdx.y, b = z / p.H, h = z - b * p.H;
-  const uint32_t dkey = fs2_drop_key(p.seed, p.salt);
-  const uint64_t T2 = (uint64_t)((p.T + 1) & ~1);   // dropout rows padded to even length
-  build_kvalid(kval, &kend_s, p, b, h);
+  int blk, z;
+  attn_block_coords(blk, z);
+  const int b = z / p.H, h = z - b * p.H;
+  const bool drop = p.p_drop > 0.f;
+  int kfull;
+  build_kvalid(kval, kbuf, p, b, h, &kfull);
   const bf16* Qb = p.qkv + (long)b * p.T * p.ldq + h * DH;
   const bf16* Kb = Qb + p.D;
   const bf16* Vb = Qb + 2 * p.D;
   const bf16* dOb = p.dout + (long)b * p.T * p.lddo + h * DH;
+  const float c = p.scale_log2;
 
-  const int key = blockIdx.x * (16 * W8) + wave * 16 + (lane & 15);   // this lane's key (B col)
+  const int key = blk * (16 * W8) + wave * 16 + (lane & 15);   // this lane's key (B col)
   const bool kin = key < p.T;
   const bool kok = kin && kval[key];
+  const uint32_t kc = (uint32_t)(key >> 1) * FS2_ATTN_KC;
   bf16x8 kf[NS], vf[NS];
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
@@ -536,13 +702,16 @@ __global__ void __launch_bounds__(W8 * 64, 1) attn_bwd_dkv_kernel(AttnP p) {
   dma.init(wave, lane, 0);
   const i32x4 rsQ = make_rsrc(Qb), rsO = make_rsrc(dOb);
   const int ntile = anyk ? (p.T + 63) / 64 : 0;
-  // lse / D rows of a tile: wave 0 streams them in by 4-byte LDS-DMA (no registers held)
+  // lse / D / row-hash rows of a tile: wave 0 streams them in by 4-byte LDS-DMA
+  const long BHT = (long)p.B * p.H * p.T;
   const i32x4 rsL = make_rsrc(p.lse + (long)z * p.T), rsD = make_rsrc(p.dsum + (long)z * p.T);
+  const i32x4 rsH = make_rsrc(p.dsum + BHT + (long)z * p.T);
   auto issue_stats = [&](int q0, int buf) {
     if (wave == 0) {
       const int vo = q0 + lane < p.T ? lane * 4 : BUF_OOB;
-      blds4(rsL, vo, q0 * 4, (char*)(lsd + buf * 128));
-      blds4(rsD, vo, q0 * 4, (char*)(lsd + buf * 128 + 64));
+      blds4(rsL, vo, q0 * 4, (char*)(lsd + buf * 192));
+      blds4(rsD, vo, q0 * 4, (char*)(lsd + buf * 192 + 64));
+      blds4(rsH, vo, q0 * 4, (char*)(lsd + buf * 192 + 128));
     }
   };
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // K/V fragments resident before the ring
@@ -555,15 +724,16 @@ __global__ void __launch_bounds__(W8 * 64, 1) attn_bwd_dkv_kernel(AttnP p) {
     const int q0 = t * 64;
     const char* Qs = smem + (t & 1) * 2 * TB;
     const char* Os = Qs + TB;
-    const float* ls_s = lsd + (t & 1) * 128;
+    const float* ls_s = lsd + (t & 1) * 192;
     const float* ds_s = ls_s + 64;
+    const uint32_t* rh_s = (const uint32_t*)(ls_s + 128);
     if (t + 1 < ntile) {
       issue_stats(q0 + 64, (t + 1) & 1);
       char* nx = smem + ((t + 1) & 1) * 2 * TB;
       dma.issue(nx, rsQ, p.ldq, q0 + 64, p.T, wave);
       dma.issue(nx + TB, rsO, p.lddo, q0 + 64, p.T, wave);
-      // tile t's pieces landed (wave 0 also has its two lse / D loads behind them)
-      if (wave == 0) wait_vmcnt<2 * TileDma<DH, W8>::PER + 2>();
+      // tile t's pieces landed (wave 0 also has its three stat-row loads behind them)
+      if (wave == 0) wait_vmcnt<2 * TileDma<DH, W8>::PER + 3>();
       else wait_vmcnt<2 * TileDma<DH, W8>::PER>();
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -588,17 +758,15 @@ __global__ void __launch_bounds__(W8 * 64, 1) attn_bwd_dkv_kernel(AttnP p) {
     for (int qt = 0; qt < 4; ++qt) {
       const f32x4 l4 = *(const f32x4*)(ls_s + qt * 16 + 4 * g);   // rows 4g..4g+3 of this qt
       const f32x4 d4 = *(const f32x4*)(ds_s + qt * 16 + 4 * g);
-      // dropout: keys 2m and 2m+1 (lanes 2m, 2m+1) share one pair hash per query row; the even
-      // lane hashes rows r = 0, 1 and the odd lane rows 2, 3, then they swap (DPP quad_perm)
+      // dropout: keys 2m and 2m+1 (lanes 2m, 2m+1) share one draw per query row; the even
+      // lane draws rows r = 0, 1 and the odd lane rows 2, 3, then they swap (DPP quad_perm)
       uint32_t hx[4];
-      if (p.p_drop > 0.f) {
+      if (drop) {
         const int odd = lane & 1;
+        const u32x2 rh2 = *(const u32x2*)(rh_s + qt * 16 + 4 * g + 2 * odd);
         uint32_t mine[2];
 #pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const int q = q0 + qt * 16 + 4 * g + 2 * odd + e;
-          mine[e] = fs2_hash_pair(dkey, (((uint64_t)z * p.T + q) * T2 + key) >> 1);
-        }
+        for (int e = 0; e < 2; ++e) mine[e] = fs2_attn_mix(rh2[e] + kc);
         uint32_t other[2];
 #pragma unroll
         for (int e = 0; e < 2; ++e)
@@ -610,14 +778,11 @@ __global__ void __launch_bounds__(W8 * 64, 1) attn_bwd_dkv_kernel(AttnP p) {
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int ql = qt * 16 + 4 * g + r, q = q0 + ql;
-        const bool ok = kok && q < p.T;
-        float pr = fexp2(sacc[qt][r] * p.scale_log2 - l4[r]);
-        pr = ok ? pr : 0.f;
+        const float pr = fexp2(fmaf(sacc[qt][r], c, -l4[r]));
         float dp = pacc[qt][r];
         float pd = pr;
-        if (p.p_drop > 0.f) {
-          const bool keep = fs2_keep_pair_bit(hx[r], (uint64_t)key, p.thr16);
+        if (drop) {
+          const bool keep = ((hx[r] >> ((key & 1) * 16)) & 0xffffu) >= p.thr16;
           dp = keep ? dp * p.inv_keep : 0.f;
           pd = keep ? pr : 0.f;       // 1 / (1 - p) applied to dV once, at the store
         }
@@ -640,17 +805,19 @@ __global__ void __launch_bounds__(W8 * 64, 1) attn_bwd_dkv_kernel(AttnP p) {
     }
     __builtin_amdgcn_s_barrier();   // every wave is done with buffer t & 1 before t+2 lands
   }
-  // C layout: col = feature (lane & 15), rows = keys 4g + r of this wave's 16
+  // C layout: col = feature (lane & 15), rows = keys 4g + r of this wave's 16; a masked key's
+  // gradients are zero (its lane computed with the key unmasked)
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const int kr = blockIdx.x * (16 * W8) + wave * 16 + 4 * g + r;
+    const int kr = blk * (16 * W8) + wave * 16 + 4 * g + r;
     if (kr >= p.T) continue;
+    const bool ok = kval[kr];
     bf16* krow = p.dqkv + ((long)b * p.T + kr) * p.lddq + p.D + h * DH;
     bf16* vrow = krow + p.D;
 #pragma unroll
     for (int d = 0; d < ND; ++d) {
-      krow[16 * d + (lane & 15)] = (bf16)(dk[d][r] * p.scale);
-      vrow[16 * d + (lane & 15)] = (bf16)(dv[d][r] * p.inv_keep);
+      krow[16 * d + (lane & 15)] = (bf16)(ok ? dk[d][r] * p.scale : 0.f);
+      vrow[16 * d + (lane & 15)] = (bf16)(ok ? dv[d][r] * p.inv_keep : 0.f);
     }
   }
 }
@@ -669,6 +836,14 @@ void launch_fwd(const AttnP& p, hipStream_t s) {
     dim3 grid((p.T + 63) / 64, p.B * p.H);
     if (attn_qg_fwd(DH) == 2) hipLaunchKernelGGL((attn_fwd_kernel<DH, 2, 4>), grid, dim3(128), 0, s, p);
     else hipLaunchKernelGGL((attn_fwd_kernel<DH, 1, 4>), grid, dim3(256), 0, s, p);
+    return;
+  }
+  // dh = 192 at decoder lengths: 8 waves x 32 queries (256-query blocks, one per CU at B = 32,
+  // T = 977): every K fragment and V^T fragment feeds two MFMAs, halving the LDS reads per
+  // MFMA that bound the 16-query form (tools/attn_bench.py: 86.2 -> 72.9 us; 4 waves x 32
+  // queries at one wave per SIMD: 111 us)
+  if (DH == 192 && !(p.xflags & 4)) {
+    hipLaunchKernelGGL((attn_fwd_kernel<DH, 2, 16>), dim3((p.T + 255) / 256, p.B * p.H), dim3(512), 0, s, p);
     return;
   }
   dim3 grid((p.T + 127) / 128, p.B * p.H);
@@ -723,6 +898,7 @@ extern "C" int fs2_attn_fwd(const void* qkv, int64_t ldq, const uint8_t* key_pad
   p.inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
   p.seed = seed; p.salt = salt;
   p.thr16 = (uint32_t)(p_drop * 65536.f + 0.5f);
+  p.xflags = fs2_exp_int("FS2_ATTN_FLAGS", 0);
   hipStream_t s = (hipStream_t)stream;
   switch (dh) {
     case 64: launch_fwd<64>(p, s); break;
@@ -765,7 +941,8 @@ extern "C" int fs2_attn_bwd(const void* qkv, int64_t ldq, const uint8_t* key_pad
   return 0;
 }
 
-extern "C" int64_t fs2_attn_workspace_floats(int B, int H, int T) { return (int64_t)B * H * T; }
+// D = rowsum(dO * O) and the dropout row hashes of every query row (dQ kernel -> dK/dV kernel)
+extern "C" int64_t fs2_attn_workspace_floats(int B, int H, int T) { return 2 * (int64_t)B * H * T; }
 
 // this translation unit's dropout seed base (fs2_common.h)
 FS2_SEED_SETTER(fs2_seed_base_flash)

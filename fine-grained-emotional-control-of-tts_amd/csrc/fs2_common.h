@@ -161,6 +161,32 @@ __device__ __forceinline__ void fs2_keep_run(uint32_t seed, uint32_t salt, uint6
   }
 }
 
+// Attention-probability dropout (flash.hip's fused kernels, attention.hip's materialised path):
+// element (row, key) of the (seed, salt) draw, row = (b*H + h)*T + query, is kept iff the 16-bit
+// half (key & 1) of fs2_attn_bits(fs2_attn_rowhash(dkey, row), key >> 1) >= thr16.  The per-row
+// part is a full lowbias32 round, computed once per query row; the per-element part is ONE add
+// of the key pair's multiple of FS2_ATTN_KC (a lane constant plus a per-tile scalar in the
+// kernels) and one xorshift-multiply-xorshift round on the full-rate 24-bit multiplier
+// (v_mul_lo_u32 issues at a quarter of the VALU rate; the murmur-style pair hash of the
+// LayerNorm masks costs four of them per pair).  Measured on 31 M draws: keep rate, 1024-bin
+// chi^2 and lag correlations over keys / rows at the level of an ideal generator (|c| < 0.003).
+constexpr uint32_t FS2_ATTN_KC = 0x27D4EB2Fu;
+__device__ __forceinline__ uint32_t fs2_attn_rowhash(uint32_t dkey, uint32_t row) {
+  uint32_t h = (row * 0x9E3779B1u) ^ dkey;
+  h ^= h >> 16; h *= 0x7FEB352Du; h ^= h >> 15; h *= 0x846CA68Bu; h ^= h >> 16;
+  return h;
+}
+__device__ __forceinline__ uint32_t fs2_attn_mix(uint32_t u) {   // u = rowhash + kpair * KC
+  u ^= u >> 15;
+  u = __umul24(u, 0x5BD1E9u);
+  return u ^ (u >> 13);
+}
+__device__ __forceinline__ bool fs2_attn_keep(uint32_t dkey, uint32_t row, uint32_t key,
+                                              uint32_t thr16) {
+  const uint32_t h = fs2_attn_mix(fs2_attn_rowhash(dkey, row) + (key >> 1) * FS2_ATTN_KC);
+  return ((h >> ((key & 1u) * 16)) & 0xffffu) >= thr16;
+}
+
 // reflect index into [0, T) (torch F.pad(mode="reflect") semantics, single bounce)
 __device__ __forceinline__ int reflect_idx(int i, int T) {
   if (i < 0) i = -i;

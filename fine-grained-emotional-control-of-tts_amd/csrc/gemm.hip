@@ -1456,15 +1456,25 @@ __device__ void llvm_raw_buffer_store_v4i32(i32x4 data, i32x4 rsrc, int voffset,
 __device__ i32x2 llvm_raw_buffer_load_v2i32(i32x4 rsrc, int voffset, int soffset,
                                             int aux) __asm("llvm.amdgcn.raw.buffer.load.v2i32");
 
-// epilogue store instructions per wave per tile: fp32 one 16-byte store per 16x16 block (16);
-// bf16 one 16-byte store per block PAIR (8: lanes l and l ^ 16 trade halves)
-constexpr int PK_STORES32 = 16, PK_STORES16 = 8;
+// epilogue store instructions per wave per tile (gemm_pk_kernel ST32 / ST16): fp32 one 16-byte
+// store per 16x16 block; bf16 one 16-byte store per block PAIR (lanes l and l ^ 16 trade halves)
 
 template <int N>
 __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 
+// MI x NJ: the 16 x 16 blocks of a wave's sub-tile (waves as 4 rows x 2 columns), so one tile is
+// (64 MI) x (32 NJ): 4 x 4 = 256 x 128 (the decoder's short-K shapes), 2 x 4 = 128 x 128 and
+// 2 x 2 = 128 x 64 for the encoder / predictor shapes (M = 6400), where 256-row tiles left most
+// CUs idle (75 tiles of 256 x 128 at N = 384); the 128 x 64 instance needs 72 KiB of LDS, so two
+// blocks share a CU.
+template <int MI, int NJ>
 __global__ void __launch_bounds__(BNT) gemm_pk_kernel(GemmP p) {
-  __shared__ __attribute__((aligned(16))) char smem[BIG_LDS];
+  constexpr int TM = 64 * MI, TN = 32 * NJ;
+  constexpr int SA = TM * 128, SSTAGE = (TM + TN) * 128;   // A bytes / stage bytes
+  constexpr int NPC = MI + NJ / 2;                           // DMA pieces per wave per K-tile
+  constexpr int ST32 = MI * NJ, ST16 = MI * NJ / 2;          // epilogue stores per wave
+  static_assert(NJ % 2 == 0 && MI >= 1 && 3 * SSTAGE <= BIG_LDS, "pk tile");
+  __shared__ __attribute__((aligned(16))) char smem[3 * SSTAGE];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
@@ -1484,49 +1494,51 @@ __global__ void __launch_bounds__(BNT) gemm_pk_kernel(GemmP p) {
   const bool has_e = p.gate || p.residual;
 
   // per-lane parts of the DMA addressing (as gemm_big_kernel, plain operands)
-  int ar[4], alc[4], br[2], blc[2];
+  int ar[MI], alc[MI], br[NJ / 2], blc[NJ / 2];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    ar[i] = (wave * 4 + i) * 8 + (lane >> 3);
+  for (int i = 0; i < MI; ++i) {
+    ar[i] = (wave * MI + i) * 8 + (lane >> 3);
     alc[i] = (lane & 7) ^ (ar[i] & 7);
   }
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    br[i] = (wave * 2 + i) * 8 + (lane >> 3);
+  for (int i = 0; i < NJ / 2; ++i) {
+    br[i] = (wave * (NJ / 2) + i) * 8 + (lane >> 3);
     blc[i] = (lane & 7) ^ (br[i] & 7);
   }
   auto issue = [&](int t, int kt, int stage) {
     const int tile = c0 + local + t * nbx;
     const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
     const int k0 = kt * 64;
-    char* la = smem + stage * BIG_STAGE;
-    char* lb = la + BIG_A;
+    char* la = smem + stage * SSTAGE;
+    char* lb = la + SA;
     const bool kin = k0 + 64 <= p.K;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = tm * BBM + ar[i];
+    for (int i = 0; i < MI; ++i) {
+      const int row = tm * TM + ar[i];
       const bool ok = row < p.M && (kin || k0 + alc[i] * 8 < p.K);
       blds16(rsA, ok ? (int)(((long)row * p.lda + alc[i] * 8) * 2) : BUF_OOB, k0 * 2,
-             la + (wave * 4 + i) * 1024);
+             la + (wave * MI + i) * 1024);
     }
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int row = tn * 128 + br[i];
+    for (int i = 0; i < NJ / 2; ++i) {
+      const int row = tn * TN + br[i];
       const bool ok = row < p.N && (kin || k0 + blc[i] * 8 < p.K);
       blds16(rsB, ok ? (int)(((long)row * p.ldb + blc[i] * 8) * 2) : BUF_OOB, k0 * 2,
-             lb + (wave * 2 + i) * 1024);
+             lb + (wave * (NJ / 2) + i) * 1024);
     }
   };
 
-  f32x4 acc[4][4];
+  f32x4 acc[MI][NJ];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   // epilogue operands of the current tile
-  f32x4 bv[4] = {};
-  float rs[4] = {1.f, 1.f, 1.f, 1.f}, rs2[4] = {1.f, 1.f, 1.f, 1.f};
-  i32x2 ev[4][4] = {};
+  f32x4 bv[NJ] = {};
+  float rs[MI], rs2[MI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i) { rs[i] = 1.f; rs2[i] = 1.f; }
+  i32x2 ev[MI][NJ] = {};
 
   // (t, kt) of iterations it (current), it + 2 (prefetch)
   int t = 0, kt = 0, t2 = 0, kt2 = 0;
@@ -1543,41 +1555,41 @@ __global__ void __launch_bounds__(BNT) gemm_pk_kernel(GemmP p) {
   auto step = [&](auto LD, auto EP) __attribute__((always_inline)) {
     constexpr bool LOADS = decltype(LD)::value, EPI = decltype(EP)::value;
     const bool more = it + 1 < total;
-    // stage it landed: younger than its 6 pieces are those of it + 1 and, after a tile's
-    // epilogue, that epilogue's 16 stores
+    // stage it landed: younger than its NPC pieces are those of it + 1 and, after a tile's
+    // epilogue, that epilogue's stores
     if (more) {
-      if (!prev_last) vm_wait<6>();
-      else if (p.c_fp32) vm_wait<6 + PK_STORES32>();
-      else vm_wait<6 + PK_STORES16>();
+      if (!prev_last) vm_wait<NPC>();
+      else if (p.c_fp32) vm_wait<NPC + ST32>();
+      else vm_wait<NPC + ST16>();
     } else {
       if (!prev_last) vm_wait<0>();
-      else if (p.c_fp32) vm_wait<PK_STORES32>();
-      else vm_wait<PK_STORES16>();
+      else if (p.c_fp32) vm_wait<ST32>();
+      else vm_wait<ST16>();
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     const int tile = c0 + local + t * nbx;
     const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
-    const int mb = tm * BBM + wm * 64, nb = tn * 128 + wn * 64;
+    const int mb = tm * TM + wm * 16 * MI, nb = tn * TN + wn * 16 * NJ;
     // epilogue operands one iteration ahead of the epilogue (nk >= 2): issued before this
     // iteration's prefetch, they are retired by the NEXT iteration's stage wait, so the
     // epilogue itself never waits on a load (with nk == 1 they are issued in the same one)
     if constexpr (LOADS) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < NJ; ++j) {
         const int n = nb + 16 * j + 4 * lg;
         bv[j] = (p.bias && n < p.nvalid) ? *(const f32x4*)(p.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
       }
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < MI; ++i) {
         const int m = mb + 16 * i + li;
         const bool in = m < p.mvalid;
         rs[i] = (p.row_scale && in) ? p.row_scale[m] : 1.f;
         rs2[i] = (p.row_scale_post && in) ? p.row_scale_post[m] : 1.f;
         if (has_e) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
+          for (int j = 0; j < NJ; ++j) {
             const int n = nb + 16 * j + 4 * lg;
             const bool ok = in && n < p.nvalid;
             ev[i][j] = llvm_raw_buffer_load_v2i32(rsE, ok ? (int)(((long)m * lde + n) * 2) : BUF_OOB, 0, 0);
@@ -1590,28 +1602,28 @@ __global__ void __launch_bounds__(BNT) gemm_pk_kernel(GemmP p) {
       issue(t2, kt2, (it + 2) % 3);
       if (++kt2 == nk) { kt2 = 0; ++t2; }
     }
-    const char* la = smem + (it % 3) * BIG_STAGE;
-    const char* lb = la + BIG_A;
-    bf16x8 af[2][4], bfr[2][4];
+    const char* la = smem + (it % 3) * SSTAGE;
+    const char* lb = la + SA;
+    bf16x8 af[2][MI], bfr[2][NJ];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i) af[s][i] = frag_bf16_kmajor(la, wm * 16 * MI + i * 16, s, lane);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) bfr[s][j] = frag_bf16_kmajor(lb, wn * 16 * NJ + j * 16, s, lane);
+    }
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        af[s][i] = frag_bf16_kmajor(la, wm * 64 + i * 16, s, lane);
-        bfr[s][i] = frag_bf16_kmajor(lb, wn * 64 + i * 16, s, lane);
-      }
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < NJ; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[s][j], af[s][i], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);
-    __builtin_amdgcn_sched_group_barrier(0x008, 32, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, 2 * (MI + NJ), 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 2 * MI * NJ, 0);
     if constexpr (EPI) {
       if (nk == 1) {   // operands issued this iteration: retire them, keep the prefetch in flight
-        if (pre) vm_wait<6>(); else vm_wait<0>();
+        if (pre) vm_wait<NPC>(); else vm_wait<0>();
       }
       const bool nost = XFLAGS(p) & 16;   // timing experiments only: no stores (wrong results)
       const bool odd = lg & 1;
@@ -1637,12 +1649,12 @@ __global__ void __launch_bounds__(BNT) gemm_pk_kernel(GemmP p) {
                          ((unsigned)__builtin_bit_cast(unsigned short, (bf16)v[3]) << 16)};
       };
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < MI; ++i) {
         const int m = mb + 16 * i + li;
         const bool rowok = m < p.mvalid;
         if (p.c_fp32) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
+          for (int j = 0; j < NJ; ++j) {
             const int n = nb + 16 * j + 4 * lg;
             const f32x4 v = fin(i, j);
             if (nost) continue;
@@ -1654,7 +1666,7 @@ __global__ void __launch_bounds__(BNT) gemm_pk_kernel(GemmP p) {
         // bf16: lanes l and l ^ 16 trade halves of a block pair -> 8 consecutive columns each,
         // one 16-byte store (the CU's store path, not HBM, bounds the 8-byte form)
 #pragma unroll
-        for (int j = 0; j < 4; j += 2) {
+        for (int j = 0; j < NJ; j += 2) {
           const u32x2 a = pack(fin(i, j)), b = pack(fin(i, j + 1));
           const unsigned r0 = (unsigned)__shfl_xor((int)(odd ? a[0] : b[0]), 16, 64);
           const unsigned r1 = (unsigned)__shfl_xor((int)(odd ? a[1] : b[1]), 16, 64);
@@ -2273,15 +2285,43 @@ int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
     // FS2_PK_NARROW=1 keeps them on the persistent kernel
     static const bool pk_narrow = getenv_flag("FS2_PK_NARROW");
     const bool pk_shape = p.K <= 768 || p.N > 512 || pk_narrow;
-    if (!no_pk && ak && bk && p.conv_mode == 0 && batch == 1 && p.split_k <= 1 && p.vec_ok &&
-        !p.accumulate && !(p.gate && p.residual) && p.K > 64 && p.K <= 1536 && pk_shape && pk_fits) {
+    const bool pk_ok = !no_pk && ak && bk && p.conv_mode == 0 && batch == 1 && p.split_k <= 1 &&
+                       p.vec_ok && !p.accumulate && !(p.gate && p.residual) && p.K > 64 && pk_fits;
+    // tile of the persistent short-K kernel: 256 x 128 where those tiles fill most of a round
+    // (the decoder's shapes that gemm_ps_kernel does not take); below 160 such tiles (the
+    // encoder / predictor shapes, M = 6400) 128 x 128 or 128 x 64 tiles, whichever finishes in
+    // fewer per-CU tile-areas (two 128 x 64 blocks share a CU) -- K up to 4096 there, since the
+    // per-tile 256 x 128 kernel that takes the narrow long-K shapes fills 75 of the 256 CUs.
+    // FS2_PK_CFG = 44 / 24 / 22 forces one for A/B runs.
+    int pk_cfg = 0;
+    if (pk_ok) {
+      const long t44 = (long)((p.M + 255) / 256) * ((p.N + 127) / 128);
+      const long t24 = (long)((p.M + 127) / 128) * ((p.N + 127) / 128);
+      const long t22 = (long)((p.M + 127) / 128) * ((p.N + 63) / 64);
+      // per-CU work in 128 x 128 tile units over the rounds each needs (ties: larger tile)
+      const long c44 = (t44 + 255) / 256 * 2, c24 = (t24 + 255) / 256, c22 = (t22 + 511) / 512;
+      long best = 1L << 40;
+      if (p.K <= 1536 && pk_shape) { pk_cfg = 44; best = c44; }
+      if (t44 < 400 && p.K <= 4096) {
+        if (c24 < best) { pk_cfg = 24; best = c24; }
+        if (c22 < best) { pk_cfg = 22; best = c22; }
+      }
+      static const int force = getenv_int("FS2_PK_CFG", 0);
+      if (force == 44 || force == 24 || force == 22) pk_cfg = force;
+    }
+    if (pk_cfg) {
       GemmP q = p;
       q.g4_flags = getenv_int("FS2_PK_FLAGS", 0);
-      q.tiles_m = (p.M + BBM - 1) / BBM;
+      const int TM = pk_cfg == 44 ? 256 : 128, TN = pk_cfg == 22 ? 64 : 128;
+      q.tiles_m = (p.M + TM - 1) / TM;
+      q.tiles_n = (p.N + TN - 1) / TN;
       const int nt = q.tiles_m * q.tiles_n;
+      const int slots = pk_cfg == 22 ? 512 : 256;   // blocks resident at once (LDS)
       // >= 8 blocks: every XCD chunk needs a block (blocks with no tile exit at once)
-      const int g = nt < 256 ? (nt + 7) / 8 * 8 : 256;
-      hipLaunchKernelGGL(gemm_pk_kernel, dim3(g), dim3(BNT), 0, s, q);
+      const int g = nt < slots ? (nt + 7) / 8 * 8 : slots;
+      if (pk_cfg == 44) hipLaunchKernelGGL((gemm_pk_kernel<4, 4>), dim3(g), dim3(BNT), 0, s, q);
+      else if (pk_cfg == 24) hipLaunchKernelGGL((gemm_pk_kernel<2, 4>), dim3(g), dim3(BNT), 0, s, q);
+      else hipLaunchKernelGGL((gemm_pk_kernel<2, 2>), dim3(g), dim3(BNT), 0, s, q);
       FS2_CHECK_LAUNCH();
       return 0;
     }

@@ -553,6 +553,22 @@ class FS2Engine:
             return self._wgrad_km(dY, lddy, X, ldx, M, T, wname, gemm_tag, bias, dy_img)
         if dy_img is not None:
             raise RuntimeError(f"{wname}: a padded dY image needs the K-major weight gradient")
+        if n_cols is not None and n_cols != KW * C and KW == 1 and n_cols % 8 == 0 and self.dt == 1:
+            # padded X columns (concat_proj: 2D + 5 -> 776): split-K slices over the padded width,
+            # then the valid columns added into the gradient -- the unpadded GEMM's odd row
+            # pitch forced the scalar atomic epilogue (92 -> ~35 us, tools/wgrad1x1_bench.py)
+            K = round_up(M, self.epc)
+            ns = eff_split(K, wgrad_slices(O, n_cols, n_cols, K, self.dt), _BK[self.dt])
+            ns = max(ns, 2)
+            stride = O * n_cols
+            ws = self.ws((ns + 1) * stride)
+            ops.gemm(O, n_cols, K, dY, lddy, X, ldx, ws, n_cols, dt=self.dt, a_kmajor=0,
+                     b_kmajor=0, c_fp32=1, kvalid=M, nvalid=n_cols, split_k=ns,
+                     split_stride=stride)
+            tot = ws[ns * stride:(ns + 1) * stride]
+            ops.sum_slices(ws, ns, stride, stride, tot, accumulate=0)
+            self.grads[wname].view(O, C).add_(tot.view(O, n_cols)[:, :C])
+            return
         Ncols = n_cols or KW * C
         K = round_up(M, self.epc)
         tiles = -(-O // 128) * -(-Ncols // 128)

@@ -151,8 +151,8 @@ def test_layernorm_fwd_bwd(cuda, dt, code, tol, D):
 
 
 def _keep_ln_np(seed, salt, idx, p):
-    """The per-element LayerNorm dropout mask: fs2_keep (fs2_common.h) is the same pair hash as
-    the attention mask (restated by _keep_np below), evaluated per element."""
+    """The per-element LayerNorm dropout mask: fs2_keep (fs2_common.h), the pair hash restated by
+    _keep_np below, evaluated per element (the attention probabilities draw fs2_attn_keep)."""
     return _keep_np(seed, salt, idx, p)
 
 
@@ -718,7 +718,7 @@ def test_colsum_bias_gradient(cuda, dt, code, tol, M, N, ldx):
 
 
 def _keep_np(seed, salt, idx, p):
-    """numpy restatement of fs2_keep_fast (fs2_common.h): the attention-dropout mask."""
+    """numpy restatement of fs2_keep_fast (fs2_common.h): the LayerNorm dropout masks."""
     M32 = np.uint64(0xffffffff)
 
     def mix(h):
@@ -742,6 +742,38 @@ def _keep_np(seed, salt, idx, p):
     h = (h * np.uint64(0x297A2D39)) & M32
     h ^= h >> np.uint64(15)
     bits = (h >> ((idx & np.uint64(1)) * np.uint64(16))) & np.uint64(0xffff)
+    return bits >= np.uint64(int(p * 65536 + 0.5))
+
+
+def _attn_keep_np(seed, salt, rows, keys, p):
+    """numpy restatement of fs2_attn_keep (fs2_common.h), the attention-probability dropout:
+    a lowbias32 hash per query row (rows = (b*H + h)*T + q), one add of (key >> 1) * KC and one
+    xorshift / 24-bit multiply / xorshift round per key pair.  rows (R, 1), keys (1, K)."""
+    M32 = np.uint64(0xffffffff)
+
+    def mix(h):
+        h = h & M32
+        h ^= h >> np.uint64(16)
+        h = (h * np.uint64(0x85ebca6b)) & M32
+        h ^= h >> np.uint64(13)
+        h = (h * np.uint64(0xc2b2ae35)) & M32
+        h ^= h >> np.uint64(16)
+        return h
+
+    dkey = int(mix(np.uint64((seed ^ ((salt * 0x9E3779B9) & 0xffffffff)) & 0xffffffff))) | 1
+    r = rows.astype(np.uint64)
+    k = keys.astype(np.uint64)
+    h = ((r * np.uint64(0x9E3779B1)) & M32) ^ np.uint64(dkey)
+    h ^= h >> np.uint64(16)
+    h = (h * np.uint64(0x7FEB352D)) & M32
+    h ^= h >> np.uint64(15)
+    h = (h * np.uint64(0x846CA68B)) & M32
+    h ^= h >> np.uint64(16)
+    u = (h + (k >> np.uint64(1)) * np.uint64(0x27D4EB2F)) & M32
+    u ^= u >> np.uint64(15)
+    u = ((u & np.uint64(0xffffff)) * np.uint64(0x5BD1E9)) & M32
+    u ^= u >> np.uint64(13)
+    bits = (u >> ((k & np.uint64(1)) * np.uint64(16))) & np.uint64(0xffff)
     return bits >= np.uint64(int(p * 65536 + 0.5))
 
 
@@ -786,10 +818,8 @@ def test_fused_attention_vs_torch(cuda, dh, T, p_drop, B):
     s = (q @ k.transpose(-1, -2)) * scale
     P = torch.softmax(s.masked_fill(mask, float("-inf")), -1)
     if p_drop > 0:
-        T2 = (T + 1) & ~1                          # dropout rows padded to even length
-        idx = (np.arange(B * H * T, dtype=np.uint64)[:, None] * np.uint64(T2)
-               + np.arange(T, dtype=np.uint64)[None, :])
-        keep = torch.from_numpy(_keep_np(seed, salt, idx, p_drop).reshape(B, H, T, T)).to(cuda)
+        keep = _attn_keep_np(seed, salt, np.arange(B * H * T)[:, None], np.arange(T)[None, :], p_drop)
+        keep = torch.from_numpy(keep.reshape(B, H, T, T)).to(cuda)
         P = P * keep / (1 - p_drop)
     o = P @ v
     ref = o.permute(0, 2, 1, 3).reshape(B * T, D)
