@@ -625,15 +625,31 @@ __global__ void __launch_bounds__(W8 * 64 / QG, 1) attn_bwd_dq_kernel(AttnP p) {
       sf[qg][0] = pack8(ds[0], ds[1]);
       sf[qg][1] = pack8(ds[2], ds[3]);
     }
+    // dQ^T += K^T dS^T: K^T fragments by asm transposed reads (no compiler DMA drain), two
+    // output blocks ahead of their MFMAs
+    TrFrag kb2[3][2];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-    for (int d = 0; d < ND; ++d)
+    for (int d = 0; d < 2; ++d)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const bf16x8 kf = lds_tr_frag(Ks, DH * 2, 32 * j, 16 * d, lane);
+      for (int j = 0; j < 2; ++j) lds_tr_frag_issue(kb2[d][j], Ks, DH * 2, 32 * j, 16 * d, lane);
+    static_for<0, ND>([&](auto DI) {
+      constexpr int d = decltype(DI)::value;
+      if constexpr (d + 2 < ND) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) lds_tr_frag_issue(kb2[(d + 2) % 3][j], Ks, DH * 2, 32 * j, 16 * (d + 2), lane);
+        lds_wait<8>(kb2[d % 3][0], kb2[d % 3][1]);
+      } else if constexpr (d + 1 < ND) {
+        lds_wait<4>(kb2[d % 3][0], kb2[d % 3][1]);
+      } else {
+        lds_wait<0>(kb2[d % 3][0], kb2[d % 3][1]);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int qg = 0; qg < QG; ++qg)
-          qacc[d][qg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, sf[qg][j], qacc[d][qg], 0, 0, 0);
-      }
+          qacc[d][qg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_val(kb2[d % 3][j]), sf[qg][j], qacc[d][qg], 0, 0, 0);
+    });
     __builtin_amdgcn_s_barrier();   // every wave is done with buffer t & 1 before t+2 lands
   }
 #pragma unroll
@@ -791,18 +807,30 @@ __global__ void __launch_bounds__(W8 * 64, 1) attn_bwd_dkv_kernel(AttnP p) {
       }
     }
     // dV += Pd^T dO, dK += dS^T Q : A = (key x query) from registers, B = tile^T via tr reads
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const bf16x8 pa = pack8(pdv[2 * j], pdv[2 * j + 1]);
-      const bf16x8 sa = pack8(dsv[2 * j], dsv[2 * j + 1]);
-#pragma unroll
-      for (int d = 0; d < ND; ++d) {
-        const bf16x8 ob = lds_tr_frag(Os, DH * 2, 32 * j, 16 * d, lane);
-        const bf16x8 qb = lds_tr_frag(Qs, DH * 2, 32 * j, 16 * d, lane);
-        dv[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, ob, dv[d], 0, 0, 0);
-        dk[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sa, qb, dk[d], 0, 0, 0);
+    // (asm transposed reads of dO^T / Q^T one (j, d) step ahead of their MFMAs: the kernel sits
+    // at the 256-register budget, a deeper ring spills)
+    bf16x8 pa, sa;
+    TrFrag ob[2], qb[2];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    lds_tr_frag_issue(ob[0], Os, DH * 2, 0, 0, lane);
+    lds_tr_frag_issue(qb[0], Qs, DH * 2, 0, 0, lane);
+    static_for<0, 2 * ND>([&](auto NI) {
+      constexpr int n = decltype(NI)::value, j = n / ND, d = n % ND;
+      if constexpr (n + 1 < 2 * ND) {
+        constexpr int n1 = n + 1;
+        lds_tr_frag_issue(ob[n1 & 1], Os, DH * 2, 32 * (n1 / ND), 16 * (n1 % ND), lane);
+        lds_tr_frag_issue(qb[n1 & 1], Qs, DH * 2, 32 * (n1 / ND), 16 * (n1 % ND), lane);
+        lds_wait<4>(ob[n & 1], qb[n & 1]);
+      } else {
+        lds_wait<0>(ob[n & 1], qb[n & 1]);
       }
-    }
+      if constexpr (d == 0) {
+        pa = pack8(pdv[2 * j], pdv[2 * j + 1]);
+        sa = pack8(dsv[2 * j], dsv[2 * j + 1]);
+      }
+      dv[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, tr_val(ob[n & 1]), dv[d], 0, 0, 0);
+      dk[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sa, tr_val(qb[n & 1]), dk[d], 0, 0, 0);
+    });
     __builtin_amdgcn_s_barrier();   // every wave is done with buffer t & 1 before t+2 lands
   }
   // C layout: col = feature (lane & 15), rows = keys 4g + r of this wave's 16; a masked key's

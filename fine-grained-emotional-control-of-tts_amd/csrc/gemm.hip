@@ -358,6 +358,34 @@ __device__ __forceinline__ bf16x8 frag_bf16_mnmajor(const char* lds, int r0, int
   const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   return __builtin_bit_cast(bf16x8, v);
 }
+// The same MN-major fragment through inline-asm transposed reads, for the LDS-DMA ring kernels
+// (gemm_big_kernel, gemm256_kernel).  hipcc's waitcnt pass treats the ds_read_tr16_b64 builtin
+// as a read that may alias any in-flight LDS-DMA and puts an s_waitcnt vmcnt(0) in front of it:
+// in the MN-major instances (the weight gradients) that drained the whole prefetch ring at
+// every K-tile.  The asm reads are invisible to that pass; mn_ready() after an explicit
+// lgkmcnt wait hands the registers back to the compiler.
+__device__ __forceinline__ uint32_t lds_off(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+template <int ROWB>   // bytes per k-row of the image: 256 (128 mn) or 512 (256 mn)
+__device__ __forceinline__ bf16x8 frag_bf16_mnmajor_asm(const char* lds, int r0, int s, int lane) {
+  const int li = lane & 15, g = lane >> 4, q = li >> 2, p = li & 3;
+  const int m = r0 + 4 * p;
+  const int c = m >> 3, boff = (m & 7) * 2;
+  const int k1 = s * 32 + 8 * g + q, k2 = k1 + 4;
+  const char* a1 = lds + k1 * ROWB + ((c ^ mn_swz<bf16>(k1)) << 4) + boff;
+  const char* a2 = lds + k2 * ROWB + ((c ^ mn_swz<bf16>(k2)) << 4) + boff;
+  s16x4 lo, hi;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(lds_off(a1)));
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(hi) : "v"(lds_off(a2)));
+  typedef __attribute__((ext_vector_type(8))) short s16x8;
+  const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+// after an asm "s_waitcnt lgkmcnt(..)" that retired the reads of f: order every consumer of f
+// after that wait (an empty asm that "rewrites" the registers; volatile asm keeps its order)
+__device__ __forceinline__ void mn_ready(bf16x8& f) { asm volatile("" : "+v"(f)); }
+
 // fp32 16x16x4 operand, lane l: row (mn) r0 + (l&15), k = s*4 + (l>>4)
 __device__ __forceinline__ float frag_f32_kmajor(const char* lds, int r0, int s, int lane) {
   const int r = r0 + (lane & 15);
@@ -660,20 +688,6 @@ constexpr int BIG_B = 128 * 128;          // B stage bytes (16 KiB)
 constexpr int BIG_STAGE = BIG_A + BIG_B;  // 48 KiB
 constexpr int BIG_LDS = 3 * BIG_STAGE;    // 144 KiB (the 256x128 fp32 epilogue tile fits)
 
-// MN-major rows of 256 mn (512 B): same chunk swizzle on the low 4 chunk bits
-__device__ __forceinline__ bf16x8 frag_bf16_mnmajor512(const char* lds, int r0, int s, int lane) {
-  const int li = lane & 15, g = lane >> 4, q = li >> 2, p = li & 3;
-  const int m = r0 + 4 * p;
-  const int c = m >> 3, boff = (m & 7) * 2;
-  const int k1 = s * 32 + 8 * g + q, k2 = k1 + 4;
-  const char* a1 = lds + k1 * 512 + ((c ^ mn_swz<bf16>(k1)) << 4) + boff;
-  const char* a2 = lds + k2 * 512 + ((c ^ mn_swz<bf16>(k2)) << 4) + boff;
-  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a1);
-  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a2);
-  typedef __attribute__((ext_vector_type(8))) short s16x8;
-  const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(bf16x8, v);
-}
 
 // Direct epilogue of one wave's 4 x 4 grid of 16x16 result blocks.  The large-tile kernels
 // compute every block TRANSPOSED (MFMA A operand = the B tile's fragment), so a lane holds
@@ -1038,10 +1052,20 @@ __global__ void __launch_bounds__(BNT) gemm_big_kernel(GemmP p) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         af[s][i] = AK ? frag_bf16_kmajor(la, wm * 64 + i * 16, s, lane)
-                      : frag_bf16_mnmajor512(la, wm * 64 + i * 16, s, lane);
+                      : frag_bf16_mnmajor_asm<512>(la, wm * 64 + i * 16, s, lane);
         bfr[s][i] = BKM ? frag_bf16_kmajor(lb, wn * 64 + i * 16, s, lane)
-                        : frag_bf16_mnmajor(lb, wn * 64 + i * 16, s, lane);
+                        : frag_bf16_mnmajor_asm<256>(lb, wn * 64 + i * 16, s, lane);
       }
+    if constexpr (!AK || !BKM) {   // asm reads: retire them before the MFMAs
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          if constexpr (!AK) mn_ready(af[s][i]);
+          if constexpr (!BKM) mn_ready(bfr[s][i]);
+        }
+    }
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
@@ -1052,8 +1076,10 @@ __global__ void __launch_bounds__(BNT) gemm_big_kernel(GemmP p) {
     // pin the order: every fragment read of the tile is issued before the first MFMA, so the
     // step-1 reads land while step-0 MFMAs run (hipcc otherwise recycles 2 registers and
     // waits lgkmcnt(0) in front of every MFMA group)
-    __builtin_amdgcn_sched_group_barrier(0x100, AK && BKM ? 16 : (AK || BKM ? 24 : 32), 0);
-    __builtin_amdgcn_sched_group_barrier(0x008, 32, 0);
+    if constexpr (AK && BKM) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 32, 0);
+    }
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 
@@ -1353,12 +1379,12 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256_kernel(GemmP p) {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           bfr[j] = BKM ? g4_frag_k(rB, wc * 64 + j * 16 + (lane & 15), lane >> 4)
-                       : frag_bf16_mnmajor512(rB, wc * 64 + j * 16, 0, lane);
+                       : frag_bf16_mnmajor_asm<512>(rB, wc * 64 + j * 16, 0, lane);
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
         af[i] = AK ? g4_frag_k(rA, wr * 128 + mq * 64 + i * 16 + (lane & 15), lane >> 4)
-                   : frag_bf16_mnmajor512(rA, wr * 128 + mq * 64 + i * 16, 0, lane);
+                   : frag_bf16_mnmajor_asm<512>(rA, wr * 128 + mq * 64 + i * 16, 0, lane);
       const bool iss = !noissue && (ph < 2 ? more : it + 2 < nk);
       if (iss && !dma_mm) issue(ph < 2 ? it + 1 : it + 2, 3 - ph);
       // phase 1 retires this tile's k1 regions, phase 3 the next tile's k0 regions (with the
@@ -1373,6 +1399,14 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256_kernel(GemmP p) {
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if constexpr (!AK) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) mn_ready(af[i]);
+      }
+      if constexpr (!BKM) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) mn_ready(bfr[j]);
+      }
       // ---- matrix section: one 64x64 quadrant x K=32 ----
       if (prio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
