@@ -2202,6 +2202,18 @@ void launch4(const GemmP& p, dim3 grid, hipStream_t s, int ak, int bk) {
   else hipLaunchKernelGGL((gemm_kernel<T, false, false, GA, GB>), grid, dim3(NT), 0, s, p);
 }
 
+// Persistent-kernel grid budget per stream (fs2_set_stream_ctas): a stream that shares the GPU
+// with a latency-critical one (the weight-gradient side stream beside the data-gradient chain)
+// can leave CUs free by sizing its persistent grids below the CU count.  Default 256.
+struct StreamCtas { hipStream_t s; int ctas; };
+StreamCtas g_stream_ctas[8];
+int g_nstream_ctas = 0;
+int stream_ctas(hipStream_t s) {
+  for (int i = 0; i < g_nstream_ctas; ++i)
+    if (g_stream_ctas[i].s == s) return g_stream_ctas[i].ctas;
+  return 256;
+}
+
 template <typename T>
 int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
   dim3 grid(p.tiles_m * p.tiles_n, 1, gz);
@@ -2299,7 +2311,8 @@ int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
       const bool w192 = ps_w192;
       q.tiles_n = w192 ? (p.N + 191) / 192 : (p.N + 255) / 256;
       const int nt = q.tiles_m * q.tiles_n;
-      const int g = nt < 256 ? (nt + 7) / 8 * 8 : 256;
+      const int cus = stream_ctas(s);
+      const int g = nt < cus ? (nt + 7) / 8 * 8 : cus;
       if (w192) {
         if (ps_op) hipLaunchKernelGGL((gemm_ps_kernel<0, 48, 1>), dim3(g), dim3(BNT), 0, s, q);
         else if (cm_ps == 0) hipLaunchKernelGGL((gemm_ps_kernel<0, 48>), dim3(g), dim3(BNT), 0, s, q);
@@ -2350,7 +2363,7 @@ int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
       q.tiles_m = (p.M + TM - 1) / TM;
       q.tiles_n = (p.N + TN - 1) / TN;
       const int nt = q.tiles_m * q.tiles_n;
-      const int slots = pk_cfg == 22 ? 512 : 256;   // blocks resident at once (LDS)
+      const int slots = (pk_cfg == 22 ? 2 : 1) * stream_ctas(s);   // blocks resident at once (LDS)
       // >= 8 blocks: every XCD chunk needs a block (blocks with no tile exit at once)
       const int g = nt < slots ? (nt + 7) / 8 * 8 : slots;
       if (pk_cfg == 44) hipLaunchKernelGGL((gemm_pk_kernel<4, 4>), dim3(g), dim3(BNT), 0, s, q);
@@ -2460,6 +2473,16 @@ int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
 bool aligned16(const void* ptr) { return ((uintptr_t)ptr & 15) == 0; }
 
 }  // namespace
+
+extern "C" int fs2_set_stream_ctas(void* stream, int ctas) {
+  if (ctas < 8 || ctas > 256) return FS2_EINVAL;
+  const hipStream_t s = (hipStream_t)stream;
+  for (int i = 0; i < g_nstream_ctas; ++i)
+    if (g_stream_ctas[i].s == s) { g_stream_ctas[i].ctas = ctas / 8 * 8; return 0; }
+  if (g_nstream_ctas == 8) return FS2_EINVAL;
+  g_stream_ctas[g_nstream_ctas++] = {s, ctas / 8 * 8};
+  return 0;
+}
 
 extern "C" int fs2_gemm(const fs2_gemm_desc* d, void* stream) {
   if (!d || d->M < 0 || d->N < 0 || d->K < 0) return FS2_EINVAL;

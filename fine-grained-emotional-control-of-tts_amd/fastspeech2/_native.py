@@ -104,6 +104,7 @@ Fl = ctypes.c_float
 # name -> (restype, argtypes); must match include/fs2_hip.h exactly
 SIGNATURES = {
     "fs2_gemm": (I, [ctypes.POINTER(GemmDesc), P]),
+    "fs2_set_stream_ctas": (I, [P, I]),
     "fs2_colsum": (I, [P, I64, I, I, I, P, I, P, P]),
     "fs2_conv_fold": (I, [P, I, I64, I, I, I, I, P, I64, P, I64, P, P, I, P]),
     "fs2_colsum_workspace_floats": (I64, [I, I]),

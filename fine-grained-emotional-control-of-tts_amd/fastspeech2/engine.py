@@ -81,6 +81,12 @@ _PAD_FWD = N.exp_int("FS2_PAD_FWD", 1)
 # serial mode for per-call-site timing (bench.py --detail runs with the experiments library)
 _NO_SIDE = N.exp_flag("FS2_NO_SIDE_STREAM")
 _NO_AUX = N.exp_flag("FS2_NO_AUX_STREAM")
+# persistent-GEMM grid budget of the weight-gradient side stream (fs2_set_stream_ctas): the
+# CUs it leaves free take the main stream's LayerNorm / reduction / short GEMM launches, which
+# otherwise queue behind side-stream blocks that hold a whole CU's registers.  Same-box sweep
+# (tools/r04_side.sh, 2 x 7 interleaved bench runs): 256 -> 18.23-18.29 ms, 176-240 ->
+# 18.01-18.13, 160 -> 18.87; 208 kept.  FS2_SIDE_CTAS overrides in the experiments build.
+_SIDE_CTAS = N.exp_int("FS2_SIDE_CTAS", 208)
 
 
 def ps_plain_ok(M, lda, N, ldb, out_rows, ldc, out_bytes):
@@ -140,6 +146,11 @@ class FS2Engine:
         self._ws_key = torch.cuda.current_stream(self.dev).cuda_stream
         self._ws_other = {}
         self._side = torch.cuda.Stream(self.dev) if (self.dt == N.BF16 and not _NO_SIDE) else None
+        self._side_ctas = 256
+        if self._side is not None and _SIDE_CTAS < 256:
+            N.check(N.lib().fs2_set_stream_ctas(self._side.cuda_stream, _SIDE_CTAS),
+                    "fs2_set_stream_ctas")
+            self._side_ctas = _SIDE_CTAS // 8 * 8
         # duration / pitch predictor chains (independent of the rest of the step when the
         # pitch target is given) run on a third stream; their weight gradients stay on it
         self._aux = torch.cuda.Stream(self.dev) if (self._side is not None and not _NO_AUX) else None
@@ -517,7 +528,8 @@ class FS2Engine:
         ncol = KW * C
         tiles = -(-O // 256) * -(-ncol // 256)
         # one (split, tile) unit per CU; >= 16 K-tiles per unit, <= 25 fp32 slices to sum
-        S = max(1, min(256 // tiles, -(-Bt // 64) // 16, 25))
+        cus = self._side_ctas if self._side is not None else 256
+        S = max(1, min(cus // tiles, -(-Bt // 64) // 16, 25))
         Kp = round_up(Bt, 64 * S)
         dYT = self._km_image("dy", O, Kp)
         XT = self._km_image("x", C, Kp)

@@ -92,6 +92,12 @@ typedef struct fs2_gemm_desc {
 
 int fs2_gemm(const fs2_gemm_desc* d, void* stream);
 
+/* grid budget of the persistent GEMM kernels launched on `stream` (default 256 = one block per
+ * CU): a stream that runs beside a latency-critical one -- the weight-gradient side stream
+ * beside the data-gradient chain of the train step (model.py:279-441 backward) -- leaves
+ * 256 - ctas CUs to the other stream's kernels.  8 <= ctas <= 256 (rounded down to 8). */
+int fs2_set_stream_ctas(void* stream, int ctas);
+
 /* reflect-padding adjoint + dgrad epilogue (K16): Xpad fp32 [B][T+2P][C] from conv_mode 4
  * (nsplit split-K slices split_stride floats apart, summed here; nsplit <= 1: one slice),
  *   out[b,s] = ((Xpad[s+P] + Xpad[P-s]{1<=s<=P} + Xpad[2(T-1)-s+P]{T-1-P<=s<=T-2}) * rs
