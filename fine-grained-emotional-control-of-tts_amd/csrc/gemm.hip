@@ -1550,14 +1550,14 @@ __global__ void __launch_bounds__(BNT) gemm_pk_kernel(GemmP p) {
     for (int i = 0; i < MI; ++i) {
       const int row = tm * TM + ar[i];
       const bool ok = row < p.M && (kin || k0 + alc[i] * 8 < p.K);
-      blds16(rsA, ok ? (int)(((long)row * p.lda + alc[i] * 8) * 2) : BUF_OOB, k0 * 2,
+      blds16(rsA, ok ? ((row * (int)p.lda + alc[i] * 8) * 2) : BUF_OOB, k0 * 2,
              la + (wave * MI + i) * 1024);
     }
 #pragma unroll
     for (int i = 0; i < NJ / 2; ++i) {
       const int row = tn * TN + br[i];
       const bool ok = row < p.N && (kin || k0 + blc[i] * 8 < p.K);
-      blds16(rsB, ok ? (int)(((long)row * p.ldb + blc[i] * 8) * 2) : BUF_OOB, k0 * 2,
+      blds16(rsB, ok ? ((row * (int)p.ldb + blc[i] * 8) * 2) : BUF_OOB, k0 * 2,
              lb + (wave * (NJ / 2) + i) * 1024);
     }
   };
@@ -1626,7 +1626,7 @@ __global__ void __launch_bounds__(BNT) gemm_pk_kernel(GemmP p) {
           for (int j = 0; j < NJ; ++j) {
             const int n = nb + 16 * j + 4 * lg;
             const bool ok = in && n < p.nvalid;
-            ev[i][j] = llvm_raw_buffer_load_v2i32(rsE, ok ? (int)(((long)m * lde + n) * 2) : BUF_OOB, 0, 0);
+            ev[i][j] = llvm_raw_buffer_load_v2i32(rsE, ok ? ((m * (int)lde + n) * 2) : BUF_OOB, 0, 0);
           }
         }
       }
@@ -1693,7 +1693,7 @@ __global__ void __launch_bounds__(BNT) gemm_pk_kernel(GemmP p) {
             const f32x4 v = fin(i, j);
             if (nost) continue;
             llvm_raw_buffer_store_v4i32(__builtin_bit_cast(i32x4, v), rsC,
-                                        rowok && n < p.nvalid ? (int)(((long)m * p.ldc + n) * 4) : BUF_OOB, 0, 0);
+                                        rowok && n < p.nvalid ? ((m * (int)p.ldc + n) * 4) : BUF_OOB, 0, 0);
           }
           continue;
         }
@@ -1709,10 +1709,10 @@ __global__ void __launch_bounds__(BNT) gemm_pk_kernel(GemmP p) {
           if (nost) continue;
           if (!rowok || n0 + 8 <= p.nvalid || n0 >= p.nvalid) {
             llvm_raw_buffer_store_v4i32(__builtin_bit_cast(i32x4, o), rsC,
-                                        rowok && n0 < p.nvalid ? (int)(((long)m * p.ldc + n0) * 2) : BUF_OOB, 0, 0);
+                                        rowok && n0 < p.nvalid ? ((m * (int)p.ldc + n0) * 2) : BUF_OOB, 0, 0);
           } else {   // 4 valid columns at the right edge: still ONE store (the count is exact)
             llvm_raw_buffer_store_v2i32(i32x2{(int)o[0], (int)o[1]}, rsC,
-                                        (int)(((long)m * p.ldc + n0) * 2), 0, 0);
+                                        ((m * (int)p.ldc + n0) * 2), 0, 0);
           }
         }
       }
@@ -1851,7 +1851,7 @@ __global__ void __launch_bounds__(BNT, 1) gemm_ps_kernel(GemmP p) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       if constexpr (CM == 0) {
-        aoff[q] = aval[q] ? (int)(((long)at_[q] * p.lda + alc[q] * 8) * 2) : BUF_OOB;
+        aoff[q] = aval[q] ? ((at_[q] * (int)p.lda + alc[q] * 8) * 2) : BUF_OOB;
       } else {
         int ts;
         bool ok = aval[q];
@@ -1861,7 +1861,7 @@ __global__ void __launch_bounds__(BNT, 1) gemm_ps_kernel(GemmP p) {
           ts = at_[q] - a_tap;
           ok = ok && ts >= 0 && ts < p.conv_t;
         }
-        aoff[q] = ok ? (int)(((long)(abt[q] + ts) * p.lda + alc[q] * 8) * 2) : BUF_OOB;
+        aoff[q] = ok ? (((abt[q] + ts) * (int)p.lda + alc[q] * 8) * 2) : BUF_OOB;
       }
     }
   };
@@ -1913,7 +1913,7 @@ __global__ void __launch_bounds__(BNT, 1) gemm_ps_kernel(GemmP p) {
 #pragma unroll
       for (int q = 0; q < 2 + NB1; ++q) {
         const int row = tn * BN + brow[q];
-        boff[q] = row < p.N ? (int)(((long)row * p.ldb + blc[q] * 8) * 2) : BUF_OOB;
+        boff[q] = row < p.N ? ((row * (int)p.ldb + blc[q] * 8) * 2) : BUF_OOB;
       }
     }
   };
@@ -1924,7 +1924,7 @@ __global__ void __launch_bounds__(BNT, 1) gemm_ps_kernel(GemmP p) {
     for (int q = 0; q < 2 + NB1; ++q) {
       const int row = tn * BN + brow[q];
       const int j = row / p.conv_c, c = row - j * p.conv_c;
-      boff[q] = row < p.N ? (int)(((long)c * p.ldb + blc[q] * 8 + j - p.conv_p + BT_GUARD) * 2)
+      boff[q] = row < p.N ? ((c * (int)p.ldb + blc[q] * 8 + j - p.conv_p + BT_GUARD) * 2)
                           : BUF_OOB;
     }
   }
@@ -2022,8 +2022,12 @@ __global__ void __launch_bounds__(BNT, 1) gemm_ps_kernel(GemmP p) {
 #pragma unroll
             for (int j = 0; j < NJ; ++j) {
               const int m = mb + 16 * i + li, n = nb + 16 * j + 4 * lg;
-              ev[i][j] = llvm_raw_buffer_load_v2i32(
-                  rsE, (m < p.mvalid && n < p.nvalid) ? (int)(((long)m * lde + n) * 2) : BUF_OOB, 0, 0);
+              // inline asm: hipcc's own wait for a builtin load's registers descended to
+              // vmcnt(0) -- a drain of the whole DMA ring per tile; the asm
+              // loads are retired by the ring's counted waits (phase 3 of this iteration
+              // retires everything older than its A0 pieces) and handed back below
+              const int vo = (m < p.mvalid && n < p.nvalid) ? ((m * (int)lde + n) * 2) : BUF_OOB;
+              asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen" : "=v"(ev[i][j]) : "v"(vo), "s"(rsE));
             }
         }
       }
@@ -2074,6 +2078,12 @@ __global__ void __launch_bounds__(BNT, 1) gemm_ps_kernel(GemmP p) {
         const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
         const int mb = tm * 256 + wr * 128, nb = tn * BN + wc * WN;
         const int soc = BT ? (int)(bt_sp * p.split_stride * 4) : 0;
+        if constexpr (EO) {   // the operand loads were retired by this phase's counted wait
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) asm volatile("" : "+v"(ev[i][j]));
+        }
         f32x4 bv[NJ];
 #pragma unroll
         for (int j = 0; j < NJ; ++j) bv[j] = *(const f32x4*)(epl + (16 * j + 4 * lg) * 4);
@@ -2140,7 +2150,7 @@ __global__ void __launch_bounds__(BNT, 1) gemm_ps_kernel(GemmP p) {
               // write of the store's data VGPRs -- on gfx950 the store then read the NEXT
               // fragment's values in lanes 12-15 of each row group (tools/km_debug.py)
               llvm_raw_buffer_store_v4i32(__builtin_bit_cast(i32x4, v), rsC,
-                                          ok ? (int)(((long)m * p.ldc + n) * 4) + soc : BUF_OOB, 0, 0);
+                                          ok ? ((m * (int)p.ldc + n) * 4) + soc : BUF_OOB, 0, 0);
             }
             continue;
           }
@@ -2157,10 +2167,10 @@ __global__ void __launch_bounds__(BNT, 1) gemm_ps_kernel(GemmP p) {
             } else if (!rowok || n0 + 8 <= p.nvalid || n0 >= p.nvalid) {
               const bool ok = rowok && n0 < p.nvalid;
               llvm_raw_buffer_store_v4i32(__builtin_bit_cast(i32x4, o), rsC,
-                                          ok ? (int)(((long)m * p.ldc + n0) * 2) : BUF_OOB, 0, 0);
+                                          ok ? ((m * (int)p.ldc + n0) * 2) : BUF_OOB, 0, 0);
             } else {   // 4 valid columns at the right edge
               llvm_raw_buffer_store_v2i32(i32x2{(int)o[0], (int)o[1]}, rsC,
-                                          (int)(((long)m * p.ldc + n0) * 2), 0, 0);
+                                          ((m * (int)p.ldc + n0) * 2), 0, 0);
             }
           }
           if constexpr (NJ % 2 == 1) {
@@ -2168,7 +2178,7 @@ __global__ void __launch_bounds__(BNT, 1) gemm_ps_kernel(GemmP p) {
             const int n = nb + 16 * (NJ - 1) + 4 * lg;
             const bool ok = rowok && n < p.nvalid && !nost;
             llvm_raw_buffer_store_v2i32(i32x2{(int)a[0], (int)a[1]}, rsC,
-                                        ok ? (int)(((long)m * p.ldc + n) * 2) : BUF_OOB, 0, 0);
+                                        ok ? ((m * (int)p.ldc + n) * 2) : BUF_OOB, 0, 0);
           }
         }
       }
@@ -2288,6 +2298,9 @@ int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
     const int ps_t256 = ps_tm * ((p.N + 255) / 256), ps_t192 = ps_tm * ((p.N + 191) / 192);
     // a gate / residual operand (plain A only) takes the 256 x 192 instance (its register budget)
     const bool ps_op = p.gate || p.residual;
+    // a gate / residual operand takes the 256 x 192 instance (a 256 x 128 one, free of the
+    // spills of this one, measured slower: decoder gated dgrad 105-110 -> 120-122 us, step
+    // 18.05-18.11 -> 18.23-18.25 ms, tools/r04_eo.sh)
     const bool ps_w192 = ps_op ||
                          (long)((ps_t192 + 255) / 256) * 192 < (long)((ps_t256 + 255) / 256) * 256;
     const int ps_nt = ps_w192 ? ps_t192 : ps_t256;
