@@ -630,6 +630,69 @@ def test_gemm_persistent_short_k(cuda, M, N, K, op):
     assert rel(C, ref) < 1e-2
 
 
+@pytest.mark.parametrize("M,N,K,op,c32", [(6400, 384, 384, None, 0), (6400, 384, 1536, "residual", 0),
+                                          (6400, 1152, 1152, None, 1), (6400, 768, 384, "gate", 0),
+                                          (6400, 384, 776, None, 0), (31264, 80, 384, None, 0),
+                                          (31264, 384, 80, "residual", 0), (5000, 200, 3000, "gate", 1)])
+def test_gemm_persistent_small_tiles(cuda, M, N, K, op, c32):
+    """The persistent short-K kernel's 128 x 128 / 128 x 64 tile instances (round 4), which the
+    dispatcher picks below 160 tiles of 256 x 128 (the encoder / predictor / concat / mel-linear
+    shapes, M = 6400 or N = 80): bias + row scales + gate or residual epilogues, partial row /
+    column / K tiles, bf16 and fp32 outputs; fp32 reference on the same bf16 values, rel 1e-2."""
+    from fastspeech2 import ops
+    torch.manual_seed(M + N + K + 7)
+    A = torch.randn(M, K, device=cuda).to(torch.bfloat16)
+    W = (torch.randn(N, K, device=cuda) * 0.05).to(torch.bfloat16)
+    bias = torch.randn(N, device=cuda)
+    rs = (torch.rand(M, device=cuda) > 0.2).float()
+    rs2 = torch.rand(M, device=cuda) + 0.5
+    E = torch.randn(M, N + 8, device=cuda).to(torch.bfloat16)
+    x = A.float() @ W.float().t() + bias
+    kw = {}
+    if op == "gate":
+        x = torch.where(E[:, :N].float() > 0, x, torch.zeros_like(x)) * rs[:, None]
+        kw = dict(gate=E, ldg=N + 8)
+    elif op == "residual":
+        x = x * rs[:, None] + E[:, :N].float()
+        kw = dict(residual=E, ldr=N + 8)
+    else:
+        x = x * rs[:, None]
+    ref = x * rs2[:, None]
+    C = torch.full((M, N), float("nan"), device=cuda,
+                   dtype=torch.float32 if c32 else torch.bfloat16)
+    ops.gemm(M, N, K, A, K, W, K, C, N, dt=1, c_fp32=c32, bias=bias, row_scale=rs,
+             row_scale_post=rs2, **kw)
+    torch.cuda.synchronize()
+    assert torch.isfinite(C.float()).all()
+    assert rel(C, ref) < 1e-2
+
+
+def test_gemm_stream_grid_budget(cuda):
+    """fs2_set_stream_ctas: persistent GEMMs launched on a stream with a grid budget (the
+    weight-gradient side stream runs at 208 blocks) walk more tiles per block and give results
+    bit-identical to the full-grid launch, for the long-K (gemm_ps_kernel) and short-K
+    (gemm_pk_kernel, 128-row and 256-row tiles) instances."""
+    from fastspeech2 import ops, _native
+    torch.manual_seed(11)
+    shapes = [(31264, 1536, 3456), (31264, 1152, 384), (6400, 384, 1152)]
+    s_budget = torch.cuda.Stream()
+    assert _native.lib().fs2_set_stream_ctas(s_budget.cuda_stream, 64) == 0
+    assert _native.lib().fs2_set_stream_ctas(s_budget.cuda_stream, 4) != 0
+    for M, N, K in shapes:
+        A = torch.randn(M, K, device=cuda).to(torch.bfloat16)
+        W = (torch.randn(N, K, device=cuda) * 0.05).to(torch.bfloat16)
+        bias = torch.randn(N, device=cuda)
+        C0 = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+        ops.gemm(M, N, K, A, K, W, K, C0, N, dt=1, bias=bias, relu=1)
+        s_budget.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s_budget):
+            C1 = torch.full((M, N), float("nan"), device=cuda, dtype=torch.bfloat16)
+            ops.gemm(M, N, K, A, K, W, K, C1, N, dt=1, bias=bias, relu=1)
+        torch.cuda.current_stream().wait_stream(s_budget)
+        torch.cuda.synchronize()
+        assert torch.equal(C0, C1), (M, N, K)
+
+
 @pytest.mark.parametrize("M,N,K,conv", [(31264, 1152, 384, None), (6400, 384, 1536, None),
                                          (31264, 1536, 3456, (1, 977, 9, 384)),
                                          (31264, 384, 13824, (4, 977, 9, 1536)), (200, 80, 384, None)])
