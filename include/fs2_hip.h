@@ -106,9 +106,6 @@ int fs2_conv_fold(const float* Xpad, int nsplit, int64_t split_stride, int B, in
                   int C, void* out, int64_t ldo, const void* residual, int64_t ldr,
                   const float* row_scale, const float* row_scale_post, int dtype, void* stream);
 
-/* out[i] (+)= sum_{s < nslices} ws[s*stride + i], i < n (fp32; n, stride multiples of 4,
- * 16-byte aligned): the sum of split-K weight-gradient slices written by fs2_gemm with
- * split_stride (no atomics; fixed summation order)                                         */
 /* channel-major padded image for conv_mode 6 (backward of the SB Conv1d weights, App. A.1;
  * model.py:241-267 FFN conv1): out[c][b*(T+2P) + i] = X[b*T + reflect(i-P)][c] (reflect = 1)
  * or X[b*T + i-P][c] inside [0,T) and 0 outside (reflect = 0), i in [0, T+2P); columns
@@ -120,6 +117,9 @@ int fs2_pad_transpose(const void* X, int64_t ldx, int B, int T, int C, int P, in
                       void* out, int64_t ldo, int ncols, float* colsum, float* workspace,
                       int dtype, void* stream);
 
+/* out[i] (+)= sum_{s < nslices} ws[s*stride + i], i < n (fp32; n, stride multiples of 4,
+ * 16-byte aligned): the sum of split-K weight-gradient slices written by fs2_gemm with
+ * split_stride (no atomics; fixed summation order)                                         */
 int fs2_sum_slices(const float* ws, int nslices, int64_t stride, int64_t n, float* out,
                    int accumulate, void* stream);
 
