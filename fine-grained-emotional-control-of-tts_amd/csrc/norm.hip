@@ -175,7 +175,6 @@ struct LnBwdP {
   const float* row_mask; int relu_gate_in; char* ds; long ldds; char* dr; float p_r;
   uint32_t salt_r; float* part_g; float* part_b; int M, D; uint32_t seed; int rows_per_block;
   float* part_c; long pstride;  // partial rows are pstride floats apart (scalar kernel)
-  fs2_fold_src f;               // fs2_ln_bwd_fold: dy from a padded-domain conv data gradient
 };
 
 template <typename T>
@@ -485,55 +484,7 @@ __global__ void __launch_bounds__(256) ln_bwd_vec_kernel(LnBwdP p, float* part, 
 // (PostNet, D = 512) measured no faster this way (94 vs 103 us) and keeps the one-row kernel.  No tanh gate (that
 // case keeps the one-row kernel).  The one-row loop
 // keeps ~1.5 KB per wave in flight and ran at 1-2 TB/s (latency bound: 15 waves per CU).
-// dy row m, channels [c, c+8), of fs2_ln_bwd_fold: conv_fold8_kernel's arithmetic (same
-// summation order, same rounding), C = p.D
-__device__ __forceinline__ u32x4 fold_dy8(const fs2_fold_src& f, int m, int c, int C) {
-  const int T_ = f.T, P = f.P;
-  const int b = m / T_, s = m - b * T_;
-  const long rb = (long)b * (T_ + 2 * P);
-  const bool lo = s >= 1 && s <= P, hi = s >= T_ - 1 - P && s <= T_ - 2;
-  f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0;
-  for (int z = 0; z < f.nsplit; ++z) {
-    const float* X = f.Xpad + z * f.split_stride;
-    const float* x0 = X + (rb + s + P) * C + c;
-    a0 += *(const f32x4*)x0;
-    a1 += *(const f32x4*)(x0 + 4);
-    if (lo) {
-      const float* x1 = X + (rb + P - s) * C + c;
-      a0 += *(const f32x4*)x1;
-      a1 += *(const f32x4*)(x1 + 4);
-    }
-    if (hi) {
-      const float* x2 = X + (rb + 2 * (T_ - 1) - s + P) * C + c;
-      a0 += *(const f32x4*)x2;
-      a1 += *(const f32x4*)(x2 + 4);
-    }
-  }
-  const float r1 = f.row_scale ? f.row_scale[m] : 1.f, r2 = f.row_scale_post ? f.row_scale_post[m] : 1.f;
-  float rv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  if (f.residual) {
-    const u32x4 u = *(const u32x4*)((const bf16*)f.residual + (long)m * f.ldr + c);
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      rv[2 * w] = __builtin_bit_cast(float, u[w] << 16);
-      rv[2 * w + 1] = __builtin_bit_cast(float, u[w] & 0xffff0000u);
-    }
-  }
-  u32x4 o;
-#pragma unroll
-  for (int w = 0; w < 4; ++w) {
-    const int e = 2 * w;
-    const float v0 = w < 2 ? a0[e] : a1[e - 4], v1 = w < 2 ? a0[e + 1] : a1[e - 3];
-    float x0 = v0 * r1, x1 = v1 * r1;
-    if (f.residual) { x0 += rv[e]; x1 += rv[e + 1]; }
-    const bf16 h0 = (bf16)(x0 * r2), h1 = (bf16)(x1 * r2);
-    o[w] = (unsigned)__builtin_bit_cast(unsigned short, h0) |
-           ((unsigned)__builtin_bit_cast(unsigned short, h1) << 16);
-  }
-  return o;
-}
-
-template <int R, bool TANH, bool FOLD = false>
+template <int R, bool TANH>
 __global__ void __launch_bounds__(256) ln_bwd_rows_kernel(LnBwdP p, float* part, int npart,
                                                           int kind0) {
   constexpr int V = 8;
@@ -565,10 +516,7 @@ __global__ void __launch_bounds__(256) ln_bwd_rows_kernel(LnBwdP p, float* part,
       const bool ok = row < rend;
       const int rr = ok ? row : row0;
       us[j] = act ? *(const u32x4*)((const bf16*)p.s + (long)rr * p.lds + d0) : u32x4{0, 0, 0, 0};
-      if constexpr (FOLD)
-        ud[j] = act ? fold_dy8(p.f, rr, d0, p.D) : u32x4{0, 0, 0, 0};
-      else
-        ud[j] = act ? *(const u32x4*)((const bf16*)p.dy + (long)rr * p.lddy + d0) : u32x4{0, 0, 0, 0};
+      ud[j] = act ? *(const u32x4*)((const bf16*)p.dy + (long)rr * p.lddy + d0) : u32x4{0, 0, 0, 0};
       mean[j] = p.mean[rr];
       rstd[j] = p.rstd[rr];
       rm[j] = p.row_mask ? p.row_mask[rr] : 1.f;
@@ -975,24 +923,15 @@ extern "C" int fs2_ln_fwd(const void* x, int64_t ldx, const void* r, int64_t ldr
   return 0;
 }
 
-static int ln_bwd_impl(const void* dy, int64_t lddy, const fs2_fold_src* fold, const void* s,
-                       int64_t lds, const float* mean, const float* rstd, const float* gamma,
-                       const float* beta, int do_tanh, float p_o, uint32_t salt_o,
-                       const float* row_mask, int relu_gate_in, void* ds, int64_t ldds,
-                       void* dr, float p_r, uint32_t salt_r, float* dgamma, float* dbeta,
-                       float* dcol, int M, int D, int dtype, uint32_t seed, float* workspace,
-                       void* stream) {
+extern "C" int fs2_ln_bwd(const void* dy, int64_t lddy, const void* s, int64_t lds,
+                          const float* mean, const float* rstd, const float* gamma,
+                          const float* beta, int do_tanh, float p_o, uint32_t salt_o,
+                          const float* row_mask, int relu_gate_in, void* ds, int64_t ldds,
+                          void* dr, float p_r, uint32_t salt_r, float* dgamma, float* dbeta,
+                          float* dcol, int M, int D, int dtype, uint32_t seed, float* workspace,
+                          void* stream) {
   if (M <= 0) return 0;
-  if (D <= 0 || D > 64 * MAXJ || (!dy && !fold) || !s || !ds || !gamma || !beta) return FS2_EINVAL;
-  if (fold) {
-    // the fused fold runs on the 8-channel rows kernel only
-    if (dtype != FS2_BF16 || do_tanh || D % 8 || D > 512 || !fold->Xpad || fold->T <= 0 ||
-        fold->P < 0 || (fold->P > 0 && fold->P >= fold->T) || M % fold->T || !a16(fold->Xpad) ||
-        (fold->residual && (!a16(fold->residual) || fold->ldr % 8)) ||
-        (fold->nsplit > 1 && (fold->split_stride % 4 ||
-                              fold->split_stride < (long)(M / fold->T) * (fold->T + 2 * fold->P) * D)))
-      return FS2_EINVAL;
-  }
+  if (D <= 0 || D > 64 * MAXJ || !dy || !s || !ds || !gamma || !beta) return FS2_EINVAL;
   if ((dgamma || dbeta) && (!dgamma || !dbeta)) return FS2_EINVAL;
   if ((dgamma || dcol) && !workspace) return FS2_EINVAL;
   const int nb = ln_blocks(M);
@@ -1004,24 +943,16 @@ static int ln_bwd_impl(const void* dy, int64_t lddy, const fs2_fold_src* fold, c
   float* pcl = dcol ? workspace + (dgamma ? 2 * D : 0) : nullptr;
   LnBwdP p{(const char*)dy, lddy, (const char*)s, lds, mean, rstd, gamma, beta, do_tanh, p_o,
            salt_o, row_mask, relu_gate_in, (char*)ds, ldds, (char*)dr, p_r, salt_r, pg, pb, M,
-           D, seed, rpb, pcl, (long)npart * D, {}};
-  if (fold) {
-    p.f = *fold;
-    if (p.f.nsplit < 1) p.f.nsplit = 1;
-  }
+           D, seed, rpb, pcl, (long)npart * D};
   hipStream_t st = (hipStream_t)stream;
   const int V = dtype == FS2_BF16 ? 8 : 4;
   const int nch = (D / V + 63) / 64;
-  const bool vec = (D % V) == 0 && nch <= 4 && (fold || (a16(dy) && (lddy % V) == 0)) &&
-                   a16(s) && (lds % V) == 0 && a16(ds) && (ldds % V) == 0 && (!dr || a16(dr)) &&
+  const bool vec = (D % V) == 0 && nch <= 4 && a16(dy) && (lddy % V) == 0 && a16(s) &&
+                   (lds % V) == 0 && a16(ds) && (ldds % V) == 0 && (!dr || a16(dr)) &&
                    a16(gamma) && a16(beta);
   float* part = npart ? workspace : nullptr;
   const int kind0 = dgamma ? 0 : 2;
-  if (fold) {
-    if (!vec) return FS2_EINVAL;
-    if (ln_rows_r() == 2) hipLaunchKernelGGL((ln_bwd_rows_kernel<2, false, true>), dim3(nb), dim3(256), 0, st, p, part, npart, kind0);
-    else hipLaunchKernelGGL((ln_bwd_rows_kernel<4, false, true>), dim3(nb), dim3(256), 0, st, p, part, npart, kind0);
-  } else if (dtype == FS2_BF16) {
+  if (dtype == FS2_BF16) {
     if (!vec) hipLaunchKernelGGL(ln_bwd_kernel<bf16>, dim3(nb), dim3(256), 0, st, p);
     else if (nch == 1 && ln_rows_r() == 4 && !do_tanh) hipLaunchKernelGGL((ln_bwd_rows_kernel<4, false>), dim3(nb), dim3(256), 0, st, p, part, npart, kind0);
     else if (nch == 1 && ln_rows_r() == 2 && !do_tanh) hipLaunchKernelGGL((ln_bwd_rows_kernel<2, false>), dim3(nb), dim3(256), 0, st, p, part, npart, kind0);
@@ -1046,32 +977,6 @@ static int ln_bwd_impl(const void* dy, int64_t lddy, const fs2_fold_src* fold, c
     FS2_CHECK_LAUNCH();
   }
   return 0;
-}
-
-extern "C" int fs2_ln_bwd(const void* dy, int64_t lddy, const void* s, int64_t lds,
-                          const float* mean, const float* rstd, const float* gamma,
-                          const float* beta, int do_tanh, float p_o, uint32_t salt_o,
-                          const float* row_mask, int relu_gate_in, void* ds, int64_t ldds,
-                          void* dr, float p_r, uint32_t salt_r, float* dgamma, float* dbeta,
-                          float* dcol, int M, int D, int dtype, uint32_t seed, float* workspace,
-                          void* stream) {
-  if (!dy && M > 0) return FS2_EINVAL;
-  return ln_bwd_impl(dy, lddy, nullptr, s, lds, mean, rstd, gamma, beta, do_tanh, p_o, salt_o,
-                     row_mask, relu_gate_in, ds, ldds, dr, p_r, salt_r, dgamma, dbeta, dcol, M, D,
-                     dtype, seed, workspace, stream);
-}
-
-extern "C" int fs2_ln_bwd_fold(const fs2_fold_src* fold, const void* s, int64_t lds,
-                               const float* mean, const float* rstd, const float* gamma,
-                               const float* beta, float p_o, uint32_t salt_o,
-                               const float* row_mask, int relu_gate_in, void* ds, int64_t ldds,
-                               void* dr, float p_r, uint32_t salt_r, float* dgamma, float* dbeta,
-                               float* dcol, int M, int D, int dtype, uint32_t seed,
-                               float* workspace, void* stream) {
-  if (!fold && M > 0) return FS2_EINVAL;
-  return ln_bwd_impl(nullptr, 0, fold, s, lds, mean, rstd, gamma, beta, 0, p_o, salt_o, row_mask,
-                     relu_gate_in, ds, ldds, dr, p_r, salt_r, dgamma, dbeta, dcol, M, D, dtype,
-                     seed, workspace, stream);
 }
 
 extern "C" int fs2_colsum(const void* X, int64_t ldx, int M, int N, int dtype, float* out,

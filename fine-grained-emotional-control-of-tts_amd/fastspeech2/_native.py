@@ -86,16 +86,6 @@ class LossDesc(ctypes.Structure):
     ]
 
 
-class FoldSrc(ctypes.Structure):
-    """fs2_fold_src (include/fs2_hip.h)"""
-    _fields_ = [
-        ("Xpad", ctypes.c_void_p), ("nsplit", ctypes.c_int), ("split_stride", ctypes.c_int64),
-        ("T", ctypes.c_int), ("P", ctypes.c_int), ("residual", ctypes.c_void_p),
-        ("ldr", ctypes.c_int64), ("row_scale", ctypes.c_void_p),
-        ("row_scale_post", ctypes.c_void_p),
-    ]
-
-
 class WPrepDesc(ctypes.Structure):
     _fields_ = [
         ("W", ctypes.c_void_p), ("Wf", ctypes.c_void_p), ("Wb", ctypes.c_void_p),
@@ -125,8 +115,6 @@ SIGNATURES = {
                        I, I, I, U32, P]),
     "fs2_ln_bwd": (I, [P, I64, P, I64, P, P, P, P, I, Fl, U32, P, I, P, I64, P, Fl, U32, P, P, P,
                        I, I, I, U32, P, P]),
-    "fs2_ln_bwd_fold": (I, [P, P, I64, P, P, P, P, Fl, U32, P, I, P, I64, P, Fl, U32, P, P, P, I,
-                            I, I, U32, P, P]),
     "fs2_ln_workspace_floats": (I64, [I, I]),
     "fs2_attn_supported": (I, [I, I, I]),
     "fs2_attn_fwd": (I, [P, I64, P, I, I, I, I, I, Fl, Fl, U32, U32, P, I64, P, I, P]),

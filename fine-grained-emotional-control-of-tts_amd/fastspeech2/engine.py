@@ -20,7 +20,6 @@ import torch
 
 from . import _native as N
 from . import ops
-from . import streams
 from .ops import round_up
 
 _BK = {N.F32: 32, N.BF16: 64}
@@ -88,23 +87,6 @@ _NO_AUX = N.exp_flag("FS2_NO_AUX_STREAM")
 # (tools/r04_side.sh, 2 x 7 interleaved bench runs): 256 -> 18.23-18.29 ms, 176-240 ->
 # 18.01-18.13, 160 -> 18.87; 208 kept.  FS2_SIDE_CTAS overrides in the experiments build.
 _SIDE_CTAS = N.exp_int("FS2_SIDE_CTAS", 208)
-# cross-stream forks / joins through fence-free events (streams.py); FS2_TORCH_STREAM_WAIT=1 uses
-# torch's wait_stream (A/B in the experiments build)
-_TORCH_WAIT = N.exp_flag("FS2_TORCH_STREAM_WAIT")
-# AdamW in two launches when FusedTrainer.step defers the backward's final side-stream join: the
-# parameters of all but the first _ADAM_SPLIT encoder layers update while the side stream still
-# computes those layers' weight gradients (0: one launch after the join)
-_ADAM_SPLIT = N.exp_int("FS2_ADAM_SPLIT", 2)
-# the FFT block's conv1 data-gradient fold read in place by the LayerNorm backward that consumes
-# it (fs2_ln_bwd_fold) instead of a conv_fold launch and a dy tensor
-_FOLD_LN = N.exp_int("FS2_FOLD_LN", 1)
-
-
-def _wait(consumer, producer):
-    if _TORCH_WAIT:
-        consumer.wait_stream(producer)
-    else:
-        streams.wait(consumer, producer)
 
 
 def ps_plain_ok(M, lda, N, ldb, out_rows, ldc, out_bytes):
@@ -180,12 +162,6 @@ class FS2Engine:
         self.timer = None            # optional KernelTimer: HIP events around tagged launches
         self._km = {}                # conv_mode-6 images, reused layer after layer (side stream)
         self._img = {}               # per-layer zero-padded dY images (_dy_image)
-        # FusedTrainer.step sets defer_side_join: backward then leaves the main stream's wait for
-        # the weight-gradient stream to adamw_step (_side_pending), which splits the update
-        self.defer_side_join = False
-        self._side_pending = False
-        self._adam_mark = None
-        self._adam_split = None
 
     def _tic(self, tag):
         if self.timer is not None:
@@ -225,7 +201,7 @@ class FS2Engine:
         main = torch.cuda.current_stream(self.dev)
         if self._aux is not None and main.cuda_stream == self._aux.cuda_stream:
             return None          # the aux chain is already off the critical path
-        _wait(self._side, main)
+        self._side.wait_stream(main)
         ctx = torch.cuda.stream(self._side)
         ctx.__enter__()
         return ctx, tensors
@@ -242,7 +218,7 @@ class FS2Engine:
     def _aux_fork(self, *tensors):
         """enter the aux stream after everything queued so far on the current stream"""
         main = torch.cuda.current_stream(self.dev)
-        _wait(self._aux, main)
+        self._aux.wait_stream(main)
         for t in tensors:
             if t is not None:
                 t.record_stream(self._aux)
@@ -255,7 +231,7 @@ class FS2Engine:
 
     def _aux_join(self, main, *tensors):
         """the main stream waits for the aux chain; its outputs are now used on main"""
-        _wait(main, self._aux)
+        main.wait_stream(self._aux)
         for t in tensors:
             if t is not None:
                 t.record_stream(main)
@@ -271,14 +247,8 @@ class FS2Engine:
         return [main] if self._side is None else [main, self._side]
 
     def side_join(self):
-        self._side_pending = False
         if self._side is not None:
-            _wait(torch.cuda.current_stream(self.dev), self._side)
-
-    def finish_backward(self):
-        """the main stream waits for a deferred weight-gradient stream (no-op otherwise)"""
-        if self._side_pending:
-            self.side_join()
+            torch.cuda.current_stream(self.dev).wait_stream(self._side)
 
     def empty(self, *shape, dtype=None):
         return torch.empty(*shape, dtype=dtype or self.adt, device=self.dev)
@@ -359,45 +329,10 @@ class FS2Engine:
             self.prepare_weights(force=True)      # builds the descriptor table
         if getattr(self, "_rtable", None) is None:
             self._rtable = ops.adamw_ranges_table(self._adam_ranges(), self.dev)
-        scal = (decay_mul, omb1, beta2, omb2, step_size, bc2_sqrt, eps, gscale)
-        if self._side_pending and self._adam_mark is not None:
-            # the early parameters' gradients are complete at the side-stream mark recorded after
-            # encoder layer _ADAM_SPLIT's weight gradients; the late ones after the whole stream
-            if self._adam_split is None:
-                self._adam_split = [self._adam_tables(late) for late in (False, True)]
-            (we, re_), (wl, rl) = self._adam_split
-            self._adam_mark.wait(torch.cuda.current_stream(self.dev))
-            ops.adamw_prep(we, re_, m._flat, m._gflat, opt.exp_avg, opt.exp_avg_sq, *scal,
-                           dt=self.dt)
-            self.side_join()
-            ops.adamw_prep(wl, rl, m._flat, m._gflat, opt.exp_avg, opt.exp_avg_sq, *scal,
-                           dt=self.dt)
-        else:
-            self.finish_backward()
-            ops.adamw_prep(self._wtable, self._rtable, m._flat, m._gflat, opt.exp_avg,
-                           opt.exp_avg_sq, *scal, dt=self.dt)
+        ops.adamw_prep(self._wtable, self._rtable, m._flat, m._gflat, opt.exp_avg, opt.exp_avg_sq,
+                       decay_mul, omb1, beta2, omb2, step_size, bc2_sqrt, eps, gscale, dt=self.dt)
         m.mark_params_updated()
         self._prepared_version = (m._param_version, m._flat._version)
-
-    def _adam_late(self, name):
-        """parameters of the first _ADAM_SPLIT encoder layers (the side stream's last weight
-        gradients)"""
-        mt = re.match(r"encoder[.]layers[.]([0-9]+)[.]", name)
-        return mt is not None and int(mt.group(1)) < _ADAM_SPLIT
-
-    def _adam_tables(self, late):
-        """(weight table, range table) of fs2_adamw_prep over the late / early parameters"""
-        ents = [e for n, e in self._wentries.items() if self._adam_late(n) == late]
-        rng = []
-        for name, off, k, _, _ in self.m._layout:
-            if name in self._wspecs or self._adam_late(name) != late:
-                continue
-            if rng and off - (rng[-1][0] + rng[-1][1]) < 16:
-                rng[-1] = (rng[-1][0], off + k - rng[-1][0])
-            else:
-                rng.append((off, k))
-        wt = ops.weight_prep_table(ents) if ents else (None, 0, 0)
-        return wt, ops.adamw_ranges_table(rng, self.dev)
 
     def _dtag(self, kind, wname, T):
         """per-call-site tag for the detailed timer (FS2 layer indices folded)"""
@@ -442,16 +377,13 @@ class FS2Engine:
                 self.w[wname][0].shape[1] == KW * C and
                 ps_plain_ok((M // T) * (T + 2 * P), C, O, KW * C, M, O, 2))
 
-    def _dgrad(self, dY, lddy, M, T, wname, out, ldo, n_out=None, fold_out=False, **epi):
-        """data gradient into ``out``; with fold_out a reflect conv may instead return the
-        fold source (ops.conv_fold_src) for ln_bwd(fold=...), leaving ``out`` unwritten"""
+    def _dgrad(self, dY, lddy, M, T, wname, out, ldo, n_out=None, **epi):
         tag = self._dtag("dgrad", wname, T)
         if tag:
             self._tic(tag)
-        r = self._dgrad_impl(dY, lddy, M, T, wname, out, ldo, n_out, fold_out, **epi)
+        self._dgrad_impl(dY, lddy, M, T, wname, out, ldo, n_out, **epi)
         if tag:
             self._toc(tag)
-        return r
 
     def _pad_dgrad(self, wname):
         """FFN conv1 data gradients over a zero-padded token-major dY image (bf16): the
@@ -506,7 +438,7 @@ class FS2Engine:
         img = buf[:n].view((B + 1) * L, F)[T:]
         return img, img[2 * P:]
 
-    def _dgrad_impl(self, dY, lddy, M, T, wname, out, ldo, n_out=None, fold_out=False, **epi):
+    def _dgrad_impl(self, dY, lddy, M, T, wname, out, ldo, n_out=None, **epi):
         O, C, KW = self._wspecs[wname]
         _, Wb = self.w[wname]
         if KW == 1:
@@ -529,11 +461,6 @@ class FS2Engine:
             ops.gemm(Mp, C, KW * O, dY, lddy, Wb, KW * O, Xpad, C, dt=self.dt, conv=(4, T, KW, O),
                      c_fp32=1, split_k=split, split_stride=Mp * C if split > 1 else 0)
         assert set(epi) <= {"residual", "ldr", "row_scale", "row_scale_post"}, epi
-        if fold_out and self.dt == 1 and C % 8 == 0 and C <= 512:
-            return ops.conv_fold_src(Xpad, T, P, residual=epi.get("residual"),
-                                     ldr=epi.get("ldr", 0), row_scale=epi.get("row_scale"),
-                                     row_scale_post=epi.get("row_scale_post"), nsplit=split,
-                                     split_stride=Mp * C)
         ops.conv_fold(Xpad, B, T, P, C, out, ldo, dt=self.dt, residual=epi.get("residual"),
                       ldr=epi.get("ldr", 0), row_scale=epi.get("row_scale"),
                       row_scale_post=epi.get("row_scale_post"), nsplit=split,
@@ -805,19 +732,16 @@ class FS2Engine:
         self._wgrad(dHc, F, ctx["X1"], D, M, T, w1,
                     gemm_tag="ffn_conv1_wgrad." + prefix.split(".")[0],
                     bias=prefix + "pos_ffn.0.conv.bias", dy_img=img)
-        fold = self._dgrad((img,) if pad else dHc, F, M, T, w1, dX1, D, residual=ds2, ldr=D,
-                           fold_out=bool(_FOLD_LN))
+        self._dgrad((img,) if pad else dHc, F, M, T, w1, dX1, D, residual=ds2, ldr=D)
         del dY, dHc, ds2, img
         lnws = self.ws(ops.ln_ws(M, D))
         ds1, dAo = self.empty(M, D), self.empty(M, D)
-        # with ``fold`` the LayerNorm backward reads the conv1 data gradient's padded-domain
-        # output and folds it in place (dX1 unwritten)
         ops.ln_bwd(dX1, D, ctx["s1"], D, ctx["mean1"], ctx["rstd1"], P[prefix + "norm1.norm.weight"],
                    P[prefix + "norm1.norm.bias"], ds1, D, M, D, dt=self.dt, ws=lnws, seed=seed,
                    dr=dAo, p_r=p_drop, salt_r=ctx["s_r1"], dgamma=G[prefix + "norm1.norm.weight"],
                    dbeta=G[prefix + "norm1.norm.bias"],
-                   dcol=G[prefix + "self_att.att.out_proj.bias"], fold=fold)
-        del dX1, fold
+                   dcol=G[prefix + "self_att.att.out_proj.bias"])
+        del dX1
         wo = prefix + "self_att.att.out_proj.weight"
         dAtt = self.empty(M, D)
         self._wgrad(dAo, D, ctx["Att"], D, M, T, wo)
@@ -1250,22 +1174,12 @@ class FS2Engine:
                    dgamma=G["encoder.norm.norm.weight"], dbeta=G["encoder.norm.norm.bias"])
         notify("conditioning")
         dX = dXl
-        defer = (self.defer_side_join and self._side is not None and self.on_grads_ready is None
-                 and 0 < _ADAM_SPLIT < c.enc_num_layers
-                 and not torch.cuda.is_current_stream_capturing())
         for i in reversed(range(c.enc_num_layers)):
             dX = self._fft_bwd(dX, ctx["enc_ctx"][i], B, Tp, f"encoder.layers.{i}.", H_e,
                                ctx["p_enc"], seed)
             notify(f"encoder.layers.{i}")
-            if defer and i == _ADAM_SPLIT:
-                if self._adam_mark is None:
-                    self._adam_mark = streams.Mark()
-                self._adam_mark.record(self._side)
         ops.embed_bwd(ctx["tokens"], dX, keep_p, Mp, D, c.n_char,
                       G["encPreNet.token_embedding.Embedding.weight"], dt=self.dt,
                       ws=self.ws(ops.embed_bwd_ws(D, c.n_char)))
-        if defer:
-            self._side_pending = True      # adamw_step (or finish_backward) joins
-        else:
-            self.side_join()
+        self.side_join()
         notify("prenet")

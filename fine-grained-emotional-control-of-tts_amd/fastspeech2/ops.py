@@ -68,15 +68,6 @@ def conv_fold(Xpad, B, T, P, C, out, ldo, *, dt, residual=None, ldr=0, row_scale
                                _p(row_scale), _p(row_scale_post), dt, _s()), "fs2_conv_fold")
 
 
-def conv_fold_src(Xpad, T, P, *, residual=None, ldr=0, row_scale=None, row_scale_post=None,
-                  nsplit=1, split_stride=0):
-    """fs2_fold_src of conv_fold's arguments, for ln_bwd(fold=...); the tensors are kept with
-    the descriptor so they outlive its use"""
-    f = N.FoldSrc(_p(Xpad), nsplit, split_stride, T, P, _p(residual), ldr, _p(row_scale),
-                  _p(row_scale_post))
-    return f, (Xpad, residual, row_scale, row_scale_post)
-
-
 def pad_transpose(X, ldx, B, T, C, P, reflect, out, ldo, ncols, *, dt, colsum=None, ws=None):
     _chk(N.lib().fs2_pad_transpose(_p(X), ldx, B, T, C, P, reflect, _p(out), ldo, ncols,
                                    _p(colsum), _p(ws), dt, _s()), "fs2_pad_transpose")
@@ -114,17 +105,7 @@ def ln_fwd(x, ldx, gamma, beta, eps, y, ldy, mean, rstd, M, D, *, dt, seed=0, r=
 
 def ln_bwd(dy, lddy, s, lds, mean, rstd, gamma, beta, ds, ldds, M, D, *, dt, ws, seed=0,
            do_tanh=0, p_o=0.0, salt_o=0, row_mask=None, relu_gate_in=0, dr=None, p_r=0.0,
-           salt_r=0, dgamma=None, dbeta=None, dcol=None, fold=None):
-    """fold: dy is not a tensor but the reflect fold of a padded conv data gradient (the
-    FoldSrc conv_fold_src() returns; dy / lddy are ignored) -- fs2_ln_bwd_fold"""
-    if fold is not None:
-        assert not do_tanh
-        _chk(N.lib().fs2_ln_bwd_fold(ctypes.byref(fold[0]), _p(s), lds, _p(mean), _p(rstd),
-                                     _p(gamma), _p(beta), p_o, salt_o, _p(row_mask),
-                                     relu_gate_in, _p(ds), ldds, _p(dr), p_r, salt_r, _p(dgamma),
-                                     _p(dbeta), _p(dcol), M, D, dt, seed & 0xffffffff, _p(ws),
-                                     _s()), "fs2_ln_bwd_fold")
-        return
+           salt_r=0, dgamma=None, dbeta=None, dcol=None):
     _chk(N.lib().fs2_ln_bwd(_p(dy), lddy, _p(s), lds, _p(mean), _p(rstd), _p(gamma), _p(beta),
                             do_tanh, p_o, salt_o, _p(row_mask), relu_gate_in, _p(ds), ldds, _p(dr),
                             p_r, salt_r, _p(dgamma), _p(dbeta), _p(dcol), M, D, dt,

@@ -57,8 +57,6 @@ class FusedAdamW:
             # the update also writes the next forward's GEMM weight images
             eng.adamw_step(self, *args)
             return
-        if eng is not None:
-            eng.finish_backward()
         ops.adamw(m._flat, m._gflat, self.exp_avg, self.exp_avg_sq, m._flat.numel(), *args)
         m.mark_params_updated()
 

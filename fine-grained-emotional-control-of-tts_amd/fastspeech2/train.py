@@ -15,7 +15,6 @@ import torch
 import torch.distributed as dist
 
 from . import ops
-from . import streams
 from .loss import fused_loss
 from .optim import FusedAdamW
 
@@ -73,7 +72,7 @@ class GradBucketer:
                                                 group=self.group, async_op=True))
         else:
             for st in streams or [torch.cuda.current_stream(self.flat.device)]:
-                streams.wait(self.comm, st)
+                self.comm.wait_stream(st)
             with torch.cuda.stream(self.comm):
                 self.handles.append(dist.all_reduce(self.flat[s:e], op=dist.ReduceOp.SUM,
                                                     group=self.group, async_op=True))
@@ -91,7 +90,7 @@ class GradBucketer:
         for h in self.handles:
             h.wait()
         if self.comm is not None:
-            streams.wait(torch.cuda.current_stream(self.flat.device), self.comm)
+            torch.cuda.current_stream(self.flat.device).wait_stream(self.comm)
         self.handles, self.launched = [], set()
 
 
@@ -210,12 +209,6 @@ class FusedTrainer:
             mlm = mel_len_max if mel_len_max is not None else batch[3].shape[1]
             loss = self._graph_for(batch, intensity, mlm).replay(batch, intensity, self.seed)
         else:
-            # single process: the backward leaves its last wait for the weight-gradient stream
-            # to the AdamW launch, which updates most parameters before that stream has finished
-            self.eng.defer_side_join = self.bucketer is None
-            try:
-                loss = self.forward_backward(batch, intensity, mel_len_max)
-            finally:
-                self.eng.defer_side_join = False
+            loss = self.forward_backward(batch, intensity, mel_len_max)
         self.apply()
         return loss

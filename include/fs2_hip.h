@@ -163,29 +163,6 @@ int fs2_ln_bwd(const void* dy, int64_t lddy, const void* s, int64_t lds, const f
                int dtype, uint32_t seed, float* workspace, void* stream);
 int64_t fs2_ln_workspace_floats(int M, int D);
 
-/* fs2_ln_bwd whose dy is the reflect-padding fold of a padded-domain conv data gradient, read
- * in place (SB Conv1d backward feeding the FFT block's LayerNorm backward, model.py:241-267):
- * row m = b*T + s of dy is fs2_conv_fold's output row m, bf16(((Xpad[b, s+P] + reflect terms)
- * * row_scale + residual) * row_scale_post), with the same arithmetic and rounding -- no dy
- * tensor and no fold launch.  bf16 only, D % 8 == 0, D <= 512, no tanh gate, Xpad / residual
- * 16-byte aligned (FS2_EINVAL otherwise; fs2_conv_fold + fs2_ln_bwd is the general form).    */
-typedef struct fs2_fold_src {
-  const float* Xpad;            /* fp32 [nsplit][B*(T+2P)][D] (split-K slices, summed here)  */
-  int nsplit;
-  int64_t split_stride;         /* floats between slices                                    */
-  int T, P;
-  const void* residual;         /* bf16 [B*T][ldr] or NULL                                   */
-  int64_t ldr;
-  const float* row_scale;       /* [B*T] or NULL                                             */
-  const float* row_scale_post;  /* [B*T] or NULL                                             */
-} fs2_fold_src;
-int fs2_ln_bwd_fold(const fs2_fold_src* fold, const void* s, int64_t lds, const float* mean,
-                    const float* rstd, const float* gamma, const float* beta, float p_o,
-                    uint32_t salt_o, const float* row_mask, int relu_gate_in, void* ds,
-                    int64_t ldds, void* dr, float p_r, uint32_t salt_r, float* dgamma,
-                    float* dbeta, float* dcol, int M, int D, int dtype, uint32_t seed,
-                    float* workspace, void* stream);
-
 /* ------------------------------------------------------------------------------------------
  * Attention softmax over materialised scores, with the reference's key masking
  * (model.py:338-343 / 414-419 + key_padding_mask; head-major tiling quirk):

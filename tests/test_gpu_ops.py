@@ -412,49 +412,6 @@ def test_conv_fold_vector_form_bit_exact(cuda, split):
     assert torch.equal(a, b[:, :C])
 
 
-@pytest.mark.parametrize("Bn,T,P,split", [(4, 977, 4, 1), (3, 200, 4, 3), (5, 37, 1, 2),
-                                         (2, 9, 4, 1)])
-def test_ln_bwd_fold_bit_exact(cuda, Bn, T, P, split):
-    """fs2_ln_bwd_fold (the LayerNorm backward reading the conv data gradient's padded-domain
-    output and folding it in place) equals conv_fold + fs2_ln_bwd bit for bit: ds, dr and the
-    three column sums, with residual, row scales, dropout on both outputs and the relu gate;
-    split-K slices; T = 9 with P = 4 puts every row in a reflect band"""
-    from fastspeech2 import ops
-    torch.manual_seed(T + split)
-    D = 384
-    M, Mp = Bn * T, Bn * (T + 2 * P)
-    Xpad = torch.randn(split, Mp, D, device=cuda)
-    res = torch.randn(M, D, device=cuda).to(torch.bfloat16)
-    rs = (torch.rand(M, device=cuda) > 0.3).float()
-    rs2 = torch.rand(M, device=cuda)
-    x = torch.randn(M, D, device=cuda).to(torch.bfloat16)
-    g, b = torch.randn(D, device=cuda), torch.randn(D, device=cuda)
-    y = torch.empty(M, D, device=cuda, dtype=torch.bfloat16)
-    mean, rstd = torch.empty(M, device=cuda), torch.empty(M, device=cuda)
-    ops.ln_fwd(x, D, g, b, 1e-5, y, D, mean, rstd, M, D, dt=1)
-    keep = (torch.rand(M, device=cuda) > 0.2).float()
-    outs = []
-    for fused in (False, True):
-        dy = torch.empty(M, D, device=cuda, dtype=torch.bfloat16)
-        fold = None
-        if fused:
-            fold = ops.conv_fold_src(Xpad, T, P, residual=res, ldr=D, row_scale=rs,
-                                     row_scale_post=rs2, nsplit=split, split_stride=Mp * D)
-        else:
-            ops.conv_fold(Xpad, Bn, T, P, D, dy, D, dt=1, residual=res, ldr=D, row_scale=rs,
-                          row_scale_post=rs2, nsplit=split, split_stride=Mp * D)
-        ds = torch.empty(M, D, device=cuda, dtype=torch.bfloat16)
-        dr = torch.empty(M, D, device=cuda, dtype=torch.bfloat16)
-        dg, db, dc = (torch.zeros(D, device=cuda) for _ in range(3))
-        ws = torch.empty(int(ops.ln_ws(M, D)), device=cuda)
-        ops.ln_bwd(dy, D, x, D, mean, rstd, g, b, ds, D, M, D, dt=1, ws=ws, seed=5, p_o=0.1,
-                   salt_o=3, row_mask=keep, relu_gate_in=1, dr=dr, p_r=0.2, salt_r=9,
-                   dgamma=dg, dbeta=db, dcol=dc, fold=fold)
-        outs.append((ds, dr, dg, db, dc))
-    for a, c in zip(*outs):
-        assert torch.equal(a, c)
-
-
 @pytest.mark.parametrize("Bn,T", [(32, 640), (1, 640), (32, 200), (32, 977)])
 def test_gemm_big_tile_paths_bf16(cuda, Bn, T):
     """BASELINE-sized GEMMs that take the 256x128 LDS-DMA kernel (gemm_big_kernel): implicit
