@@ -1462,6 +1462,231 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256_kernel(GemmP p) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// gemm256r_kernel: the 256x256 phased kernel for K-major A and B with FULL-ROW LDS regions.
+//
+// gemm256_kernel's regions are K-halves (256 rows x 64 B): every LDS-DMA piece fetches 16 rows
+// of 64-byte half lines.  Here a region is 128 rows x one whole 64-wide K-tile (128 B per row,
+// 8 rows x 128 B per DMA piece): A0 = tile rows {0-63, 128-191} (the wave rows of m-half 0),
+// A1 = rows {64-127, 192-255}, B0 = columns 0-127, B1 = columns 128-255; chunk swizzle
+// (row >> 1) & 7 (conflict-free ds_read_b128 for the 16-lane groups).  Phases run (m-half, k-half)
+// = (p >> 1, p & 1): B fragments of both k-halves are read in phases 0-1 and kept in registers
+// (bfr[2][4]), so B0 / B1 / A0 are free after phase 1 and A1 after phase 3.  Region schedule,
+// one or two per phase: phase 0 of tile t issues A1 of t+1 (read from its phase 2: 6 phases to
+// land), phase 2 issues A0 and B0 of t+2 and phase 3 B1 of t+2 (read from phase 0 of t+2: 6 / 5
+// phases).  Counted waits, both 8 pieces in the steady state: phase 3 retires the next tile's
+// A0 / B0 / B1, phase 1 this tile's A1 (group 1 before its memory-section barrier, group 0 after
+// its MFMAs -- before the barrier that precedes the first read, as gemm256_kernel).  Each wave
+// drains its own ds_reads (lgkmcnt(0)) before the barrier that ends its memory section, so a
+// region is restaged one phase after its last read.  Taps: a 64-wide K-tile lies in one tap
+// (conv_c % 64 == 0 for CM > 0; the dispatcher falls back to gemm256_kernel otherwise).
+constexpr int G4R_REG = 16384;
+__device__ __forceinline__ int g4r_sw(int r) { return (r >> 1) & 7; }
+__device__ __forceinline__ bf16x8 g4r_frag(const char* rg, int row, int chunk) {
+  return *(const bf16x8*)(rg + row * 128 + ((chunk ^ g4r_sw(row)) << 4));
+}
+
+template <int CM>   // 0 plain, 1 / 4 / 5 implicit conv with 64-aligned taps
+__global__ void __launch_bounds__(G4_NT, 1) gemm256r_kernel(GemmP p) {
+  __shared__ __attribute__((aligned(16))) char smem[G4_LDS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int nwg = p.tiles_m * p.tiles_n;
+  const int orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int tm = bid / p.tiles_n, tn = bid - tm * p.tiles_n;
+  const int m0 = tm * 256, n0 = tn * 256;
+  const int z = p.split_k > 1 ? 0 : blockIdx.z;
+  const long zb = z / p.batch_div, zh = z - zb * p.batch_div;
+  const char* Ab = p.A + (zb * p.sA1 + zh * p.sA2) * 2;
+  const char* Bb = p.B + (zb * p.sB1 + zh * p.sB2) * 2;
+  const int K = p.K;
+  const int nk_all = (K + 63) / 64;
+  int kt0 = 0, kt1 = nk_all;
+  if (p.split_k > 1) {
+    const int kps = (nk_all + p.split_k - 1) / p.split_k;
+    kt0 = blockIdx.z * kps;
+    kt1 = min(nk_all, kt0 + kps);
+  }
+  const int rpu = CM == 4 ? p.conv_t + 2 * p.conv_p : p.conv_t;
+
+  // per-lane DMA state: piece i (0, 1) of region q (A0 / A1) or h (B0 / B1) covers region rows
+  // (2 wave + i) * 8 + lane / 8; the lane fetches logical chunk lc[i] of that row
+  const i32x4 rsA = make_rsrc(Ab), rsB = make_rsrc(Bb);
+  int lc[2];
+  int avo[4], at[4], abt[4];
+  bool aval[4];
+  int bvo[4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int rho = (2 * wave + i) * 8 + (lane >> 3);
+    lc[i] = (lane & 7) ^ g4r_sw(rho);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int idx = q * 2 + i;
+      const int row = m0 + (rho < 64 ? rho : rho + 64) + q * 64;
+      aval[idx] = row < p.M;
+      const int rr = aval[idx] ? row : 0;
+      const int b = CM ? rr / rpu : 0;
+      abt[idx] = b * p.conv_t;
+      at[idx] = rr - b * rpu;
+      avo[idx] = aval[idx] ? (int)(((long)rr * p.lda + lc[i] * 8) * 2) : BUF_OOB;
+      const int col = n0 + rho + q * 128;
+      bvo[idx] = col < p.N ? (int)(((long)col * p.ldb + lc[i] * 8) * 2) : BUF_OOB;
+    }
+  }
+  int a_tap = -1;
+
+  auto issueA = [&](int q, int rel) {
+    const int k0 = (kt0 + rel) * 64;
+    char* dst = smem + (rel & 1) * G4_SLOT + q * G4R_REG + wave * 2048;
+    const bool kin = k0 + 64 <= K;
+    if constexpr (CM > 0) {
+      const int j = k0 / p.conv_c;            // wave-uniform: the K-tile lies in one tap
+      const int c0 = k0 - j * p.conv_c;
+      if (j != a_tap) {
+        a_tap = j;
+#pragma unroll
+        for (int idx = 0; idx < 4; ++idx) {
+          int ts;
+          bool ok = aval[idx];
+          if (CM == 1) {
+            ts = reflect_idx(at[idx] + (j - p.conv_p) * p.conv_dil, p.conv_t);
+          } else {
+            ts = CM == 5 ? at[idx] + (j - p.conv_p) * p.conv_dil : at[idx] - j;
+            ok = ok && ts >= 0 && ts < p.conv_t;
+          }
+          avo[idx] = ok ? (int)(((long)(abt[idx] + ts) * p.lda + lc[idx & 1] * 8) * 2) : BUF_OOB;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int vo = (kin || k0 + lc[i] * 8 < K) ? avo[q * 2 + i] : BUF_OOB;
+        blds16(rsA, vo, c0 * 2, dst + i * 1024);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int vo = (kin || k0 + lc[i] * 8 < K) ? avo[q * 2 + i] : BUF_OOB;
+        blds16(rsA, vo, k0 * 2, dst + i * 1024);
+      }
+    }
+  };
+  auto issueB = [&](int h, int rel) {
+    const int k0 = (kt0 + rel) * 64;
+    char* dst = smem + (rel & 1) * G4_SLOT + (2 + h) * G4R_REG + wave * 2048;
+    const bool kin = k0 + 64 <= K;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int vo = (kin || k0 + lc[i] * 8 < K) ? bvo[h * 2 + i] : BUF_OOB;
+      blds16(rsB, vo, k0 * 2, dst + i * 1024);
+    }
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = kt1 - kt0;
+  if (nk > 0) { issueA(0, 0); issueB(0, 0); issueB(1, 0); issueA(1, 0); }
+  if (nk > 1) {
+    issueA(0, 1); issueB(0, 1); issueB(1, 1);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // tile 0's A0 / B0 / B1
+  } else {
+    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  if (wr == 1) __builtin_amdgcn_s_barrier();   // group 1 runs half a phase behind
+  __builtin_amdgcn_sched_barrier(0);
+
+  bf16x8 af[4], bfr[2][4];
+  for (int it = 0; it < nk; ++it) {
+    const char* slot = smem + (it & 1) * G4_SLOT;
+    const bool more = it + 1 < nk, more2 = it + 2 < nk;
+#pragma unroll
+    for (int ph = 0; ph < 4; ++ph) {
+      const int mq = ph >> 1, s = ph & 1;
+      // ---- memory section: this phase's fragments, the phase's regions of a later tile ----
+      if (mq == 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          bfr[s][j] = g4r_frag(slot + (2 + (wc >> 1)) * G4R_REG,
+                               (wc & 1) * 64 + j * 16 + (lane & 15), s * 4 + (lane >> 4));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        af[i] = g4r_frag(slot + mq * G4R_REG, wr * 64 + i * 16 + (lane & 15), s * 4 + (lane >> 4));
+      if (ph == 0 && more) issueA(1, it + 1);
+      if (ph == 2 && more2) { issueA(0, it + 2); issueB(0, it + 2); }
+      if (ph == 3 && more2) issueB(1, it + 2);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (wr == 1) {
+        if (ph == 1) {
+          if (more) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+          else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else if (ph == 3 && more) {
+          if (more2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+          else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        }
+      }
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      // ---- matrix section: rows mq of this wave x K = 32 ----
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[mq * 4 + i][j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[s][j], acc[mq * 4 + i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      if (wr == 0) {
+        if (ph == 1) {
+          if (more) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+          else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else if (ph == 3 && more) {
+          if (more2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+          else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        }
+      }
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  if (wr == 0) __builtin_amdgcn_s_barrier();  // balance the stagger
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+
+  __syncthreads();
+
+  // ---- epilogue: as gemm256_kernel (two 256x128 column halves through LDS) ----
+  char* Cb = p.C + (zb * p.sC1 + zh * p.sC2) * (p.c_fp32 ? 4 : 2);
+  if (p.split_stride > 0 && p.split_k > 1) Cb += (long)blockIdx.z * p.split_stride * 4;
+  const char* Rb = p.residual ? p.residual + (zb * p.sR1 + zh * p.sR2) * 2 : nullptr;
+  float* cs = (float*)smem;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if ((wc >> 1) == h) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = wr * 128 + i * 16 + (lane >> 4) * 4 + r;
+            const int col = (wc & 1) * 64 + j * 16 + (lane & 15);
+            cs[row * 128 + (col ^ cs_swz(row))] = acc[i][j][r];
+          }
+    }
+    __syncthreads();
+    if (n0 + h * 128 < p.nvalid) epilogue_256x128(p, cs, m0, n0 + h * 128, Cb, Rb, tid);
+    __syncthreads();
+  }
+}
+
 // ============================================================================================
 // Persistent 256x128 kernel for the short-K GEMMs (K <= 1536, plain K-major A and B: the
 // attention projections, the FFN conv2 and the data gradients of the 1x1 weights).
@@ -2418,7 +2643,16 @@ int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
       }
       dim3 g2(tiles256, 1, gz2);
       const int cm = conv_variant(q, 32);
-      if (ak && bk) {
+      // full-row regions (gemm256r_kernel) for K-major A and B with 64-aligned taps;
+      // FS2_G4R=0 (experiments build) keeps gemm256_kernel
+      static const bool g4r = getenv_int("FS2_G4R", 1) != 0;
+      const int cm64 = conv_variant(q, 64);
+      if (ak && bk && g4r && cm64 >= 0) {
+        if (cm64 == 0) hipLaunchKernelGGL((gemm256r_kernel<0>), g2, dim3(G4_NT), 0, s, q);
+        else if (cm64 == 1) hipLaunchKernelGGL((gemm256r_kernel<1>), g2, dim3(G4_NT), 0, s, q);
+        else if (cm64 == 4) hipLaunchKernelGGL((gemm256r_kernel<4>), g2, dim3(G4_NT), 0, s, q);
+        else hipLaunchKernelGGL((gemm256r_kernel<5>), g2, dim3(G4_NT), 0, s, q);
+      } else if (ak && bk) {
         if (cm == 0) hipLaunchKernelGGL((gemm256_kernel<true, true, 0, 0>), g2, dim3(G4_NT), 0, s, q);
         else if (cm == 1) hipLaunchKernelGGL((gemm256_kernel<true, true, 1, 0>), g2, dim3(G4_NT), 0, s, q);
         else if (cm == 4) hipLaunchKernelGGL((gemm256_kernel<true, true, 4, 0>), g2, dim3(G4_NT), 0, s, q);

@@ -1,0 +1,52 @@
+"""gemm256r_kernel (full-row LDS regions) vs gemm256_kernel (K-half regions): run once with
+FS2_G4R=1 and once with FS2_G4R=0 (experiments library); prints time per shape and saves the
+outputs to /tmp/g4r_<flag>.pt so the two runs can be compared bit for bit (same K order)."""
+import os
+import sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "fine-grained-emotional-control-of-tts_amd"))
+os.environ.setdefault("FS2_HIP_LIB", os.path.join(ROOT, "fine-grained-emotional-control-of-tts_amd",
+                                                  "fastspeech2", "libfs2_hip_exp.so"))
+import torch  # noqa: E402
+
+
+def timed(fn, n=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(n):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / n * 1e3
+
+
+def main():
+    from fastspeech2 import ops
+    flag = os.environ.get("FS2_G4R", "1")
+    torch.manual_seed(0)
+    bf = torch.bfloat16
+    outs = {}
+    cases = [("dec conv1 fwd (reflect k9)", 32, 977, 384, 1536, 9, 1),
+             ("postnet conv fwd (reflect k5)", 32, 977, 512, 512, 5, 1),
+             ("plain 31264x1536x3456", 32, 977, 3456, 1536, 1, 0),
+             ("plain 8192^3", 8, 1024, 8192, 8192, 1, 0),
+             ("plain 4096^3", 4, 1024, 4096, 4096, 1, 0)]
+    for name, B, T, C, O, KW, conv in cases:
+        M, K = B * T, KW * C
+        X = (torch.rand(M, C, device="cuda") * 2 - 1).to(bf)
+        W = (torch.rand(O, K, device="cuda") * 2 - 1).to(bf) * 0.05
+        bias = torch.randn(O, device="cuda")
+        Y = torch.empty(M, O, device="cuda", dtype=bf)
+        kw = dict(conv=(1, T, KW, C)) if conv else {}
+        fn = lambda: ops.gemm(M, O, K, X, C, W, K, Y, O, dt=1, bias=bias, relu=1, **kw)
+        t = timed(fn)
+        outs[name] = Y.cpu()
+        print(f"G4R={flag} {name:32s} {t:8.1f} us  {2.0 * M * O * K / t / 1e6:6.0f} TF/s", flush=True)
+    torch.save(outs, f"/tmp/g4r_{flag}.pt")
+
+
+if __name__ == "__main__":
+    main()
