@@ -789,26 +789,34 @@ __device__ __forceinline__ void epilogue_256x128(const GemmP& p, const float* cs
   }
   const int c8 = (tid & 15) * 8;
   const int n = n0 + c8;
+  if (n >= p.nvalid) return;
+  const int nn = min(8, p.nvalid - n);
+  // this thread's 8 bias columns, loaded once per tile half (in the pass loop the compiler had
+  // to reload them after every output store, which may alias the bias)
+  float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (p.bias) {
+    if (nn == 8) {
+      const f32x4 b0 = *(const f32x4*)(p.bias + n), b1 = *(const f32x4*)(p.bias + n + 4);
+      bv[0] = b0[0]; bv[1] = b0[1]; bv[2] = b0[2]; bv[3] = b0[3];
+      bv[4] = b1[0]; bv[5] = b1[1]; bv[6] = b1[2]; bv[7] = b1[3];
+    } else {
+      for (int e = 0; e < nn; ++e) bv[e] = p.bias[n + e];
+    }
+  }
 #pragma unroll 2
   for (int pass = 0; pass < 8; ++pass) {
     const int row = (tid >> 4) + 32 * pass;
     const int m = m0 + row;
-    if (m >= p.mvalid || n >= p.nvalid) continue;
+    if (m >= p.mvalid) continue;
     const int sw = cs_swz(row);
     const f32x4 lo = *(const f32x4*)&cs[row * 128 + (c8 ^ sw)];
     const f32x4 hi = *(const f32x4*)&cs[row * 128 + ((c8 + 4) ^ sw)];
     float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    const int nn = min(8, p.nvalid - n);
     const float rs = p.row_scale ? p.row_scale[m] : 1.f;
     const float rs2 = p.row_scale_post ? p.row_scale_post[m] : 1.f;
     if (p.bias) {
-      if (nn == 8) {
-        const f32x4 b0 = *(const f32x4*)(p.bias + n), b1 = *(const f32x4*)(p.bias + n + 4);
-        v[0] += b0[0]; v[1] += b0[1]; v[2] += b0[2]; v[3] += b0[3];
-        v[4] += b1[0]; v[5] += b1[1]; v[6] += b1[2]; v[7] += b1[3];
-      } else {
-        for (int e = 0; e < nn; ++e) v[e] += p.bias[n + e];
-      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += bv[e];
     }
     float g[8], rr[8];
     if (p.gate) load8<bf16>(g, (const bf16*)p.gate + (long)m * p.ldg + n, nn);
@@ -1486,7 +1494,12 @@ __device__ __forceinline__ bf16x8 g4r_frag(const char* rg, int row, int chunk) {
   return *(const bf16x8*)(rg + row * 128 + ((chunk ^ g4r_sw(row)) << 4));
 }
 
-template <int CM>   // 0 plain, 1 / 4 / 5 implicit conv with 64-aligned taps
+// TR: the MFMA operands swapped (B fragment as the A operand), so a lane's accumulator holds 4
+// consecutive OUTPUT COLUMNS of one row; the epilogue then stores straight from registers: an
+// exchange between lanes l and l ^ 16 over two row fragments gives each lane 8 consecutive
+// columns, written as one 16-byte store (bf16 output, no gate / split; see the dispatcher), with
+// no LDS staging and no block barrier.  The products and their order per output are unchanged.
+template <int CM, bool TR = false>   // CM: 0 plain, 1 / 4 / 5 implicit conv with 64-aligned taps
 __global__ void __launch_bounds__(G4_NT, 1) gemm256r_kernel(GemmP p) {
   __shared__ __attribute__((aligned(16))) char smem[G4_LDS];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1604,6 +1617,17 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256r_kernel(GemmP p) {
   __builtin_amdgcn_sched_barrier(0);
 
   bf16x8 af[4], bfr[2][4];
+  // timing switches (experiments build; wrong results): 8 no DMA issue in the loop, 16 no
+  // fragment reads in the loop, 64 no setprio, 128 no counted waits in the loop, 512 no read
+  // drain before the memory-section barrier, 1024 no barrier after the MFMA section, 2048 no
+  // barrier before it, 4096 no epilogue
+  const int xf = XFLAGS(p);
+  if (xf & 16) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = g4r_frag(smem, i * 16 + (lane & 15), lane >> 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { bfr[0][j] = af[j]; bfr[1][j] = af[j]; }
+  }
   for (int it = 0; it < nk; ++it) {
     const char* slot = smem + (it & 1) * G4_SLOT;
     const bool more = it + 1 < nk, more2 = it + 2 < nk;
@@ -1611,20 +1635,25 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256r_kernel(GemmP p) {
     for (int ph = 0; ph < 4; ++ph) {
       const int mq = ph >> 1, s = ph & 1;
       // ---- memory section: this phase's fragments, the phase's regions of a later tile ----
-      if (mq == 0) {
+      if (!(xf & 16)) {
+        if (mq == 0) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          bfr[s][j] = g4r_frag(slot + (2 + (wc >> 1)) * G4R_REG,
-                               (wc & 1) * 64 + j * 16 + (lane & 15), s * 4 + (lane >> 4));
+          for (int j = 0; j < 4; ++j)
+            bfr[s][j] = g4r_frag(slot + (2 + (wc >> 1)) * G4R_REG,
+                                 (wc & 1) * 64 + j * 16 + (lane & 15), s * 4 + (lane >> 4));
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          af[i] = g4r_frag(slot + mq * G4R_REG, wr * 64 + i * 16 + (lane & 15), s * 4 + (lane >> 4));
       }
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        af[i] = g4r_frag(slot + mq * G4R_REG, wr * 64 + i * 16 + (lane & 15), s * 4 + (lane >> 4));
-      if (ph == 0 && more) issueA(1, it + 1);
-      if (ph == 2 && more2) { issueA(0, it + 2); issueB(0, it + 2); }
-      if (ph == 3 && more2) issueB(1, it + 2);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (wr == 1) {
+      if (!(xf & 8)) {
+        if (ph == 0 && more) issueA(1, it + 1);
+        if (ph == 2 && more2) { issueA(0, it + 2); issueB(0, it + 2); }
+        if (ph == 3 && more2) issueB(1, it + 2);
+      }
+      if (!(xf & 512)) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      else if (xf & 16) asm volatile("" ::: "memory");
+      if (wr == 1 && !(xf & 128)) {
         if (ph == 1) {
           if (more) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
           else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1633,18 +1662,19 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256r_kernel(GemmP p) {
           else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
         }
       }
-      __builtin_amdgcn_s_barrier();
+      if (!(xf & 2048)) __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
       // ---- matrix section: rows mq of this wave x K = 32 ----
-      __builtin_amdgcn_s_setprio(1);
+      if (!(xf & 64)) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           acc[mq * 4 + i][j] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[s][j], acc[mq * 4 + i][j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-      if (wr == 0) {
+              TR ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[s][j], af[i], acc[mq * 4 + i][j], 0, 0, 0)
+                 : __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[s][j], acc[mq * 4 + i][j], 0, 0, 0);
+      if (!(xf & 64)) __builtin_amdgcn_s_setprio(0);
+      if (wr == 0 && !(xf & 128)) {
         if (ph == 1) {
           if (more) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
           else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1653,7 +1683,7 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256r_kernel(GemmP p) {
           else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
         }
       }
-      __builtin_amdgcn_s_barrier();
+      if (!(xf & 1024)) __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
     }
   }
@@ -1663,9 +1693,68 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256r_kernel(GemmP p) {
   __syncthreads();
 
   // ---- epilogue: as gemm256_kernel (two 256x128 column halves through LDS) ----
+  if (XFLAGS(p) & 4096) {   // timing: keep the accumulators live, store nothing
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) asm volatile("" :: "v"(acc[i][j]));
+    return;
+  }
   char* Cb = p.C + (zb * p.sC1 + zh * p.sC2) * (p.c_fp32 ? 4 : 2);
   if (p.split_stride > 0 && p.split_k > 1) Cb += (long)blockIdx.z * p.split_stride * 4;
   const char* Rb = p.residual ? p.residual + (zb * p.sR1 + zh * p.sR2) * 2 : nullptr;
+  if constexpr (TR) {
+    // lane row q = lane >> 4: after the swap, even q hold row fragment 2t, odd q fragment 2t+1,
+    // columns j*16 + (q >> 1)*8 .. +7
+    const int q = lane >> 4;
+    const int ncol0 = n0 + wc * 64 + (q >> 1) * 8;
+    float bv[4][8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = ncol0 + j * 16;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) bv[j][e] = 0.f;
+      if (p.bias && n < p.nvalid) {
+        const f32x4 b0 = *(const f32x4*)(p.bias + n), b1 = *(const f32x4*)(p.bias + n + 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { bv[j][e] = b0[e]; bv[j][e + 4] = b1[e]; }
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int m = m0 + wr * 128 + (2 * t + (q & 1)) * 16 + (lane & 15);
+      const bool mok = m < p.mvalid;
+      const float rs = (p.row_scale && mok) ? p.row_scale[m] : 1.f;
+      const float rs2 = (p.row_scale_post && mok) ? p.row_scale_post[m] : 1.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float v[8];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          // even lane rows keep fragment 2t and take the partner's (lane ^ 16) columns 4..7 of
+          // it; odd lane rows keep fragment 2t+1 and take the partner's columns 0..3
+          const float own = (q & 1) ? acc[2 * t + 1][j][r] : acc[2 * t][j][r];
+          const float give = (q & 1) ? acc[2 * t][j][r] : acc[2 * t + 1][j][r];
+          const float got = __shfl_xor(give, 16, 64);
+          v[r] = (q & 1) ? got : own;
+          v[r + 4] = (q & 1) ? own : got;
+        }
+        const int n = ncol0 + j * 16;
+        if (!mok || n >= p.nvalid) continue;
+        float rr[8];
+        if (Rb) load8<bf16>(rr, (const bf16*)Rb + (long)m * p.ldr + n, 8);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float x = epi_act(v[e] + bv[j][e], p.relu);
+          x *= rs;
+          if (Rb) x += rr[e];
+          v[e] = x * rs2;
+        }
+        store8<bf16>((bf16*)Cb + (long)m * p.ldc + n, v, 8);
+      }
+    }
+    return;
+  }
   float* cs = (float*)smem;
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
@@ -2648,7 +2737,14 @@ int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
       static const bool g4r = getenv_int("FS2_G4R", 1) != 0;
       const int cm64 = conv_variant(q, 64);
       if (ak && bk && g4r && cm64 >= 0) {
-        if (cm64 == 0) hipLaunchKernelGGL((gemm256r_kernel<0>), g2, dim3(G4_NT), 0, s, q);
+        // register-direct epilogue (TR): bf16 output, no gate, one K split, 8-column granules
+        static const bool g4tr = getenv_int("FS2_G4R_TR", 1) != 0;
+        const bool tr = g4tr && q.vec_ok && !q.c_fp32 && !q.gate && q.split_k <= 1 &&
+                        q.nvalid % 8 == 0 && q.ldc % 8 == 0 && (!q.residual || q.ldr % 8 == 0) &&
+                        (q.relu <= 1) && !q.accumulate;
+        if (cm64 == 0 && tr) hipLaunchKernelGGL((gemm256r_kernel<0, true>), g2, dim3(G4_NT), 0, s, q);
+        else if (cm64 == 1 && tr) hipLaunchKernelGGL((gemm256r_kernel<1, true>), g2, dim3(G4_NT), 0, s, q);
+        else if (cm64 == 0) hipLaunchKernelGGL((gemm256r_kernel<0>), g2, dim3(G4_NT), 0, s, q);
         else if (cm64 == 1) hipLaunchKernelGGL((gemm256r_kernel<1>), g2, dim3(G4_NT), 0, s, q);
         else if (cm64 == 4) hipLaunchKernelGGL((gemm256r_kernel<4>), g2, dim3(G4_NT), 0, s, q);
         else hipLaunchKernelGGL((gemm256r_kernel<5>), g2, dim3(G4_NT), 0, s, q);

@@ -34,18 +34,30 @@ def main():
              ("plain 31264x1536x3456", 32, 977, 3456, 1536, 1, 0),
              ("plain 8192^3", 8, 1024, 8192, 8192, 1, 0),
              ("plain 4096^3", 4, 1024, 4096, 4096, 1, 0)]
+    only = os.environ.get("G4R_ONLY")
     for name, B, T, C, O, KW, conv in cases:
+        if only and only not in name:
+            continue
         M, K = B * T, KW * C
-        X = (torch.rand(M, C, device="cuda") * 2 - 1).to(bf)
-        W = (torch.rand(O, K, device="cuda") * 2 - 1).to(bf) * 0.05
+        data = os.environ.get("G4R_DATA", "rand")
+        if data == "zero":
+            X = torch.zeros(M, C, device="cuda", dtype=bf)
+            W = torch.zeros(O, K, device="cuda", dtype=bf)
+        elif data == "act":   # LayerNorm-output-like activations, init-scale weights
+            X = torch.randn(M, C, device="cuda").to(bf)
+            W = (torch.randn(O, K, device="cuda") * (1.0 / K) ** 0.5).to(bf)
+        else:
+            X = (torch.rand(M, C, device="cuda") * 2 - 1).to(bf)
+            W = (torch.rand(O, K, device="cuda") * 2 - 1).to(bf) * 0.05
         bias = torch.randn(O, device="cuda")
         Y = torch.empty(M, O, device="cuda", dtype=bf)
         kw = dict(conv=(1, T, KW, C)) if conv else {}
         fn = lambda: ops.gemm(M, O, K, X, C, W, K, Y, O, dt=1, bias=bias, relu=1, **kw)
         t = timed(fn)
         outs[name] = Y.cpu()
-        print(f"G4R={flag} {name:32s} {t:8.1f} us  {2.0 * M * O * K / t / 1e6:6.0f} TF/s", flush=True)
-    torch.save(outs, f"/tmp/g4r_{flag}.pt")
+        print(f"G4R={flag} data={data} flags={os.environ.get('FS2_G4_FLAGS', '0')} {name:32s} {t:8.1f} us  {2.0 * M * O * K / t / 1e6:6.0f} TF/s", flush=True)
+    if not only:
+        torch.save(outs, f"/tmp/g4r_{flag}.pt")
 
 
 if __name__ == "__main__":
