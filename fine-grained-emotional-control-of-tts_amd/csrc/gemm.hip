@@ -2529,9 +2529,12 @@ void launch4(const GemmP& p, dim3 grid, hipStream_t s, int ak, int bk) {
 // Persistent-kernel grid budget per stream (fs2_set_stream_ctas): a stream that shares the GPU
 // with a latency-critical one (the weight-gradient side stream beside the data-gradient chain)
 // can leave CUs free by sizing its persistent grids below the CU count.  Default 256.
+// A table of the last 64 streams given a budget (torch hands out pooled streams, so an engine
+// per model in one process registers a new one each time); the oldest entry is replaced.
 struct StreamCtas { hipStream_t s; int ctas; };
-StreamCtas g_stream_ctas[8];
-int g_nstream_ctas = 0;
+constexpr int kStreamCtasSlots = 64;
+StreamCtas g_stream_ctas[kStreamCtasSlots];
+int g_nstream_ctas = 0, g_stream_ctas_next = 0;
 int stream_ctas(hipStream_t s) {
   for (int i = 0; i < g_nstream_ctas; ++i)
     if (g_stream_ctas[i].s == s) return g_stream_ctas[i].ctas;
@@ -2822,8 +2825,12 @@ extern "C" int fs2_set_stream_ctas(void* stream, int ctas) {
   const hipStream_t s = (hipStream_t)stream;
   for (int i = 0; i < g_nstream_ctas; ++i)
     if (g_stream_ctas[i].s == s) { g_stream_ctas[i].ctas = ctas / 8 * 8; return 0; }
-  if (g_nstream_ctas == 8) return FS2_EINVAL;
-  g_stream_ctas[g_nstream_ctas++] = {s, ctas / 8 * 8};
+  if (g_nstream_ctas < kStreamCtasSlots) {
+    g_stream_ctas[g_nstream_ctas++] = {s, ctas / 8 * 8};
+  } else {
+    g_stream_ctas[g_stream_ctas_next] = {s, ctas / 8 * 8};
+    g_stream_ctas_next = (g_stream_ctas_next + 1) % kStreamCtasSlots;
+  }
   return 0;
 }
 

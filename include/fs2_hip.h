@@ -95,7 +95,8 @@ int fs2_gemm(const fs2_gemm_desc* d, void* stream);
 /* grid budget of the persistent GEMM kernels launched on `stream` (default 256 = one block per
  * CU): a stream that runs beside a latency-critical one -- the weight-gradient side stream
  * beside the data-gradient chain of the train step (model.py:279-441 backward) -- leaves
- * 256 - ctas CUs to the other stream's kernels.  8 <= ctas <= 256 (rounded down to 8). */
+ * 256 - ctas CUs to the other stream's kernels.  8 <= ctas <= 256 (rounded down to 8); the
+ * budgets of the last 64 streams given one are kept (older ones revert to 256).             */
 int fs2_set_stream_ctas(void* stream, int ctas);
 
 /* reflect-padding adjoint + dgrad epilogue (K16): Xpad fp32 [B][T+2P][C] from conv_mode 4
