@@ -1499,8 +1499,12 @@ __device__ __forceinline__ bf16x8 g4r_frag(const char* rg, int row, int chunk) {
 // exchange between lanes l and l ^ 16 over two row fragments gives each lane 8 consecutive
 // columns, written as one 16-byte store (bf16 output, no gate / split; see the dispatcher), with
 // no LDS staging and no block barrier.  The products and their order per output are unchanged.
-template <int CM, bool TR = false>   // CM: 0 plain, 1 / 4 / 5 implicit conv with 64-aligned taps
+// WN: output columns per wave (64: 256x256 tiles; 48: 256x192 tiles for N = 384 outputs, TR only
+// -- the B regions hold 96 columns, and waves 6-7's B pieces fill region rows 96-127, never read).
+template <int CM, bool TR = false, int WN = 64>   // CM: 0 plain, 1 / 4 / 5 implicit conv
 __global__ void __launch_bounds__(G4_NT, 1) gemm256r_kernel(GemmP p) {
+  static_assert(WN == 64 || (WN == 48 && TR), "the 192-wide tile has only the direct epilogue");
+  constexpr int NJ = WN / 16, BR = 2 * WN;   // column fragments per wave, B rows per region
   __shared__ __attribute__((aligned(16))) char smem[G4_LDS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1510,7 +1514,7 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256r_kernel(GemmP p) {
   const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
   const int tm = bid / p.tiles_n, tn = bid - tm * p.tiles_n;
-  const int m0 = tm * 256, n0 = tn * 256;
+  const int m0 = tm * 256, n0 = tn * (4 * WN);
   const int z = p.split_k > 1 ? 0 : blockIdx.z;
   const long zb = z / p.batch_div, zh = z - zb * p.batch_div;
   const char* Ab = p.A + (zb * p.sA1 + zh * p.sA2) * 2;
@@ -1546,8 +1550,8 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256r_kernel(GemmP p) {
       abt[idx] = b * p.conv_t;
       at[idx] = rr - b * rpu;
       avo[idx] = aval[idx] ? (int)(((long)rr * p.lda + lc[i] * 8) * 2) : BUF_OOB;
-      const int col = n0 + rho + q * 128;
-      bvo[idx] = col < p.N ? (int)(((long)col * p.ldb + lc[i] * 8) * 2) : BUF_OOB;
+      const int col = n0 + rho + q * BR;
+      bvo[idx] = (rho < BR && col < p.N) ? (int)(((long)col * p.ldb + lc[i] * 8) * 2) : BUF_OOB;
     }
   }
   int a_tap = -1;
@@ -1598,11 +1602,11 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256r_kernel(GemmP p) {
     }
   };
 
-  f32x4 acc[8][4];
+  f32x4 acc[8][NJ];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = kt1 - kt0;
   if (nk > 0) { issueA(0, 0); issueB(0, 0); issueB(1, 0); issueA(1, 0); }
@@ -1616,7 +1620,7 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256r_kernel(GemmP p) {
   if (wr == 1) __builtin_amdgcn_s_barrier();   // group 1 runs half a phase behind
   __builtin_amdgcn_sched_barrier(0);
 
-  bf16x8 af[4], bfr[2][4];
+  bf16x8 af[4], bfr[2][NJ];
   // timing switches (experiments build; wrong results): 8 no DMA issue in the loop, 16 no
   // fragment reads in the loop, 64 no setprio, 128 no counted waits in the loop, 512 no read
   // drain before the memory-section barrier, 1024 no barrier after the MFMA section, 2048 no
@@ -1626,7 +1630,7 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256r_kernel(GemmP p) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) af[i] = g4r_frag(smem, i * 16 + (lane & 15), lane >> 4);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) { bfr[0][j] = af[j]; bfr[1][j] = af[j]; }
+    for (int j = 0; j < NJ; ++j) { bfr[0][j] = af[j]; bfr[1][j] = af[j]; }
   }
   for (int it = 0; it < nk; ++it) {
     const char* slot = smem + (it & 1) * G4_SLOT;
@@ -1638,9 +1642,9 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256r_kernel(GemmP p) {
       if (!(xf & 16)) {
         if (mq == 0) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j)
+          for (int j = 0; j < NJ; ++j)
             bfr[s][j] = g4r_frag(slot + (2 + (wc >> 1)) * G4R_REG,
-                                 (wc & 1) * 64 + j * 16 + (lane & 15), s * 4 + (lane >> 4));
+                                 (wc & 1) * WN + j * 16 + (lane & 15), s * 4 + (lane >> 4));
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -1669,7 +1673,7 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256r_kernel(GemmP p) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < NJ; ++j)
           acc[mq * 4 + i][j] =
               TR ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[s][j], af[i], acc[mq * 4 + i][j], 0, 0, 0)
                  : __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[s][j], acc[mq * 4 + i][j], 0, 0, 0);
@@ -1697,7 +1701,7 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256r_kernel(GemmP p) {
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) asm volatile("" :: "v"(acc[i][j]));
+      for (int j = 0; j < NJ; ++j) asm volatile("" :: "v"(acc[i][j]));
     return;
   }
   char* Cb = p.C + (zb * p.sC1 + zh * p.sC2) * (p.c_fp32 ? 4 : 2);
@@ -1707,10 +1711,10 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256r_kernel(GemmP p) {
     // lane row q = lane >> 4: after the swap, even q hold row fragment 2t, odd q fragment 2t+1,
     // columns j*16 + (q >> 1)*8 .. +7
     const int q = lane >> 4;
-    const int ncol0 = n0 + wc * 64 + (q >> 1) * 8;
-    float bv[4][8];
+    const int ncol0 = n0 + wc * WN + (q >> 1) * 8;
+    float bv[NJ][8];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < NJ; ++j) {
       const int n = ncol0 + j * 16;
 #pragma unroll
       for (int e = 0; e < 8; ++e) bv[j][e] = 0.f;
@@ -1727,7 +1731,7 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256r_kernel(GemmP p) {
       const float rs = (p.row_scale && mok) ? p.row_scale[m] : 1.f;
       const float rs2 = (p.row_scale_post && mok) ? p.row_scale_post[m] : 1.f;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < NJ; ++j) {
         float v[8];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -1750,11 +1754,17 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256r_kernel(GemmP p) {
           if (Rb) x += rr[e];
           v[e] = x * rs2;
         }
-        store8<bf16>((bf16*)Cb + (long)m * p.ldc + n, v, 8);
+        if (p.c_fp32) {
+          float* Cf = (float*)Cb + (long)m * p.ldc + n;
+          *(f32x4*)Cf = f32x4{v[0], v[1], v[2], v[3]};
+          *(f32x4*)(Cf + 4) = f32x4{v[4], v[5], v[6], v[7]};
+        } else {
+          store8<bf16>((bf16*)Cb + (long)m * p.ldc + n, v, 8);
+        }
       }
     }
     return;
-  }
+  } else {
   float* cs = (float*)smem;
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
@@ -1773,6 +1783,7 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256r_kernel(GemmP p) {
     __syncthreads();
     if (n0 + h * 128 < p.nvalid) epilogue_256x128(p, cs, m0, n0 + h * 128, Cb, Rb, tid);
     __syncthreads();
+  }
   }
 }
 
@@ -2631,6 +2642,22 @@ int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
     if (!ps_go && !big_fits && p.conv_mode != 6) {
       if (p.conv_mode == 2) launch4<T, false, true>(p, grid, s, ak, bk);
       else launch4<T, true, true>(p, grid, s, ak, bk);
+      FS2_CHECK_LAUNCH();
+      return 0;
+    }
+    // long-K plain GEMMs with 192-wide tiles (the N = 384 data gradients of the FFN conv1) on the
+    // full-row-region 256x192 kernel: bit-identical but slower than the persistent kernel at the
+    // decoder conv1 data gradient (424 vs 406 us, step neutral; tools/r04_g48.sh) -- 12 MFMAs
+    // per phase against the same fragment reads.  Off; FS2_G4R48=1 (experiments build) enables.
+    static const bool g4r48 = getenv_int("FS2_G4R48", 0) != 0;
+    if (ps_go && g4r48 && ps_w192 && cm_ps == 0 && !ps_op && p.K >= 2048 && !p.c_row_t &&
+        p.nvalid % 8 == 0 && p.ldc % 8 == 0) {
+      GemmP q = p;
+      q.g4_flags = getenv_int("FS2_G4_FLAGS", 0);
+      q.tiles_m = ps_tm;
+      q.tiles_n = (p.N + 191) / 192;
+      hipLaunchKernelGGL((gemm256r_kernel<0, true, 48>), dim3(q.tiles_m * q.tiles_n), dim3(G4_NT), 0,
+                         s, q);
       FS2_CHECK_LAUNCH();
       return 0;
     }

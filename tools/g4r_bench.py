@@ -25,7 +25,7 @@ def timed(fn, n=20):
 
 def main():
     from fastspeech2 import ops
-    flag = os.environ.get("FS2_G4R", "1")
+    flag = os.environ.get("FS2_G4R", "1") + os.environ.get("FS2_G4R48", "1")
     torch.manual_seed(0)
     bf = torch.bfloat16
     outs = {}
@@ -56,6 +56,19 @@ def main():
         t = timed(fn)
         outs[name] = Y.cpu()
         print(f"G4R={flag} data={data} flags={os.environ.get('FS2_G4_FLAGS', '0')} {name:32s} {t:8.1f} us  {2.0 * M * O * K / t / 1e6:6.0f} TF/s", flush=True)
+    # FFN conv1 data gradient over the zero-padded dY image: A rows overlap (lda = F < K = 9F),
+    # N = 384, fp32 output (the 256x192 instance)
+    name = "dgrad 31680x384x13824 overlap"
+    if not only or only in name:
+        Mp, F, C, KW = 32 * 990, 1536, 384, 9
+        img = (torch.rand(Mp + 16, F, device="cuda") * 2 - 1).to(bf)
+        Wb = ((torch.rand(C, KW * F, device="cuda") * 2 - 1) * 0.05).to(bf)
+        Y = torch.empty(Mp, C, device="cuda")
+        fn = lambda: ops.gemm(Mp, C, KW * F, img, F, Wb, KW * F, Y, C, dt=1, c_fp32=1)
+        t = timed(fn)
+        outs[name] = Y.cpu()
+        print(f"G4R={flag} G4R48={os.environ.get('FS2_G4R48', '1')} {name:32s} {t:8.1f} us  "
+              f"{2.0 * Mp * C * KW * F / t / 1e6:6.0f} TF/s", flush=True)
     if not only:
         torch.save(outs, f"/tmp/g4r_{flag}.pt")
 
