@@ -1650,9 +1650,11 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256r_kernel(GemmP p) {
         for (int i = 0; i < 4; ++i)
           af[i] = g4r_frag(slot + mq * G4R_REG, wr * 64 + i * 16 + (lane & 15), s * 4 + (lane >> 4));
       }
+      // 8192 / 16384 (experiments): phase 2's B0 / phase 0's A1 issued inside the MFMA section
+      const bool mmB0 = xf & 8192, mmA1 = xf & 16384;
       if (!(xf & 8)) {
-        if (ph == 0 && more) issueA(1, it + 1);
-        if (ph == 2 && more2) { issueA(0, it + 2); issueB(0, it + 2); }
+        if (ph == 0 && more && !mmA1) issueA(1, it + 1);
+        if (ph == 2 && more2) { issueA(0, it + 2); if (!mmB0) issueB(0, it + 2); }
         if (ph == 3 && more2) issueB(1, it + 2);
       }
       if (!(xf & 512)) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1671,12 +1673,19 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256r_kernel(GemmP p) {
       // ---- matrix section: rows mq of this wave x K = 32 ----
       if (!(xf & 64)) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < 4; ++i) {
+        if (i == 2 && (xf & (8192 | 16384))) {
+          __builtin_amdgcn_sched_barrier(0);
+          if (ph == 2 && more2 && mmB0) issueB(0, it + 2);
+          if (ph == 0 && more && mmA1) issueA(1, it + 1);
+          __builtin_amdgcn_sched_barrier(0);
+        }
 #pragma unroll
         for (int j = 0; j < NJ; ++j)
           acc[mq * 4 + i][j] =
               TR ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[s][j], af[i], acc[mq * 4 + i][j], 0, 0, 0)
                  : __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[s][j], acc[mq * 4 + i][j], 0, 0, 0);
+      }
       if (!(xf & 64)) __builtin_amdgcn_s_setprio(0);
       if (wr == 0 && !(xf & 128)) {
         if (ph == 1) {
