@@ -31,6 +31,7 @@ def main():
     outs = {}
     cases = [("dec conv1 fwd (reflect k9)", 32, 977, 384, 1536, 9, 1),
              ("postnet conv fwd (reflect k5)", 32, 977, 512, 512, 5, 1),
+             ("enc conv1 fwd (reflect k9, T200)", 32, 200, 384, 1536, 9, 1),
              ("plain 31264x1536x3456", 32, 977, 3456, 1536, 1, 0),
              ("plain 8192^3", 8, 1024, 8192, 8192, 1, 0),
              ("plain 4096^3", 4, 1024, 4096, 4096, 1, 0)]
