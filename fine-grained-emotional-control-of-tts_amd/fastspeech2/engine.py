@@ -87,6 +87,9 @@ _NO_AUX = N.exp_flag("FS2_NO_AUX_STREAM")
 # (tools/r04_side.sh, 2 x 7 interleaved bench runs): 256 -> 18.23-18.29 ms, 176-240 ->
 # 18.01-18.13, 160 -> 18.87; 208 kept.  FS2_SIDE_CTAS overrides in the experiments build.
 _SIDE_CTAS = N.exp_int("FS2_SIDE_CTAS", 208)
+# AdamW of the decoder / mel-linear / PostNet parameters on the aux stream during the encoder
+# backward (FusedTrainer.step, one process); FS2_ADAM_OVERLAP=0 (experiments build): one launch
+_ADAM_OVERLAP = N.exp_int("FS2_ADAM_OVERLAP", 1)
 
 
 def ps_plain_ok(M, lda, N, ldb, out_rows, ldc, out_bytes):
@@ -162,6 +165,12 @@ class FS2Engine:
         self.timer = None            # optional KernelTimer: HIP events around tagged launches
         self._km = {}                # conv_mode-6 images, reused layer after layer (side stream)
         self._img = {}               # per-layer zero-padded dY images (_dy_image)
+        # FusedTrainer.step sets adam_split = (optimizer, AdamW scalars): the backward then updates
+        # the parameters whose gradients are final after the decoder (_adam_late) on the aux
+        # stream while the main stream runs the encoder backward; adamw_step_split does the rest
+        self.adam_split = None
+        self._adam_late_done = False
+        self._adam_tabs = None
 
     def _tic(self, tag):
         if self.timer is not None:
@@ -331,6 +340,57 @@ class FS2Engine:
             self._rtable = ops.adamw_ranges_table(self._adam_ranges(), self.dev)
         ops.adamw_prep(self._wtable, self._rtable, m._flat, m._gflat, opt.exp_avg, opt.exp_avg_sq,
                        decay_mul, omb1, beta2, omb2, step_size, bc2_sqrt, eps, gscale, dt=self.dt)
+        m.mark_params_updated()
+        self._prepared_version = (m._param_version, m._flat._version)
+
+    @staticmethod
+    def _adam_late(name):
+        """parameters whose gradients are complete once the backward has passed the decoder and
+        the variance adaptor (model.py:430-441 run first in the backward)"""
+        return name.startswith(("decoder.", "linear.", "postnet."))
+
+    def _adam_tables(self, late):
+        """(weight table, range table) of fs2_adamw_prep over the late / early parameters"""
+        ents = [e for n, e in self._wentries.items() if self._adam_late(n) == late]
+        rng = []
+        for name, off, k, _, _ in self.m._layout:
+            if name in self._wspecs or self._adam_late(name) != late:
+                continue
+            if rng and off - (rng[-1][0] + rng[-1][1]) < 16:
+                rng[-1] = (rng[-1][0], off + k - rng[-1][0])
+            else:
+                rng.append((off, k))
+        wt = ops.weight_prep_table(ents) if ents else (None, 0, 0)
+        return wt, ops.adamw_ranges_table(rng, self.dev)
+
+    def _adam_launch_late(self):
+        """the late parameters' AdamW on the aux stream, after everything queued on the main and
+        the weight-gradient streams (their gradients); the main stream does not wait here"""
+        opt, scal = self.adam_split
+        m = self.m
+        if self._wtable is None:
+            self.prepare_weights(force=True)
+        if self._adam_tabs is None:
+            self._adam_tabs = [self._adam_tables(late) for late in (False, True)]
+        wl, rl = self._adam_tabs[1]
+        h = self._aux_fork()
+        self._aux.wait_stream(self._side)
+        ops.adamw_prep(wl, rl, m._flat, m._gflat, opt.exp_avg, opt.exp_avg_sq, *scal, dt=self.dt)
+        self._aux_exit(h)
+        self._adam_late_done = True
+
+    def adamw_step_split(self, opt, scal):
+        """the rest of a step's AdamW (FusedTrainer.step): the early parameters on the main
+        stream after it has joined the aux stream's late update; the whole update if the
+        backward did not launch the late part"""
+        m = self.m
+        if not self._adam_late_done:
+            self.adamw_step(opt, *scal)
+            return
+        self._adam_late_done = False
+        we, re_ = self._adam_tabs[0]
+        torch.cuda.current_stream(self.dev).wait_stream(self._aux)
+        ops.adamw_prep(we, re_, m._flat, m._gflat, opt.exp_avg, opt.exp_avg_sq, *scal, dt=self.dt)
         m.mark_params_updated()
         self._prepared_version = (m._param_version, m._flat._version)
 
@@ -1160,6 +1220,10 @@ class FS2Engine:
             dZ = self._pred_bwd(d_dur, ctx["dctx"], keep_p, B, Tp, "durPred", ctx["p_var"], seed,
                                 residual=dZa, post_mask=True)
         notify("variance")
+        if (self.adam_split is not None and self._aux is not None and self._side is not None
+                and self.on_grads_ready is None and _ADAM_OVERLAP
+                and not torch.cuda.is_current_stream_capturing()):
+            self._adam_launch_late()
         # concat projection (Z = proj(cat) * keep) -- dZ is already masked
         ldc = ctx["ldc"]
         dcat = self.empty(Mp, 2 * D)

@@ -209,6 +209,18 @@ class FusedTrainer:
             mlm = mel_len_max if mel_len_max is not None else batch[3].shape[1]
             loss = self._graph_for(batch, intensity, mlm).replay(batch, intensity, self.seed)
         else:
-            loss = self.forward_backward(batch, intensity, mel_len_max)
+            # one process: the AdamW scalars are fixed before the backward, which updates the
+            # decoder / PostNet parameters on the aux stream during the encoder backward
+            split = self.bucketer is None and self.opt.fused_images()
+            if split:
+                scal = self.opt.begin_step(1.0)
+                self.eng.adam_split = (self.opt, scal)
+            try:
+                loss = self.forward_backward(batch, intensity, mel_len_max)
+            finally:
+                self.eng.adam_split = None
+            if split:
+                self.eng.adamw_step_split(self.opt, scal)
+                return loss
         self.apply()
         return loss
