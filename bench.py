@@ -426,7 +426,7 @@ def main():
         n, ms = ks.get("ffn_conv1_fwd.decoder", (0, float("nan")))
         kflop = 2.0 * (args.batch * Tm) * F * (KW * D)
         achieved = kflop / (ms * 1e-3) / 1e12 if n else None
-        traffic, traffic_src = (pmc_traffic("roofline", "gemm256r_kernel<1, true>")
+        traffic, traffic_src = (pmc_traffic("roofline", "gemm256r_kernel<1, true, 64>")
                                 if not args.scaled else (None, None))
         # second entry: the decoder FFN conv1 weight gradient, the largest GEMM bucket of the
         # step (2 M F 9D per launch like the forward); it runs on the side stream beside the
@@ -454,7 +454,7 @@ def main():
                                    + (", single speaker" if args.single_speaker else ""),
                        "global_batch": args.batch * world, "seq_len": Tm,
                        "valid_mel_frames_per_step": frames_all, "parallelism": f"dp{world}"},
-            "roofline": {"bound": "mfma", "kernel": "decoder FFN conv1 (k=9) implicit-GEMM fwd (gemm256r_kernel<1, true>: 256x256 tiles, full-row LDS-DMA regions, reflect conv in the loader, bias + ReLU in a register-direct epilogue)",
+            "roofline": {"bound": "mfma", "kernel": "decoder FFN conv1 (k=9) implicit-GEMM fwd (gemm256r_kernel<1, true, 64>: 256x256 tiles, full-row LDS-DMA regions, reflect conv in the loader, bias + ReLU in a register-direct epilogue)",
                          "achieved": achieved, "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": (achieved / MFMA_BF16_PEAK_TFLOPS) if achieved else None,
                          "traffic": traffic, "traffic_source": traffic_src,
