@@ -1650,8 +1650,10 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256r_kernel(GemmP p) {
         for (int i = 0; i < 4; ++i)
           af[i] = g4r_frag(slot + mq * G4R_REG, wr * 64 + i * 16 + (lane & 15), s * 4 + (lane >> 4));
       }
-      // 8192 / 16384 (experiments): phase 2's B0 / phase 0's A1 issued inside the MFMA section
-      const bool mmB0 = xf & 8192, mmA1 = xf & 16384;
+      // phase 0's A1 region is issued inside the MFMA section, after the first two fragment
+      // rows (same box, 4 x 2 interleaved: step 18.24-18.26 -> 18.16-18.20 ms); experiments:
+      // 16384 issues it in the memory section, 8192 moves phase 2's B0 into the MFMA section
+      const bool mmB0 = xf & 8192, mmA1 = !(xf & 16384);
       if (!(xf & 8)) {
         if (ph == 0 && more && !mmA1) issueA(1, it + 1);
         if (ph == 2 && more2) { issueA(0, it + 2); if (!mmB0) issueB(0, it + 2); }
@@ -1674,7 +1676,7 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256r_kernel(GemmP p) {
       if (!(xf & 64)) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        if (i == 2 && (xf & (8192 | 16384))) {
+        if (i == 2 && (ph == 0 || ph == 2)) {
           __builtin_amdgcn_sched_barrier(0);
           if (ph == 2 && more2 && mmB0) issueB(0, it + 2);
           if (ph == 0 && more && mmA1) issueA(1, it + 1);
