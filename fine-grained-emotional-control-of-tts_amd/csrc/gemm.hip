@@ -1653,11 +1653,12 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256r_kernel(GemmP p) {
       // phase 0's A1 region is issued inside the MFMA section, after the first two fragment
       // rows (same box, 4 x 2 interleaved: step 18.24-18.26 -> 18.16-18.20 ms); experiments:
       // 16384 issues it in the memory section, 8192 moves phase 2's B0 into the MFMA section
-      const bool mmB0 = xf & 8192, mmA1 = !(xf & 16384);
+      // (experiments: 32768 phase 3's B1 and 65536 phase 2's A0 inside the MFMA section)
+      const bool mmB0 = xf & 8192, mmA1 = !(xf & 16384), mmB1 = xf & 32768, mmA0 = xf & 65536;
       if (!(xf & 8)) {
         if (ph == 0 && more && !mmA1) issueA(1, it + 1);
-        if (ph == 2 && more2) { issueA(0, it + 2); if (!mmB0) issueB(0, it + 2); }
-        if (ph == 3 && more2) issueB(1, it + 2);
+        if (ph == 2 && more2) { if (!mmA0) issueA(0, it + 2); if (!mmB0) issueB(0, it + 2); }
+        if (ph == 3 && more2 && !mmB1) issueB(1, it + 2);
       }
       if (!(xf & 512)) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       else if (xf & 16) asm volatile("" ::: "memory");
@@ -1666,7 +1667,9 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256r_kernel(GemmP p) {
           if (more) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
           else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         } else if (ph == 3 && more) {
-          if (more2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+          // (B1 of tile it+2 not yet issued when it goes in the MFMA section: 6 newer pieces)
+          if (more2 && !mmB1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+          else if (more2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
           else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
         }
       }
@@ -1676,9 +1679,11 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256r_kernel(GemmP p) {
       if (!(xf & 64)) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        if (i == 2 && (ph == 0 || ph == 2)) {
+        if (i == 2 && (ph == 0 || (xf & (8192 | 32768 | 65536)))) {
           __builtin_amdgcn_sched_barrier(0);
+          if (ph == 2 && more2 && mmA0) issueA(0, it + 2);
           if (ph == 2 && more2 && mmB0) issueB(0, it + 2);
+          if (ph == 3 && more2 && mmB1) issueB(1, it + 2);
           if (ph == 0 && more && mmA1) issueA(1, it + 1);
           __builtin_amdgcn_sched_barrier(0);
         }
