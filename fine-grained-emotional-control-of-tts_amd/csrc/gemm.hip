@@ -2372,9 +2372,15 @@ __global__ void __launch_bounds__(BNT, 1) gemm_ps_kernel(GemmP p) {
             }
         }
       }
-      if (ph == 0 && more1) { a_advance(); issue_a(0, nxt); }
+      // phase 0's A0 region of the next K-tile is issued inside the MFMA section, after the
+      // first two fragment rows (its counted wait is a phase later, so the counts hold): same
+      // box, 3 x 2 interleaved, step 18.17-18.18 -> 17.88-17.92 ms, decoder conv1 data gradient
+      // 403-412 -> 394-395 us.  Experiments: 64 issues it in the memory section again; 128 moves
+      // phase 2's B0 the same way (slower: 18.60-18.64 ms)
+      const bool mm0 = !(XFLAGS(p) & 64), mm2 = XFLAGS(p) & 128;
+      if (ph == 0 && more1 && !mm0) { a_advance(); issue_a(0, nxt); }
       if (ph == 1 && more1) issue_a(1, nxt);
-      if (ph == 2 && more2) { b_advance(); issue_b(0, cur); }
+      if (ph == 2 && more2 && !mm2) { b_advance(); issue_b(0, cur); }
       if (ph == 3 && more2) issue_b(1, cur);
       auto dwait = [&]() {
         if constexpr (ph == 1) {
@@ -2405,11 +2411,18 @@ __global__ void __launch_bounds__(BNT, 1) gemm_ps_kernel(GemmP p) {
       // ---- matrix section ----
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < 4; ++i) {
+        if (i == 2 && (ph == 0 || (ph == 2 && mm2))) {
+          __builtin_amdgcn_sched_barrier(0);
+          if (ph == 0 && more1 && mm0) { a_advance(); issue_a(0, nxt); }
+          if (ph == 2 && more2 && mm2) { b_advance(); issue_b(0, cur); }
+          __builtin_amdgcn_sched_barrier(0);
+        }
 #pragma unroll
         for (int j = 0; j < NJ; ++j)
           acc[mq * 4 + i][j] =
               __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[kh][j], af[i], acc[mq * 4 + i][j], 0, 0, 0);
+      }
       __builtin_amdgcn_s_setprio(0);
       if constexpr ((ph & 1) != 0) { if (wr == 0) dwait(); }
       if (ph == 3 && last && !(XFLAGS(p) & 32)) {   // flag 32: timing only, no epilogue
