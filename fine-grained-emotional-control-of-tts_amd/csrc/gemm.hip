@@ -2377,17 +2377,25 @@ __global__ void __launch_bounds__(BNT, 1) gemm_ps_kernel(GemmP p) {
       // box, 3 x 2 interleaved, step 18.17-18.18 -> 17.88-17.92 ms, decoder conv1 data gradient
       // 403-412 -> 394-395 us.  Experiments: 64 issues it in the memory section again; 128 moves
       // phase 2's B0 the same way (slower: 18.60-18.64 ms)
+      // experiments 256 / 512: phase 1's A1 / phase 3's B1 inside the MFMA section too (wave
+      // group 1 then waits, in its memory section, before that issue: counts 2 / NB1 lower)
       const bool mm0 = !(XFLAGS(p) & 64), mm2 = XFLAGS(p) & 128;
+      const bool mm1 = XFLAGS(p) & 256, mm3 = XFLAGS(p) & 512;
       if (ph == 0 && more1 && !mm0) { a_advance(); issue_a(0, nxt); }
-      if (ph == 1 && more1) issue_a(1, nxt);
+      if (ph == 1 && more1 && !mm1) issue_a(1, nxt);
       if (ph == 2 && more2 && !mm2) { b_advance(); issue_b(0, cur); }
-      if (ph == 3 && more2) issue_b(1, cur);
-      auto dwait = [&]() {
+      if (ph == 3 && more2 && !mm3) issue_b(1, cur);
+      auto dwait = [&](bool early) {   // early: wave group 1, before this phase's MFMA section
         if constexpr (ph == 1) {
           // younger than A1 of this iteration: B of the next one, the previous tile's
           // epilogue stores and this tile's operands (first K-tile), A0 / A1 of the next one
           // (EO: + the operand loads of a tile's last K-tile; nk >= 2, so never also first)
-          if (more1) {
+          if (more1 && early && mm1) {
+            if (EO && last) vm_wait<4 + NB1 + EL>();
+            else if (!first) vm_wait<4 + NB1>();
+            else if (p.c_fp32) vm_wait<4 + NB1 + S32 + EPI_OPS>();
+            else vm_wait<4 + NB1 + S16 + EPI_OPS>();
+          } else if (more1) {
             if (EO && last) vm_wait<6 + NB1 + EL>();
             else if (!first) vm_wait<6 + NB1>();
             else if (p.c_fp32) vm_wait<6 + NB1 + S32 + EPI_OPS>();
@@ -2399,12 +2407,13 @@ __global__ void __launch_bounds__(BNT, 1) gemm_ps_kernel(GemmP p) {
             else vm_wait<S16 + EPI_OPS>();
           }
         } else {
-          if (more2) vm_wait<4 + NB1>();
+          if (more2 && early && mm3) vm_wait<4>();
+          else if (more2) vm_wait<4 + NB1>();
           else if (more1) vm_wait<2>();
           else vm_wait<0>();
         }
       };
-      if constexpr ((ph & 1) != 0) { if (wr == 1) dwait(); }
+      if constexpr ((ph & 1) != 0) { if (wr == 1) dwait(true); }
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -2412,10 +2421,12 @@ __global__ void __launch_bounds__(BNT, 1) gemm_ps_kernel(GemmP p) {
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        if (i == 2 && (ph == 0 || (ph == 2 && mm2))) {
+        if (i == 2 && (ph == 0 || (ph == 2 && mm2) || (ph == 1 && mm1) || (ph == 3 && mm3))) {
           __builtin_amdgcn_sched_barrier(0);
           if (ph == 0 && more1 && mm0) { a_advance(); issue_a(0, nxt); }
+          if (ph == 1 && more1 && mm1) issue_a(1, nxt);
           if (ph == 2 && more2 && mm2) { b_advance(); issue_b(0, cur); }
+          if (ph == 3 && more2 && mm3) issue_b(1, cur);
           __builtin_amdgcn_sched_barrier(0);
         }
 #pragma unroll
@@ -2424,7 +2435,7 @@ __global__ void __launch_bounds__(BNT, 1) gemm_ps_kernel(GemmP p) {
               __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[kh][j], af[i], acc[mq * 4 + i][j], 0, 0, 0);
       }
       __builtin_amdgcn_s_setprio(0);
-      if constexpr ((ph & 1) != 0) { if (wr == 0) dwait(); }
+      if constexpr ((ph & 1) != 0) { if (wr == 0) dwait(false); }
       if (ph == 3 && last && !(XFLAGS(p) & 32)) {   // flag 32: timing only, no epilogue
         // ---- tile epilogue, straight from the accumulators; operands from the wave's LDS
         // area (landed: retired by the counted waits since the tile's first K-tile) ----
