@@ -1050,7 +1050,9 @@ __global__ void __launch_bounds__(BNT) gemm_big_kernel(GemmP p) {
     // ... and for every wave; every wave is also done reading stage (it+2)%3 == (it-1)%3
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if (it + 2 < nk) issue(kt0 + it + 2, (it + 2) % 3);
+    // experiments 4096: the prefetch issued between the two k-steps' MFMAs instead of here
+    const bool mmi = XFLAGS(p) & 4096;
+    if (it + 2 < nk && !mmi) issue(kt0 + it + 2, (it + 2) % 3);
     const char* la = smem + (it % 3) * BIG_STAGE;
     const char* lb = la + BIG_A;
     // all fragments of both k-steps first (distinct registers), then 32 MFMAs
@@ -1073,6 +1075,22 @@ __global__ void __launch_bounds__(BNT) gemm_big_kernel(GemmP p) {
           if constexpr (!AK) mn_ready(af[s][i]);
           if constexpr (!BKM) mn_ready(bfr[s][i]);
         }
+    }
+    if (mmi) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[0][j], af[0][i], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (it + 2 < nk) issue(kt0 + it + 2, (it + 2) % 3);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[1][j], af[1][i], acc[i][j], 0, 0, 0);
+      continue;
     }
 #pragma unroll
     for (int s = 0; s < 2; ++s)
@@ -2846,6 +2864,7 @@ int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
                           (wgrad && tiles_big * split_big >= 160));
     if (use_big) {
       GemmP q = p;
+      q.g4_flags = getenv_int("FS2_BIG_FLAGS", 0);
       q.tiles_m = (p.M + BBM - 1) / BBM;
       if (wgrad) {
         q.split_k = split_big;
