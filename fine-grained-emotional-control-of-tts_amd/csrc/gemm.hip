@@ -1991,7 +1991,9 @@ __global__ void __launch_bounds__(BNT) gemm_pk_kernel(GemmP p) {
       }
     }
     const bool pre = it + 2 < total;
-    if (pre) {
+    // experiments 64: the prefetch issued between the two k-steps' MFMAs
+    const bool mmi = XFLAGS(p) & 64;
+    if (pre && !mmi) {
       issue(t2, kt2, (it + 2) % 3);
       if (++kt2 == nk) { kt2 = 0; ++t2; }
     }
@@ -2005,6 +2007,24 @@ __global__ void __launch_bounds__(BNT) gemm_pk_kernel(GemmP p) {
 #pragma unroll
       for (int j = 0; j < NJ; ++j) bfr[s][j] = frag_bf16_kmajor(lb, wn * 16 * NJ + j * 16, s, lane);
     }
+    if (mmi) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[0][j], af[0][i], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (pre) {
+        issue(t2, kt2, (it + 2) % 3);
+        if (++kt2 == nk) { kt2 = 0; ++t2; }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[1][j], af[1][i], acc[i][j], 0, 0, 0);
+    } else {
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
@@ -2014,6 +2034,7 @@ __global__ void __launch_bounds__(BNT) gemm_pk_kernel(GemmP p) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[s][j], af[s][i], acc[i][j], 0, 0, 0);
     __builtin_amdgcn_sched_group_barrier(0x100, 2 * (MI + NJ), 0);
     __builtin_amdgcn_sched_group_barrier(0x008, 2 * MI * NJ, 0);
+    }
     if constexpr (EPI) {
       if (nk == 1) {   // operands issued this iteration: retire them, keep the prefetch in flight
         if (pre) vm_wait<NPC>(); else vm_wait<0>();
