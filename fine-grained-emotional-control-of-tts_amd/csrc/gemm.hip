@@ -2377,14 +2377,19 @@ __global__ void __launch_bounds__(BNT, 1) gemm_ps_kernel(GemmP p) {
       constexpr int ph = decltype(PH)::value;
       constexpr int mq = ph >> 1, kh = ph & 1;
       // ---- memory section ----
-      if (ph == 0) {
+      // experiments 1024: the second k-half's B fragments read in phase 1 instead of phase 0
+      // (phase 1 then drains its reads before the barrier: B is restaged from phase 2)
+      const bool splitb = XFLAGS(p) & 1024;
+      if (ph == 0 || (ph == 1 && splitb)) {
 #pragma unroll
-        for (int h = 0; h < 2; ++h)
+        for (int h = 0; h < 2; ++h) {
+          if (splitb && h != ph) continue;
 #pragma unroll
           for (int j = 0; j < NJ; ++j) {
             const int r = wc * WN + j * 16 + li;
             bfr[h][j] = *(const bf16x8*)(cur + AIMG + r * 128 + (((h * 4 + lg) ^ ps_sw(r)) << 4));
           }
+        }
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -2453,6 +2458,7 @@ __global__ void __launch_bounds__(BNT, 1) gemm_ps_kernel(GemmP p) {
         }
       };
       if constexpr ((ph & 1) != 0) { if (wr == 1) dwait(true); }
+      if (ph == 1 && splitb) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
