@@ -1,0 +1,12 @@
+#!/bin/bash
+# same-box product-library A/B: A = fastspeech2/libfs2_hip_base.so (a copy of an earlier product
+# build), B = libfs2_hip.so; interleaved bench runs
+set -o pipefail
+cd ${GRAFT_REPO_ROOT:-$(pwd)}
+L=$(pwd)/fine-grained-emotional-control-of-tts_amd/fastspeech2
+BA="--no-cpu-baseline --no-extractor --no-fp32-leg --no-config2-leg"
+for i in $(seq ${1:-3}); do
+  FS2_HIP_LIB=$L/libfs2_hip_base.so timeout -k 10 200 python -u bench.py $BA 2>/dev/null > /tmp/abl_A.json || exit 1
+  timeout -k 10 200 python -u bench.py $BA 2>/dev/null > /tmp/abl_B.json || exit 1
+  python -c "import json; a=json.load(open('/tmp/abl_A.json')); b=json.load(open('/tmp/abl_B.json')); print('A', round(a['ms_per_step'], 3), 'B', round(b['ms_per_step'], 3))"
+done
