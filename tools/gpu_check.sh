@@ -26,6 +26,7 @@ python $R/tools/rocprof_summary.py kernel $O/prof "gemm256r_kernel<1, true, 64>"
 # kernel: 84 tiles x 2 splits on the 208-CU side-stream budget -> 168 blocks of 512; the encoder's, same grid, runs < 200 us)
 python $R/tools/rocprof_summary.py kernel $O/prof "gemm_ps_kernel<0, 64, 0, 1>" 86016 200 | tee $O/wgrad_kernel_trace.txt
 python $R/tools/rocprof_summary.py gaps $O/prof embed_fwd_kernel 10 $O/gaps.json | tail -3
+python $R/tools/rocprof_summary.py timeline $O/prof 2 $O/stream_timeline.txt | tail -1
 if [ "$3" == "pmc" ]; then
   for C in FETCH_SIZE WRITE_SIZE; do
     timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d $O/pmc_$C -o run -- python $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extractor --no-fp32-leg --no-config2-leg \

@@ -114,6 +114,56 @@ def gaps(d, marker="adamw_vec_kernel", last=10, out=None):
     print(json.dumps({k: v for k, v in res.items() if k != "per_step"}))
 
 
+def _short(n):
+    n = n.replace("(anonymous namespace)::", "").replace("void ", "")
+    return n.split("((")[0].split("(float")[0].split("(bool")[0].split("(long")[0][:52]
+
+
+def timeline(d, marker="embed_fwd_kernel", anchor="attn_bwd_dq_kernel<192, 1, 8>", layer=0,
+             out=None):
+    """Per-stream timeline of one decoder layer's backward in the last profiled step: every
+    dispatch on every queue between the end of the (layer+1)-th-from-last ``anchor`` dispatch
+    before it (or 1.6 ms earlier) and the first main-queue dispatch 300 us after this layer's
+    anchor; plus the step's kernel time per queue.  Steps are delimited by ``marker``."""
+    ev = []
+    for f in _find(d, "kernel_trace.csv"):
+        for r in csv.DictReader(open(f)):
+            ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"],
+                       int(r["Queue_Id"]), int(r["Grid_Size_X"]), int(r["Grid_Size_Z"])))
+    ev.sort()
+    starts = [s for s, e, n, *_ in ev if marker in n]
+    if len(starts) < 2:
+        raise SystemExit(f"fewer than 2 {marker} dispatches")
+    a, b = starts[-2], starts[-1]
+    step = [x for x in ev if a <= x[0] < b]
+    anchors = [x for x in step if anchor in x[2]]
+    if not anchors:
+        raise SystemExit(f"no {anchor} in the last step")
+    # the backward walks the decoder from the last layer: anchors[0] is layer L-1
+    k = anchors[layer]
+    lo = anchors[layer - 1][1] if layer > 0 else k[0] - 1600_000
+    hi = k[1] + 300_000
+    lines = [f"# one decoder layer's backward (anchor {anchor} #{layer} of the last step), "
+             f"us from the step start; q = HIP queue (one per stream)",
+             f"# {'q':>2} {'start':>9} {'end':>9} {'us':>7}  kernel"]
+    for s, e, n, q, gx, gz in step:
+        if e <= lo or s >= hi:
+            continue
+        lines.append(f"  {q:2d} {(s - a) / 1e3:9.1f} {(e - a) / 1e3:9.1f} {(e - s) / 1e3:7.1f}  "
+                     f"{_short(n):52s} grid {gx} z {gz}")
+    per_q = {}
+    for s, e, n, q, *_ in step:
+        per_q[q] = per_q.get(q, 0) + (e - s)
+    lines.append("")
+    lines.append("# kernel time per queue in the step (us): " +
+                 json.dumps({str(q): round(v / 1e3, 1) for q, v in sorted(per_q.items())}) +
+                 f"  step wall {(b - a) / 1e3:.1f} us, {len(step)} launches")
+    txt = "\n".join(lines)
+    if out:
+        open(out, "w").write(txt + "\n")
+    print(txt)
+
+
 def pmc(out, subs, *dirs):
     """Per (kernel, grid) averages of every counter collected in the --pmc pass directories
     ``dirs`` (one counter set per pass), for kernels whose name contains one of the
@@ -201,6 +251,9 @@ if __name__ == "__main__":
         gaps(sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else "adamw_vec_kernel",
              int(sys.argv[4]) if len(sys.argv) > 4 else 10,
              sys.argv[5] if len(sys.argv) > 5 else None)
+    elif sys.argv[1] == "timeline":
+        timeline(sys.argv[2], layer=int(sys.argv[3]) if len(sys.argv) > 3 else 0,
+                 out=sys.argv[4] if len(sys.argv) > 4 else None)
     elif sys.argv[1] == "traffic":
         traffic(sys.argv[2], sys.argv[3], sys.argv[4], int(sys.argv[5]), float(sys.argv[6]),
                 sys.argv[7] if len(sys.argv) > 7 else None)
