@@ -334,10 +334,7 @@ __global__ void __launch_bounds__(W8 * 64 / QG, 1) attn_fwd_kernel(AttnP p) {
 #endif
     const char* Ks = smem + (tb & 1) * 2 * TB;
     const char* Vs = Ks + TB;
-    // experiments 8: the next tile's DMA issued after the barrier (the buffer's last readers,
-    // iteration t-1, are all past it), so no wave issues it on the way to the barrier
-    const bool late = p.xflags & 8;
-    if (t + 1 < ntile && tb == t && !late) {
+    if (t + 1 < ntile && tb == t) {
       char* nx = smem + ((t + 1) & 1) * 2 * TB;
       dma.issue(nx, rsK, p.ldq, k0 + 64, p.T, wave);
       dma.issue(nx + TB, rsV, p.ldq, k0 + 64, p.T, wave);
@@ -347,11 +344,6 @@ __global__ void __launch_bounds__(W8 * 64 / QG, 1) attn_fwd_kernel(AttnP p) {
     }
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if (t + 1 < ntile && tb == t && late) {
-      char* nx = smem + ((t + 1) & 1) * 2 * TB;
-      dma.issue(nx, rsK, p.ldq, k0 + 64, p.T, wave);
-      dma.issue(nx + TB, rsV, p.ldq, k0 + 64, p.T, wave);
-    }
     f32x4 sacc[4][QG];
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt)
@@ -580,8 +572,7 @@ __global__ void __launch_bounds__(W8 * 64 / QG, 1) attn_bwd_dq_kernel(AttnP p) {
     const int k0 = t * 64;
     const char* Ks = smem + (t & 1) * 2 * TB;
     const char* Vs = Ks + TB;
-    const bool late = p.xflags & 8;   // experiments: as the forward
-    if (t + 1 < ntile && !late) {
+    if (t + 1 < ntile) {
       char* nx = smem + ((t + 1) & 1) * 2 * TB;
       dma.issue(nx, rsK, p.ldq, k0 + 64, p.T, wave);
       dma.issue(nx + TB, rsV, p.ldq, k0 + 64, p.T, wave);
@@ -591,11 +582,6 @@ __global__ void __launch_bounds__(W8 * 64 / QG, 1) attn_bwd_dq_kernel(AttnP p) {
     }
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if (t + 1 < ntile && late) {
-      char* nx = smem + ((t + 1) & 1) * 2 * TB;
-      dma.issue(nx, rsK, p.ldq, k0 + 64, p.T, wave);
-      dma.issue(nx + TB, rsV, p.ldq, k0 + 64, p.T, wave);
-    }
     f32x4 sacc[4][QG], pacc[4][QG];
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt)
@@ -757,8 +743,7 @@ __global__ void __launch_bounds__(W8 * 64, 1) attn_bwd_dkv_kernel(AttnP p) {
     const float* ls_s = lsd + (t & 1) * 192;
     const float* ds_s = ls_s + 64;
     const uint32_t* rh_s = (const uint32_t*)(ls_s + 128);
-    const bool late = p.xflags & 8;   // experiments: as the forward
-    if (t + 1 < ntile && !late) {
+    if (t + 1 < ntile) {
       issue_stats(q0 + 64, (t + 1) & 1);
       char* nx = smem + ((t + 1) & 1) * 2 * TB;
       dma.issue(nx, rsQ, p.ldq, q0 + 64, p.T, wave);
@@ -771,12 +756,6 @@ __global__ void __launch_bounds__(W8 * 64, 1) attn_bwd_dkv_kernel(AttnP p) {
     }
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if (t + 1 < ntile && late) {
-      issue_stats(q0 + 64, (t + 1) & 1);
-      char* nx = smem + ((t + 1) & 1) * 2 * TB;
-      dma.issue(nx, rsQ, p.ldq, q0 + 64, p.T, wave);
-      dma.issue(nx + TB, rsO, p.lddo, q0 + 64, p.T, wave);
-    }
     // S = Q K^T, dP = dO V^T for 64 queries x this wave's 16 keys (C: col key, rows queries)
     f32x4 sacc[4], pacc[4];
 #pragma unroll

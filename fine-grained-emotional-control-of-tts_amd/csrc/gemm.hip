@@ -73,6 +73,7 @@ struct GemmP {
   int vec_ok;
   int vec_align;  // vector epilogue possible if K were not split
   int c_row_t, c_row_pad;  // >0: output row m stored at m + (m / c_row_t) * c_row_pad (ps kernel)
+  int max_ctas;            // grid budget of the persistent kernels (blocks), 8..256
 };
 
 __device__ __forceinline__ u32x4 add_bf16x8(u32x4 a, u32x4 b) {
@@ -1050,9 +1051,7 @@ __global__ void __launch_bounds__(BNT) gemm_big_kernel(GemmP p) {
     // ... and for every wave; every wave is also done reading stage (it+2)%3 == (it-1)%3
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    // experiments 4096: the prefetch issued between the two k-steps' MFMAs instead of here
-    const bool mmi = XFLAGS(p) & 4096;
-    if (it + 2 < nk && !mmi) issue(kt0 + it + 2, (it + 2) % 3);
+    if (it + 2 < nk) issue(kt0 + it + 2, (it + 2) % 3);
     const char* la = smem + (it % 3) * BIG_STAGE;
     const char* lb = la + BIG_A;
     // all fragments of both k-steps first (distinct registers), then 32 MFMAs
@@ -1075,22 +1074,6 @@ __global__ void __launch_bounds__(BNT) gemm_big_kernel(GemmP p) {
           if constexpr (!AK) mn_ready(af[s][i]);
           if constexpr (!BKM) mn_ready(bfr[s][i]);
         }
-    }
-    if (mmi) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[0][j], af[0][i], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      if (it + 2 < nk) issue(kt0 + it + 2, (it + 2) % 3);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[1][j], af[1][i], acc[i][j], 0, 0, 0);
-      continue;
     }
 #pragma unroll
     for (int s = 0; s < 2; ++s)
@@ -1386,7 +1369,6 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256_kernel(GemmP p) {
   const bool prio = !(XFLAGS(p) & 2);
   const bool nowait = XFLAGS(p) & 4;   // timing experiments only (wrong results)
   const bool noissue = XFLAGS(p) & 8;
-  const bool dma_mm = XFLAGS(p) & 256;  // LDS-DMA issued inside the matrix section
   // stagger: waves 4-7 half a phase behind; without it both groups retire DMA like group 1
   const int grp = stag ? wr : 1;
   if (stag && wr == 1) __builtin_amdgcn_s_barrier();
@@ -1412,13 +1394,11 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256_kernel(GemmP p) {
         af[i] = AK ? g4_frag_k(rA, wr * 128 + mq * 64 + i * 16 + (lane & 15), lane >> 4)
                    : frag_bf16_mnmajor_asm<512>(rA, wr * 128 + mq * 64 + i * 16, 0, lane);
       const bool iss = !noissue && (ph < 2 ? more : it + 2 < nk);
-      if (iss && !dma_mm) issue(ph < 2 ? it + 1 : it + 2, 3 - ph);
-      // phase 1 retires this tile's k1 regions, phase 3 the next tile's k0 regions (with the
-      // issue in the matrix section, this phase's 2 pieces are not yet counted here)
+      if (iss) issue(ph < 2 ? it + 1 : it + 2, 3 - ph);
+      // phase 1 retires this tile's k1 regions, phase 3 the next tile's k0 regions
       if (grp == 1 && (ph & 1) && !nowait && !noissue) {
         if (iss) {
-          if (dma_mm) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-          else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+          asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         } else if (ph == 3 && more) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
@@ -1437,11 +1417,6 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256_kernel(GemmP p) {
       if (prio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        if (i == 2 && dma_mm) {   // this phase's region issued between the MFMAs
-          __builtin_amdgcn_sched_barrier(0);
-          if (iss) issue(ph < 2 ? it + 1 : it + 2, 3 - ph);
-          __builtin_amdgcn_sched_barrier(0);
-        }
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           acc[mq * 4 + i][j] =
@@ -1669,14 +1644,11 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256r_kernel(GemmP p) {
           af[i] = g4r_frag(slot + mq * G4R_REG, wr * 64 + i * 16 + (lane & 15), s * 4 + (lane >> 4));
       }
       // phase 0's A1 region is issued inside the MFMA section, after the first two fragment
-      // rows (same box, 4 x 2 interleaved: step 18.24-18.26 -> 18.16-18.20 ms); experiments:
-      // 16384 issues it in the memory section, 8192 moves phase 2's B0 into the MFMA section
-      // (experiments: 32768 phase 3's B1 and 65536 phase 2's A0 inside the MFMA section)
-      const bool mmB0 = xf & 8192, mmA1 = !(xf & 16384), mmB1 = xf & 32768, mmA0 = xf & 65536;
+      // rows (same box, 4 x 2 interleaved: step 18.24-18.26 -> 18.16-18.20 ms); phase 2's A0 /
+      // B0 or phase 3's B1 moved there measured neutral or slower
       if (!(xf & 8)) {
-        if (ph == 0 && more && !mmA1) issueA(1, it + 1);
-        if (ph == 2 && more2) { if (!mmA0) issueA(0, it + 2); if (!mmB0) issueB(0, it + 2); }
-        if (ph == 3 && more2 && !mmB1) issueB(1, it + 2);
+        if (ph == 2 && more2) { issueA(0, it + 2); issueB(0, it + 2); }
+        if (ph == 3 && more2) issueB(1, it + 2);
       }
       if (!(xf & 512)) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       else if (xf & 16) asm volatile("" ::: "memory");
@@ -1685,9 +1657,7 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256r_kernel(GemmP p) {
           if (more) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
           else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         } else if (ph == 3 && more) {
-          // (B1 of tile it+2 not yet issued when it goes in the MFMA section: 6 newer pieces)
-          if (more2 && !mmB1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-          else if (more2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+          if (more2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
           else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
         }
       }
@@ -1697,12 +1667,9 @@ __global__ void __launch_bounds__(G4_NT, 1) gemm256r_kernel(GemmP p) {
       if (!(xf & 64)) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        if (i == 2 && (ph == 0 || (xf & (8192 | 32768 | 65536)))) {
+        if (i == 2 && ph == 0) {
           __builtin_amdgcn_sched_barrier(0);
-          if (ph == 2 && more2 && mmA0) issueA(0, it + 2);
-          if (ph == 2 && more2 && mmB0) issueB(0, it + 2);
-          if (ph == 3 && more2 && mmB1) issueB(1, it + 2);
-          if (ph == 0 && more && mmA1) issueA(1, it + 1);
+          if (more && !(xf & 8)) issueA(1, it + 1);
           __builtin_amdgcn_sched_barrier(0);
         }
 #pragma unroll
@@ -1991,9 +1958,7 @@ __global__ void __launch_bounds__(BNT) gemm_pk_kernel(GemmP p) {
       }
     }
     const bool pre = it + 2 < total;
-    // experiments 64: the prefetch issued between the two k-steps' MFMAs
-    const bool mmi = XFLAGS(p) & 64;
-    if (pre && !mmi) {
+    if (pre) {
       issue(t2, kt2, (it + 2) % 3);
       if (++kt2 == nk) { kt2 = 0; ++t2; }
     }
@@ -2007,24 +1972,6 @@ __global__ void __launch_bounds__(BNT) gemm_pk_kernel(GemmP p) {
 #pragma unroll
       for (int j = 0; j < NJ; ++j) bfr[s][j] = frag_bf16_kmajor(lb, wn * 16 * NJ + j * 16, s, lane);
     }
-    if (mmi) {
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < NJ; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[0][j], af[0][i], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      if (pre) {
-        issue(t2, kt2, (it + 2) % 3);
-        if (++kt2 == nk) { kt2 = 0; ++t2; }
-      }
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < NJ; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[1][j], af[1][i], acc[i][j], 0, 0, 0);
-    } else {
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
@@ -2034,7 +1981,6 @@ __global__ void __launch_bounds__(BNT) gemm_pk_kernel(GemmP p) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[s][j], af[s][i], acc[i][j], 0, 0, 0);
     __builtin_amdgcn_sched_group_barrier(0x100, 2 * (MI + NJ), 0);
     __builtin_amdgcn_sched_group_barrier(0x008, 2 * MI * NJ, 0);
-    }
     if constexpr (EPI) {
       if (nk == 1) {   // operands issued this iteration: retire them, keep the prefetch in flight
         if (pre) vm_wait<NPC>(); else vm_wait<0>();
@@ -2377,13 +2323,9 @@ __global__ void __launch_bounds__(BNT, 1) gemm_ps_kernel(GemmP p) {
       constexpr int ph = decltype(PH)::value;
       constexpr int mq = ph >> 1, kh = ph & 1;
       // ---- memory section ----
-      // experiments 1024: the second k-half's B fragments read in phase 1 instead of phase 0
-      // (phase 1 then drains its reads before the barrier: B is restaged from phase 2)
-      const bool splitb = XFLAGS(p) & 1024;
-      if (ph == 0 || (ph == 1 && splitb)) {
+      if (ph == 0) {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-          if (splitb && h != ph) continue;
 #pragma unroll
           for (int j = 0; j < NJ; ++j) {
             const int r = wc * WN + j * 16 + li;
@@ -2419,27 +2361,17 @@ __global__ void __launch_bounds__(BNT, 1) gemm_ps_kernel(GemmP p) {
       // phase 0's A0 region of the next K-tile is issued inside the MFMA section, after the
       // first two fragment rows (its counted wait is a phase later, so the counts hold): same
       // box, 3 x 2 interleaved, step 18.17-18.18 -> 17.88-17.92 ms, decoder conv1 data gradient
-      // 403-412 -> 394-395 us.  Experiments: 64 issues it in the memory section again; 128 moves
-      // phase 2's B0 the same way (slower: 18.60-18.64 ms)
-      // experiments 256 / 512: phase 1's A1 / phase 3's B1 inside the MFMA section too (wave
-      // group 1 then waits, in its memory section, before that issue: counts 2 / NB1 lower)
-      const bool mm0 = !(XFLAGS(p) & 64), mm2 = XFLAGS(p) & 128;
-      const bool mm1 = XFLAGS(p) & 256, mm3 = XFLAGS(p) & 512;
-      if (ph == 0 && more1 && !mm0) { a_advance(); issue_a(0, nxt); }
-      if (ph == 1 && more1 && !mm1) issue_a(1, nxt);
-      if (ph == 2 && more2 && !mm2) { b_advance(); issue_b(0, cur); }
-      if (ph == 3 && more2 && !mm3) issue_b(1, cur);
-      auto dwait = [&](bool early) {   // early: wave group 1, before this phase's MFMA section
+      // 403-412 -> 394-395 us.  Moving phase 2's B0, phase 1's A1 or phase 3's B1 the same way
+      // measured slower
+      if (ph == 1 && more1) issue_a(1, nxt);
+      if (ph == 2 && more2) { b_advance(); issue_b(0, cur); }
+      if (ph == 3 && more2) issue_b(1, cur);
+      auto dwait = [&]() {   // wave group 1 before this phase's MFMA section, group 0 after it
         if constexpr (ph == 1) {
           // younger than A1 of this iteration: B of the next one, the previous tile's
           // epilogue stores and this tile's operands (first K-tile), A0 / A1 of the next one
           // (EO: + the operand loads of a tile's last K-tile; nk >= 2, so never also first)
-          if (more1 && early && mm1) {
-            if (EO && last) vm_wait<4 + NB1 + EL>();
-            else if (!first) vm_wait<4 + NB1>();
-            else if (p.c_fp32) vm_wait<4 + NB1 + S32 + EPI_OPS>();
-            else vm_wait<4 + NB1 + S16 + EPI_OPS>();
-          } else if (more1) {
+          if (more1) {
             if (EO && last) vm_wait<6 + NB1 + EL>();
             else if (!first) vm_wait<6 + NB1>();
             else if (p.c_fp32) vm_wait<6 + NB1 + S32 + EPI_OPS>();
@@ -2451,14 +2383,12 @@ __global__ void __launch_bounds__(BNT, 1) gemm_ps_kernel(GemmP p) {
             else vm_wait<S16 + EPI_OPS>();
           }
         } else {
-          if (more2 && early && mm3) vm_wait<4>();
-          else if (more2) vm_wait<4 + NB1>();
+          if (more2) vm_wait<4 + NB1>();
           else if (more1) vm_wait<2>();
           else vm_wait<0>();
         }
       };
-      if constexpr ((ph & 1) != 0) { if (wr == 1) dwait(true); }
-      if (ph == 1 && splitb) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if constexpr ((ph & 1) != 0) { if (wr == 1) dwait(); }
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -2466,12 +2396,9 @@ __global__ void __launch_bounds__(BNT, 1) gemm_ps_kernel(GemmP p) {
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        if (i == 2 && (ph == 0 || (ph == 2 && mm2) || (ph == 1 && mm1) || (ph == 3 && mm3))) {
+        if (i == 2 && ph == 0) {
           __builtin_amdgcn_sched_barrier(0);
-          if (ph == 0 && more1 && mm0) { a_advance(); issue_a(0, nxt); }
-          if (ph == 1 && more1 && mm1) issue_a(1, nxt);
-          if (ph == 2 && more2 && mm2) { b_advance(); issue_b(0, cur); }
-          if (ph == 3 && more2 && mm3) issue_b(1, cur);
+          if (more1) { a_advance(); issue_a(0, nxt); }
           __builtin_amdgcn_sched_barrier(0);
         }
 #pragma unroll
@@ -2480,7 +2407,7 @@ __global__ void __launch_bounds__(BNT, 1) gemm_ps_kernel(GemmP p) {
               __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[kh][j], af[i], acc[mq * 4 + i][j], 0, 0, 0);
       }
       __builtin_amdgcn_s_setprio(0);
-      if constexpr ((ph & 1) != 0) { if (wr == 0) dwait(false); }
+      if constexpr ((ph & 1) != 0) { if (wr == 0) dwait(); }
       if (ph == 3 && last && !(XFLAGS(p) & 32)) {   // flag 32: timing only, no epilogue
         // ---- tile epilogue, straight from the accumulators; operands from the wave's LDS
         // area (landed: retired by the counted waits since the tile's first K-tile) ----
@@ -2622,21 +2549,6 @@ void launch4(const GemmP& p, dim3 grid, hipStream_t s, int ak, int bk) {
   else hipLaunchKernelGGL((gemm_kernel<T, false, false, GA, GB>), grid, dim3(NT), 0, s, p);
 }
 
-// Persistent-kernel grid budget per stream (fs2_set_stream_ctas): a stream that shares the GPU
-// with a latency-critical one (the weight-gradient side stream beside the data-gradient chain)
-// can leave CUs free by sizing its persistent grids below the CU count.  Default 256.
-// A table of the last 64 streams given a budget (torch hands out pooled streams, so an engine
-// per model in one process registers a new one each time); the oldest entry is replaced.
-struct StreamCtas { hipStream_t s; int ctas; };
-constexpr int kStreamCtasSlots = 64;
-StreamCtas g_stream_ctas[kStreamCtasSlots];
-int g_nstream_ctas = 0, g_stream_ctas_next = 0;
-int stream_ctas(hipStream_t s) {
-  for (int i = 0; i < g_nstream_ctas; ++i)
-    if (g_stream_ctas[i].s == s) return g_stream_ctas[i].ctas;
-  return 256;
-}
-
 template <typename T>
 int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
   dim3 grid(p.tiles_m * p.tiles_n, 1, gz);
@@ -2730,22 +2642,6 @@ int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
       FS2_CHECK_LAUNCH();
       return 0;
     }
-    // long-K plain GEMMs with 192-wide tiles (the N = 384 data gradients of the FFN conv1) on the
-    // full-row-region 256x192 kernel: bit-identical but slower than the persistent kernel at the
-    // decoder conv1 data gradient (424 vs 406 us, step neutral; tools/r04_g48.sh) -- 12 MFMAs
-    // per phase against the same fragment reads.  Off; FS2_G4R48=1 (experiments build) enables.
-    static const bool g4r48 = getenv_int("FS2_G4R48", 0) != 0;
-    if (ps_go && g4r48 && ps_w192 && cm_ps == 0 && !ps_op && p.K >= 2048 && !p.c_row_t &&
-        p.nvalid % 8 == 0 && p.ldc % 8 == 0) {
-      GemmP q = p;
-      q.g4_flags = getenv_int("FS2_G4_FLAGS", 0);
-      q.tiles_m = ps_tm;
-      q.tiles_n = (p.N + 191) / 192;
-      hipLaunchKernelGGL((gemm256r_kernel<0, true, 48>), dim3(q.tiles_m * q.tiles_n), dim3(G4_NT), 0,
-                         s, q);
-      FS2_CHECK_LAUNCH();
-      return 0;
-    }
     if (ps_go) {
       GemmP q = p;
       q.g4_flags = getenv_int("FS2_PS_FLAGS", 0);
@@ -2753,7 +2649,7 @@ int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
       const bool w192 = ps_w192;
       q.tiles_n = w192 ? (p.N + 191) / 192 : (p.N + 255) / 256;
       const int nt = q.tiles_m * q.tiles_n;
-      const int cus = stream_ctas(s);
+      const int cus = p.max_ctas;
       const int g = nt < cus ? (nt + 7) / 8 * 8 : cus;
       if (w192) {
         if (ps_op) hipLaunchKernelGGL((gemm_ps_kernel<0, 48, 1>), dim3(g), dim3(BNT), 0, s, q);
@@ -2805,7 +2701,7 @@ int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
       q.tiles_m = (p.M + TM - 1) / TM;
       q.tiles_n = (p.N + TN - 1) / TN;
       const int nt = q.tiles_m * q.tiles_n;
-      const int slots = (pk_cfg == 22 ? 2 : 1) * stream_ctas(s);   // blocks resident at once (LDS)
+      const int slots = (pk_cfg == 22 ? 2 : 1) * p.max_ctas;   // blocks resident at once (LDS)
       // >= 8 blocks: every XCD chunk needs a block (blocks with no tile exit at once)
       const int g = nt < slots ? (nt + 7) / 8 * 8 : slots;
       if (pk_cfg == 44) hipLaunchKernelGGL((gemm_pk_kernel<4, 4>), dim3(g), dim3(BNT), 0, s, q);
@@ -2933,20 +2829,6 @@ bool aligned16(const void* ptr) { return ((uintptr_t)ptr & 15) == 0; }
 
 }  // namespace
 
-extern "C" int fs2_set_stream_ctas(void* stream, int ctas) {
-  if (ctas < 8 || ctas > 256) return FS2_EINVAL;
-  const hipStream_t s = (hipStream_t)stream;
-  for (int i = 0; i < g_nstream_ctas; ++i)
-    if (g_stream_ctas[i].s == s) { g_stream_ctas[i].ctas = ctas / 8 * 8; return 0; }
-  if (g_nstream_ctas < kStreamCtasSlots) {
-    g_stream_ctas[g_nstream_ctas++] = {s, ctas / 8 * 8};
-  } else {
-    g_stream_ctas[g_stream_ctas_next] = {s, ctas / 8 * 8};
-    g_stream_ctas_next = (g_stream_ctas_next + 1) % kStreamCtasSlots;
-  }
-  return 0;
-}
-
 extern "C" int fs2_gemm(const fs2_gemm_desc* d, void* stream) {
   if (!d || d->M < 0 || d->N < 0 || d->K < 0) return FS2_EINVAL;
   if (d->M == 0 || d->N == 0) return 0;
@@ -2979,6 +2861,7 @@ extern "C" int fs2_gemm(const fs2_gemm_desc* d, void* stream) {
   const int batch = d->batch > 1 ? d->batch : 1;
   p.c_row_t = d->c_row_t > 0 ? d->c_row_t : 0;
   p.c_row_pad = p.c_row_t ? d->c_row_pad : 0;
+  p.max_ctas = d->max_ctas > 0 && d->max_ctas < 256 ? max(8, d->max_ctas / 8 * 8) : 256;
   if (p.c_row_t && (d->dtype != FS2_BF16 || !d->a_kmajor || !d->b_kmajor ||
                     p.conv_mode || batch > 1 || p.split_k > 1 || p.accumulate || p.c_conv_kw))
     return FS2_EINVAL;

@@ -63,7 +63,7 @@ class GemmDesc(ctypes.Structure):
         ("sA1", ctypes.c_int64), ("sA2", ctypes.c_int64), ("sB1", ctypes.c_int64),
         ("sB2", ctypes.c_int64), ("sC1", ctypes.c_int64), ("sC2", ctypes.c_int64),
         ("sR1", ctypes.c_int64), ("sR2", ctypes.c_int64), ("conv_dil", ctypes.c_int),
-        ("c_row_t", ctypes.c_int), ("c_row_pad", ctypes.c_int),
+        ("c_row_t", ctypes.c_int), ("c_row_pad", ctypes.c_int), ("max_ctas", ctypes.c_int),
     ]
 
 
@@ -104,7 +104,6 @@ Fl = ctypes.c_float
 # name -> (restype, argtypes); must match include/fs2_hip.h exactly
 SIGNATURES = {
     "fs2_gemm": (I, [ctypes.POINTER(GemmDesc), P]),
-    "fs2_set_stream_ctas": (I, [P, I]),
     "fs2_colsum": (I, [P, I64, I, I, I, P, I, P, P]),
     "fs2_conv_fold": (I, [P, I, I64, I, I, I, I, P, I64, P, I64, P, P, I, P]),
     "fs2_colsum_workspace_floats": (I64, [I, I]),

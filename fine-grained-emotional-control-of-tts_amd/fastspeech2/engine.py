@@ -81,8 +81,8 @@ _PAD_FWD = N.exp_int("FS2_PAD_FWD", 1)
 # serial mode for per-call-site timing (bench.py --detail runs with the experiments library)
 _NO_SIDE = N.exp_flag("FS2_NO_SIDE_STREAM")
 _NO_AUX = N.exp_flag("FS2_NO_AUX_STREAM")
-# persistent-GEMM grid budget of the weight-gradient side stream (fs2_set_stream_ctas): the
-# CUs it leaves free take the main stream's LayerNorm / reduction / short GEMM launches, which
+# persistent-GEMM grid budget of the weight-gradient side stream (fs2_gemm_desc.max_ctas, passed
+# with every weight-gradient GEMM enqueued there): the CUs it leaves free take the main stream's LayerNorm / reduction / short GEMM launches, which
 # otherwise queue behind side-stream blocks that hold a whole CU's registers.  Same-box sweep
 # (tools/r04_side.sh, 2 x 7 interleaved bench runs): 256 -> 18.23-18.29 ms, 176-240 ->
 # 18.01-18.13, 160 -> 18.87; 208 kept.  FS2_SIDE_CTAS overrides in the experiments build.
@@ -149,11 +149,9 @@ class FS2Engine:
         self._ws_key = torch.cuda.current_stream(self.dev).cuda_stream
         self._ws_other = {}
         self._side = torch.cuda.Stream(self.dev) if (self.dt == N.BF16 and not _NO_SIDE) else None
-        self._side_ctas = 256
-        if self._side is not None and _SIDE_CTAS < 256:
-            N.check(N.lib().fs2_set_stream_ctas(self._side.cuda_stream, _SIDE_CTAS),
-                    "fs2_set_stream_ctas")
-            self._side_ctas = _SIDE_CTAS // 8 * 8
+        # grid budget of the persistent GEMMs this engine enqueues on its side stream (per call,
+        # in the GEMM descriptor: no library state, whichever stream handle torch recycles)
+        self._side_ctas = min(256, max(8, _SIDE_CTAS // 8 * 8)) if self._side is not None else 256
         # duration / pitch predictor chains (independent of the rest of the step when the
         # pitch target is given) run on a third stream; their weight gradients stay on it
         self._aux = torch.cuda.Stream(self.dev) if (self._side is not None and not _NO_AUX) else None
@@ -535,7 +533,9 @@ class FS2Engine:
         tag = self._dtag("wgrad", wname, T)
         if tag:
             self._tic(tag)
-        done = self._wgrad_impl(dY, lddy, X, ldx, M, T, wname, n_cols, gemm_tag, bias, dy_img)
+        ctas = self._side_ctas if h is not None else 0
+        done = self._wgrad_impl(dY, lddy, X, ldx, M, T, wname, n_cols, gemm_tag, bias, dy_img,
+                                ctas)
         if tag:
             self._toc(tag)
         if bias is not None and not done:
@@ -575,7 +575,8 @@ class FS2Engine:
             buf = ent[1]
         return buf[64:64 + n]
 
-    def _wgrad_km(self, dY, lddy, X, ldx, M, T, wname, gemm_tag=None, bias=None, dy_img=None):
+    def _wgrad_km(self, dY, lddy, X, ldx, M, T, wname, gemm_tag=None, bias=None, dy_img=None,
+                  ctas=0):
         """grad[O][KW][C] += sum_{b,t} dY[b,t,o] X[b, reflect(t+j-P), c] with both GEMM operands
         K-major: dY and X are first written channel-major over the padded token domain (T+2P
         columns per utterance; dY's pad columns zero, X's reflected), where tap j is a constant
@@ -588,7 +589,7 @@ class FS2Engine:
         ncol = KW * C
         tiles = -(-O // 256) * -(-ncol // 256)
         # one (split, tile) unit per CU; >= 16 K-tiles per unit, <= 25 fp32 slices to sum
-        cus = self._side_ctas if self._side is not None else 256
+        cus = ctas if 0 < ctas < 256 else 256
         S = max(1, min(cus // tiles, -(-Bt // 64) // 16, 25))
         Kp = round_up(Bt, 64 * S)
         dYT = self._km_image("dy", O, Kp)
@@ -609,20 +610,20 @@ class FS2Engine:
         if gemm_tag:
             self._tic(gemm_tag)
         ops.gemm(O, ncol, Kp, dYT, Kp, XT, Kp, ws, ncol, dt=self.dt, conv=(6, T, KW, C),
-                 c_fp32=1, split_k=S, split_stride=stride if S > 1 else 0)
+                 c_fp32=1, split_k=S, split_stride=stride if S > 1 else 0, max_ctas=ctas)
         if gemm_tag:
             self._toc(gemm_tag)
         ops.sum_slices(ws, S, stride, stride, self.grads[wname], accumulate=1)
         return True
 
     def _wgrad_impl(self, dY, lddy, X, ldx, M, T, wname, n_cols=None, gemm_tag=None, bias=None,
-                    dy_img=None):
+                    dy_img=None, ctas=0):
         """grad[O][KW][C] += sum_m dY[m][o] * X[reflect(t+j-P)][c]   (fp32, accumulate).
         ``gemm_tag``: HIP events around the GEMM launch alone (bench.py's roofline entry for
         the FFN conv1 weight gradient), on the stream it runs on (the side stream)."""
         O, C, KW = self._wspecs[wname]
         if self._km_ok(O, C, KW, T, n_cols) and lddy % 8 == 0 and ldx % 8 == 0:
-            return self._wgrad_km(dY, lddy, X, ldx, M, T, wname, gemm_tag, bias, dy_img)
+            return self._wgrad_km(dY, lddy, X, ldx, M, T, wname, gemm_tag, bias, dy_img, ctas)
         if dy_img is not None:
             raise RuntimeError(f"{wname}: a padded dY image needs the K-major weight gradient")
         if n_cols is not None and n_cols != KW * C and KW == 1 and n_cols % 8 == 0 and self.dt == 1:
@@ -636,7 +637,7 @@ class FS2Engine:
             ws = self.ws((ns + 1) * stride)
             ops.gemm(O, n_cols, K, dY, lddy, X, ldx, ws, n_cols, dt=self.dt, a_kmajor=0,
                      b_kmajor=0, c_fp32=1, kvalid=M, nvalid=n_cols, split_k=ns,
-                     split_stride=stride)
+                     split_stride=stride, max_ctas=ctas)
             tot = ws[ns * stride:(ns + 1) * stride]
             ops.sum_slices(ws, ns, stride, stride, tot, accumulate=0)
             self.grads[wname].view(O, C).add_(tot.view(O, n_cols)[:, :C])
@@ -662,7 +663,8 @@ class FS2Engine:
             if gemm_tag:
                 self._tic(gemm_tag)
             ops.gemm(O, Ncols, K, dY, lddy, X, ldx, ws, ldc, dt=self.dt, a_kmajor=0, b_kmajor=0,
-                     conv=conv, c_fp32=1, kvalid=M, nvalid=ldc, split_k=ns, split_stride=stride)
+                     conv=conv, c_fp32=1, kvalid=M, nvalid=ldc, split_k=ns, split_stride=stride,
+                     max_ctas=ctas)
             if gemm_tag:
                 self._toc(gemm_tag)
             ops.sum_slices(ws, ns, stride, stride, self.grads[wname], accumulate=1)
@@ -670,7 +672,7 @@ class FS2Engine:
         # conv weight gradients land contiguous in the [O][KW][C] flat layout (model._kw_major)
         ops.gemm(O, Ncols, K, dY, lddy, X, ldx, self.grads[wname], ldc, dt=self.dt, a_kmajor=0,
                  b_kmajor=0, conv=conv, c_fp32=1, kvalid=M, nvalid=KW * C, accumulate=1,
-                 split_k=split)
+                 split_k=split, max_ctas=ctas)
 
     def _bias_grad(self, dY, lddy, M, n, gname):
         h = self._side_enter(dY)

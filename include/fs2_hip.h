@@ -88,16 +88,14 @@ typedef struct fs2_gemm_desc {
    * domain, fs2_pad_rows).  bf16, both K-major, no split / batch / conv; runs on the
    * persistent 256-row kernel (FS2_EINVAL where that kernel does not apply).                */
   int c_row_t, c_row_pad;
+  /* grid budget of the persistent GEMM kernels for this call (0 or >= 256: one block per CU):
+   * a GEMM enqueued beside a latency-critical stream -- the weight gradients of the train step
+   * (model.py:279-441 backward) beside the data-gradient chain -- leaves 256 - max_ctas CUs to
+   * the other stream's kernels; 8..255, rounded down to 8.  Results do not depend on it.     */
+  int max_ctas;
 } fs2_gemm_desc;
 
 int fs2_gemm(const fs2_gemm_desc* d, void* stream);
-
-/* grid budget of the persistent GEMM kernels launched on `stream` (default 256 = one block per
- * CU): a stream that runs beside a latency-critical one -- the weight-gradient side stream
- * beside the data-gradient chain of the train step (model.py:279-441 backward) -- leaves
- * 256 - ctas CUs to the other stream's kernels.  8 <= ctas <= 256 (rounded down to 8); the
- * budgets of the last 64 streams given one are kept (older ones revert to 256).             */
-int fs2_set_stream_ctas(void* stream, int ctas);
 
 /* reflect-padding adjoint + dgrad epilogue (K16): Xpad fp32 [B][T+2P][C] from conv_mode 4
  * (nsplit split-K slices split_stride floats apart, summed here; nsplit <= 1: one slice),

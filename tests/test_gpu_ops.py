@@ -667,34 +667,36 @@ def test_gemm_persistent_small_tiles(cuda, M, N, K, op, c32):
     assert rel(C, ref) < 1e-2
 
 
-def test_gemm_stream_grid_budget(cuda):
-    """fs2_set_stream_ctas: persistent GEMMs launched on a stream with a grid budget (the
-    weight-gradient side stream runs at 208 blocks) walk more tiles per block and give results
-    bit-identical to the full-grid launch, for the long-K (gemm_ps_kernel) and short-K
-    (gemm_pk_kernel, 128-row and 256-row tiles) instances."""
-    from fastspeech2 import ops, _native
+def test_gemm_grid_budget(cuda):
+    """fs2_gemm_desc.max_ctas: persistent GEMMs given a grid budget (the weight-gradient side
+    stream's GEMMs run at 208 blocks) walk more tiles per block and give results bit-identical
+    to the full-grid launch, for the long-K (gemm_ps_kernel) and short-K (gemm_pk_kernel,
+    128-row and 256-row tiles) instances, on any stream; out-of-range budgets mean the full
+    grid (8 is the floor).  The budget is per call: the library keeps no per-stream state."""
+    from fastspeech2 import ops
     torch.manual_seed(11)
     shapes = [(31264, 1536, 3456), (31264, 1152, 384), (6400, 384, 1152)]
-    s_budget = torch.cuda.Stream()
-    assert _native.lib().fs2_set_stream_ctas(s_budget.cuda_stream, 64) == 0
-    assert _native.lib().fs2_set_stream_ctas(s_budget.cuda_stream, 4) != 0
+    s_side = torch.cuda.Stream()
     for M, N, K in shapes:
         A = torch.randn(M, K, device=cuda).to(torch.bfloat16)
         W = (torch.randn(N, K, device=cuda) * 0.05).to(torch.bfloat16)
         bias = torch.randn(N, device=cuda)
         C0 = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
         ops.gemm(M, N, K, A, K, W, K, C0, N, dt=1, bias=bias, relu=1)
-        s_budget.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s_budget):
-            C1 = torch.full((M, N), float("nan"), device=cuda, dtype=torch.bfloat16)
-            ops.gemm(M, N, K, A, K, W, K, C1, N, dt=1, bias=bias, relu=1)
-        torch.cuda.current_stream().wait_stream(s_budget)
+        outs = []
+        s_side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s_side):
+            for ctas in (64, 208, 3, 300):
+                C1 = torch.full((M, N), float("nan"), device=cuda, dtype=torch.bfloat16)
+                ops.gemm(M, N, K, A, K, W, K, C1, N, dt=1, bias=bias, relu=1, max_ctas=ctas)
+                outs.append(C1)
+        # the same stream, no budget: the full grid again (nothing was registered)
+        C2 = torch.full((M, N), float("nan"), device=cuda, dtype=torch.bfloat16)
+        ops.gemm(M, N, K, A, K, W, K, C2, N, dt=1, bias=bias, relu=1)
+        torch.cuda.current_stream().wait_stream(s_side)
         torch.cuda.synchronize()
-        assert torch.equal(C0, C1), (M, N, K)
-    # one engine per model registers a side stream each: the table keeps the newest 64 budgets
-    # and never refuses a new stream (host-only; the handles are not launched on)
-    for k in range(100):
-        assert _native.lib().fs2_set_stream_ctas(0x10000 + 64 * k, 208) == 0
+        for C1 in outs + [C2]:
+            assert torch.equal(C0, C1), (M, N, K)
 
 
 @pytest.mark.parametrize("M,N,K,conv", [(31264, 1152, 384, None), (6400, 384, 1536, None),

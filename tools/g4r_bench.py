@@ -25,7 +25,7 @@ def timed(fn, n=20):
 
 def main():
     from fastspeech2 import ops
-    flag = os.environ.get("FS2_G4R", "1") + os.environ.get("FS2_G4R48", "1")
+    flag = os.environ.get("FS2_G4R", "1")
     torch.manual_seed(0)
     bf = torch.bfloat16
     outs = {}
@@ -68,7 +68,7 @@ def main():
         fn = lambda: ops.gemm(Mp, C, KW * F, img, F, Wb, KW * F, Y, C, dt=1, c_fp32=1)
         t = timed(fn)
         outs[name] = Y.cpu()
-        print(f"G4R={flag} G4R48={os.environ.get('FS2_G4R48', '1')} {name:32s} {t:8.1f} us  "
+        print(f"G4R={flag} {name:32s} {t:8.1f} us  "
               f"{2.0 * Mp * C * KW * F / t / 1e6:6.0f} TF/s", flush=True)
     if not only:
         torch.save(outs, f"/tmp/g4r_{flag}.pt")
