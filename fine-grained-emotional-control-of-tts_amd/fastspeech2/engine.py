@@ -347,9 +347,9 @@ class FS2Engine:
         the variance adaptor (model.py:430-441 run first in the backward)"""
         return name.startswith(("decoder.", "linear.", "postnet."))
 
-    def _adam_tables(self, late):
-        """(weight table, range table) of fs2_adamw_prep over the late / early parameters"""
-        ents = [e for n, e in self._wentries.items() if self._adam_late(n) == late]
+    def _adam_range_list(self, late):
+        """flat (start, length) ranges of the late / early non-GEMM parameters (_adam_ranges
+        split by _adam_late; neighbours within the 16-float alignment padding merged)"""
         rng = []
         for name, off, k, _, _ in self.m._layout:
             if name in self._wspecs or self._adam_late(name) != late:
@@ -358,8 +358,13 @@ class FS2Engine:
                 rng[-1] = (rng[-1][0], off + k - rng[-1][0])
             else:
                 rng.append((off, k))
+        return rng
+
+    def _adam_tables(self, late):
+        """(weight table, range table) of fs2_adamw_prep over the late / early parameters"""
+        ents = [e for n, e in self._wentries.items() if self._adam_late(n) == late]
         wt = ops.weight_prep_table(ents) if ents else (None, 0, 0)
-        return wt, ops.adamw_ranges_table(rng, self.dev)
+        return wt, ops.adamw_ranges_table(self._adam_range_list(late), self.dev)
 
     def _adam_launch_late(self):
         """the late parameters' AdamW on the aux stream, after everything queued on the main and

@@ -164,6 +164,7 @@ class FusedTrainer:
             raise ValueError("FusedTrainer(graph=True) needs world size 1")
         self.use_graph = (self.world == 1 and _GRAPH) if graph is None else bool(graph)
         self._graphs = {}
+        self._torn = False         # a failed split step left the optimizer half-applied
 
     def _graph_for(self, batch, intensity, mel_len_max):
         key = tuple(tuple(t.shape) for t in batch[:8]) + (tuple(intensity.shape), mel_len_max)
@@ -211,12 +212,26 @@ class FusedTrainer:
         else:
             # one process: the AdamW scalars are fixed before the backward, which updates the
             # decoder / PostNet parameters on the aux stream during the encoder backward
+            if self._torn:
+                raise RuntimeError("FusedTrainer: an earlier step failed after the decoder / "
+                                   "PostNet half of its AdamW update was applied; the optimizer "
+                                   "state is inconsistent -- restore it from a checkpoint")
             split = self.bucketer is None and self.opt.fused_images()
             if split:
                 scal = self.opt.begin_step(1.0)
                 self.eng.adam_split = (self.opt, scal)
             try:
                 loss = self.forward_backward(batch, intensity, mel_len_max)
+            except BaseException:
+                if split:
+                    if self.eng._adam_late_done:
+                        # the late parameters are already updated (aux stream): the step cannot
+                        # be undone, and retrying it in place would update them twice
+                        self._torn = True
+                    else:    # nothing applied: undo the step count, the step may be retried
+                        self.opt.step_count -= 1
+                    self.eng._adam_late_done = False
+                raise
             finally:
                 self.eng.adam_split = None
             if split:

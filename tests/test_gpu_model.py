@@ -349,3 +349,162 @@ def test_fused_adamw_writes_the_weight_images(cuda, cfg_all, dtname, monkeypatch
         assert torch.equal(w1[k][0], w2[k][0]), k
         assert torch.equal(w1[k][1], w2[k][1]), k
 
+
+
+def _fresh_grads(cfg_kw, flat, batch, inten, seed):
+    """loss and flat gradient of one forward + loss + backward on a NEW model / engine holding
+    the weights ``flat`` (no cached images, workspaces or weight tables from earlier steps)"""
+    from fastspeech2.model import FastSpeech2
+    from fastspeech2.train import FusedTrainer
+    m = FastSpeech2(**cfg_kw, n_speakers=4, act_dtype=torch.bfloat16).cuda().train()
+    m._ensure_packed()
+    m._flat.copy_(flat)
+    m.mark_params_updated()
+    tr = FusedTrainer(m, lr=1e-4, graph=False)
+    loss = tr.forward_backward(batch, inten, seed=seed)
+    torch.cuda.synchronize()
+    return loss.cpu(), m._gflat.cpu(), m._layout
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_shape_changing_steps_match_fresh_engine(cuda, cfg_all, parity_log, graph):
+    """Real training changes (B, T_mel,max) every batch (dataset.py:62-133 pads per batch).
+    FusedTrainer steps over batches that grow, shrink after a grow, and come back, so the
+    engine's per-layer zero-padded dY images (_dy_image) and the K-major weight-gradient
+    images (_km_image) are re-laid-out, grown and re-guarded between steps -- eager, and with
+    HIP-graph replay (one captured graph per shape, several resident).  Every step's loss and
+    every parameter gradient must equal those of a freshly constructed engine on the same
+    weights, batch and dropout seed: bit-exact, except the split-K fp32-atomic weight
+    gradients, whose summation order varies (<= 2e-6 of the tensor's max; observed values go
+    to parity_observed.json).  The caches stay
+    bounded: one dY image per layer, one K-major image per (operand, channels)."""
+    from fastspeech2.model import FastSpeech2
+    from fastspeech2.train import FusedTrainer
+    from fastspeech2.synthetic import make_batch, as_tuple
+    kw = dict(cfg_all["model"]["fastspeech2"], enc_num_layers=2, dec_num_layers=2)
+    shapes = [(8, 60, 90, 31), (6, 30, 50, 32), (8, 70, 110, 33), (6, 30, 50, 34), (8, 60, 90, 31)]
+    batches = []
+    for B, lo, hi, sd in shapes:
+        bt, inten = as_tuple(make_batch(B=B, tp_min=lo, tp_max=hi, seed=sd, device="cuda"))
+        batches.append((bt, inten))
+    tms = [bt[3].shape[1] for bt, _ in batches]
+    assert tms[2] > tms[0] > tms[1] and tms[3] == tms[1]       # grow, shrink after a grow
+    torch.manual_seed(0)
+    m = FastSpeech2(**kw, n_speakers=4, act_dtype=torch.bfloat16).cuda().train()
+    tr = FusedTrainer(m, lr=1e-4, graph=graph)
+    worst = 0.0
+    for i, (bt, inten) in enumerate(batches):
+        w0 = m._flat.clone()
+        loss = tr.step(bt, inten)                 # forward + loss + backward + AdamW
+        torch.cuda.synchronize()
+        g_long = m._gflat.cpu()                   # this step's gradients (AdamW leaves them)
+        l_f, g_f, layout = _fresh_grads(kw, w0, bt, inten, tr.seed)
+        assert torch.equal(loss.cpu(), l_f), (i, loss.cpu(), l_f)
+        for name, off, k, _, _ in layout:
+            a, b = g_long[off:off + k], g_f[off:off + k]
+            if torch.equal(a, b):
+                continue
+            r = ((a - b).abs().max() / b.abs().max().clamp(min=1e-30)).item()
+            worst = max(worst, r)
+            assert r <= 2e-6, (i, name, r)
+    eng = m.engine()
+    L = kw["enc_num_layers"] + kw["dec_num_layers"]
+    assert len(eng._img) == L, sorted(eng._img)
+    assert len(eng._km) <= 6, sorted(eng._km)
+    if graph:
+        assert len(tr._graphs) == 3               # one per distinct shape, all resident
+    parity_log[f"shape_changing_steps_graph{int(graph)}_max_grad_rel"] = worst
+
+
+def test_split_adamw_equals_single_update(cuda, cfg_all):
+    """FusedTrainer's split AdamW (the decoder / mel-linear / PostNet parameters on the aux
+    stream during the encoder backward, the rest after it; engine._adam_launch_late +
+    adamw_step_split) against ONE fs2_adamw_prep over everything (engine.adamw_step), bf16, on
+    fixed random gradients: parameters, both moments and every Wf / Wb weight image
+    bit-identical.  The two range tables are disjoint and together cover every non-GEMM
+    parameter; the two weight tables partition the GEMM weights."""
+    from fastspeech2.model import FastSpeech2
+    from fastspeech2.optim import FusedAdamW
+    kw = dict(cfg_all["model"]["fastspeech2"], enc_num_layers=2, dec_num_layers=2)
+    res = []
+    for split in (False, True):
+        torch.manual_seed(0)
+        m = FastSpeech2(**kw, n_speakers=4, act_dtype=torch.bfloat16).cuda()
+        eng = m.engine()
+        eng.prepare_weights()
+        opt = FusedAdamW(m, lr=1e-3)
+        g = torch.Generator(device="cuda").manual_seed(7)
+        for _ in range(2):
+            m._gflat.copy_(torch.randn(m._gflat.shape, device="cuda", generator=g) * 1e-3)
+            scal = opt.begin_step(0.5)
+            if split:
+                eng.adam_split = (opt, scal)
+                eng._adam_launch_late()
+                eng.adam_split = None
+                eng.adamw_step_split(opt, scal)
+            else:
+                eng.adamw_step(opt, *scal)
+        torch.cuda.synchronize()
+        res.append((m._flat.clone(), opt.exp_avg.clone(), opt.exp_avg_sq.clone(),
+                    {k: (a.clone(), b.clone()) for k, (a, b) in eng.w.items()}))
+        if split:
+            n = m._flat.numel()
+            cover = {}
+            for late in (False, True):
+                mask = torch.zeros(n, dtype=torch.bool)
+                for st, ln in eng._adam_range_list(late):
+                    mask[st:st + ln] = True
+                cover[late] = mask
+            assert not (cover[False] & cover[True]).any()
+            for name, off, k, _, _ in m._layout:
+                if name in eng._wspecs:
+                    continue
+                assert bool((cover[False] | cover[True])[off:off + k].all()), name
+                assert bool(cover[eng._adam_late(name)][off:off + k].all()), name
+            late_w = {nm for nm in eng._wspecs if eng._adam_late(nm)}
+            early_w = set(eng._wspecs) - late_w
+            assert late_w and early_w and set(eng._wentries) == late_w | early_w
+    (p1, m1, v1, w1), (p2, m2, v2, w2) = res
+    assert torch.equal(p1, p2) and torch.equal(m1, m2) and torch.equal(v1, v2)
+    for k in w1:
+        assert torch.equal(w1[k][0], w2[k][0]), k
+        assert torch.equal(w1[k][1], w2[k][1]), k
+
+
+def test_failed_split_step_is_not_half_applied_silently(cuda, cfg_all, monkeypatch):
+    """A step whose backward raises: before the late AdamW half was launched the
+    optimizer is untouched (step count restored) and the step can be retried; after it, the
+    trainer refuses further steps instead of running on a half-updated optimizer."""
+    from fastspeech2.model import FastSpeech2
+    from fastspeech2.train import FusedTrainer
+    from fastspeech2.synthetic import make_batch, as_tuple
+    kw = dict(cfg_all["model"]["fastspeech2"], enc_num_layers=1, dec_num_layers=1)
+    bt, inten = as_tuple(make_batch(B=4, tp_min=30, tp_max=40, seed=5, device="cuda"))
+    torch.manual_seed(0)
+    m = FastSpeech2(**kw, n_speakers=4, act_dtype=torch.bfloat16).cuda().train()
+    tr = FusedTrainer(m, lr=1e-4, graph=False)
+    tr.step(bt, inten)
+    eng = m.engine()
+    assert tr.opt.step_count == 1
+
+    def boom(*a, **k):
+        raise RuntimeError("injected")
+    monkeypatch.setattr(eng, "backward", boom)
+    with pytest.raises(RuntimeError, match="injected"):
+        tr.step(bt, inten)
+    assert tr.opt.step_count == 1 and not eng._adam_late_done and eng.adam_split is None
+    monkeypatch.undo()
+    tr.step(bt, inten)                        # retried: a normal step
+    assert tr.opt.step_count == 2
+    late = eng._adam_launch_late
+
+    def late_then_boom():
+        late()
+        raise RuntimeError("injected late")
+    monkeypatch.setattr(eng, "_adam_launch_late", late_then_boom)
+    with pytest.raises(RuntimeError, match="injected late"):
+        tr.step(bt, inten)
+    monkeypatch.undo()
+    with pytest.raises(RuntimeError, match="inconsistent"):
+        tr.step(bt, inten)
+    torch.cuda.synchronize()

@@ -293,11 +293,13 @@ def test_avg_over_durations_bit_exact(cuda, golden_dir):
 
 
 @pytest.mark.parametrize("dt,B,Tp,ties", [(torch.float32, 3, 20, False), (torch.bfloat16, 3, 20, False),
-                                          (torch.float32, 4, 60, True), (torch.bfloat16, 4, 60, True)])
+                                          (torch.float32, 4, 60, True), (torch.bfloat16, 4, 60, True),
+                                          (torch.float32, 300, 8, False)])
 def test_fused_loss_vs_oracle(cuda, dt, B, Tp, ties):
     """fs2_loss_fwd_bwd vs LossOracle (loss.py:101-186).  ``ties``: predictions clamped so
     their max / min repeat many times across the min-max kernels' 16 chunks per utterance --
-    the SSIM normalisation gradient is split over every tie (torch amax / amin semantics)."""
+    the SSIM normalisation gradient is split over every tie (torch amax / amin semantics).
+    B = 300: more utterances than one 256-thread finalize block (strided per-utterance sums)."""
     from fastspeech2.loss import fused_loss
     from oracle.fs2_oracle import LossOracle
     torch.manual_seed(4 + Tp)
@@ -1040,13 +1042,15 @@ def test_conv_fwd_padded_image(cuda, B, T, C, O, KW):
 
 
 @pytest.mark.parametrize("dt,code", [(torch.float32, 0), (torch.bfloat16, 1)])
-@pytest.mark.parametrize("B,T,V", [(32, 200, 95), (3, 37, 128), (1, 5, 7)])
+@pytest.mark.parametrize("B,T,V", [(32, 200, 95), (3, 37, 128), (1, 5, 7), (4, 50, 200),
+                                   (2, 40, 300)])
 def test_embedding_fwd_bwd(cuda, dt, code, B, T, V):
     """fs2_embed_fwd (table row + positional encoding, pad rows zero) and fs2_embed_bwd (token
     rows scatter-added into the table gradient through per-wave LDS accumulators, fixed-order
     combine) against torch: forward exact up to the output rounding, backward rel 1e-5 (fp32
     sums of the same values in another order).  Bench shape (B*T_p = 6400, V = 95 = n_char),
-    a ragged one with V at the kernel's limit, a tiny one; pad tokens (id 0) are masked."""
+    a ragged one with V at one grid.z id window (128), a tiny one, and V = 200 / 300 (two and
+    three id windows); pad tokens (id 0) are masked."""
     from fastspeech2 import ops
     torch.manual_seed(B * T + V)
     D = 384
@@ -1089,3 +1093,47 @@ def test_rowdot_bwd(cuda, dt, code, M, D, ldu):
     assert rel(du, (g[:, None] * w[None, :]).to(dt)) < (1e-6 if dt == torch.float32 else 1e-2)
     assert rel(dw, (g[:, None] * u[:, :D].float()).sum(0)) < 1e-5
     assert abs(db.item() - g.sum().item()) <= 1e-4 * max(1.0, abs(g.sum().item()))
+
+
+def test_attention_dropout_mask_statistics(cuda, parity_log):
+    """Quality of the attention-probability dropout draw (fs2_attn_rowhash + one fs2_attn_mix
+    round per key pair, fs2_common.h), on the bench decoder grid (B*H*T rows x T keys = 61 M
+    draws, p = 0.1) taken from the materialised softmax path, which uses the same bits as the
+    fused kernels: keep rate within 6 binomial sigmas of 0.9; lag-1 (inside and across key
+    pairs) and lag-2 correlations along keys, and lag-1 / lag-2 along rows, below 0.002 (an
+    ideal generator's sigma here is ~1.3e-4); two dropout salts draw unrelated masks."""
+    from fastspeech2 import ops
+    B, H, T, p = 32, 2, 977, 0.1
+    ldt = (T + 7) // 8 * 8
+    S = torch.zeros(B * H, T, ldt, device=cuda)
+    kp = torch.zeros(B * T, dtype=torch.uint8, device=cuda)
+    Pm = torch.empty_like(S)
+    stats = {}
+
+    def keep_bits(salt):
+        Pd = torch.empty_like(S)
+        ops.softmax_fwd(S, kp, B, H, T, T, ldt, 1.0, p, 1234, salt, Pm, Pd, dt=0)
+        torch.cuda.synchronize()
+        return (Pd[:, :, :T] > 0).reshape(B * H * T, T).float()
+
+    def corr(a, b):
+        a = a - a.mean()
+        b = b - b.mean()
+        return ((a * b).mean() / (a.std() * b.std())).item()
+
+    k = keep_bits(9)
+    n = k.numel()
+    rate = k.mean().item()
+    sigma = (p * (1 - p) / n) ** 0.5
+    assert abs(rate - (1 - p)) <= 6 * sigma, rate
+    stats["keep_rate"] = rate
+    stats["lag1_key_in_pair"] = corr(k[:, 0:T - 1:2], k[:, 1:T:2])
+    stats["lag1_key_across_pair"] = corr(k[:, 1:T - 1:2], k[:, 2:T:2])
+    stats["lag2_key"] = corr(k[:, :-2], k[:, 2:])
+    stats["lag1_row"] = corr(k[:-1], k[1:])
+    stats["lag2_row"] = corr(k[:-2], k[2:])
+    stats["other_salt"] = corr(k, keep_bits(10))
+    for name, c in stats.items():
+        if name != "keep_rate":
+            assert abs(c) < 2e-3, (name, c)
+    parity_log["attn_dropout_mask_stats"] = stats
