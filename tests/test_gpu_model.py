@@ -375,7 +375,7 @@ def test_shape_changing_steps_match_fresh_engine(cuda, cfg_all, parity_log, grap
     HIP-graph replay (one captured graph per shape, several resident).  Every step's loss and
     every parameter gradient must equal those of a freshly constructed engine on the same
     weights, batch and dropout seed: bit-exact, except the split-K fp32-atomic weight
-    gradients, whose summation order varies (<= 2e-6 of the tensor's max; observed values go
+    gradients, whose summation order varies (<= 1e-6 of the tensor's max, observed 2.1e-7; values go
     to parity_observed.json).  The caches stay
     bounded: one dY image per layer, one K-major image per (operand, channels)."""
     from fastspeech2.model import FastSpeech2
@@ -406,7 +406,7 @@ def test_shape_changing_steps_match_fresh_engine(cuda, cfg_all, parity_log, grap
                 continue
             r = ((a - b).abs().max() / b.abs().max().clamp(min=1e-30)).item()
             worst = max(worst, r)
-            assert r <= 2e-6, (i, name, r)
+            assert r <= 1e-6, (i, name, r)
     eng = m.engine()
     L = kw["enc_num_layers"] + kw["dec_num_layers"]
     assert len(eng._img) == L, sorted(eng._img)
