@@ -246,8 +246,17 @@ __device__ __forceinline__ int build_kvalid(uint8_t* kval, int* kbuf, const Attn
     if (v) last = j + 1;
     else first = min(first, j);
   }
-  atomicMax(&kbuf[0], last);
-  atomicMin(&kbuf[1], first);
+  // one LDS atomic per wave: 512 same-address atomics serialised into ~10 k cycles of every
+  // block's prologue (tools/attn_stamps.py)
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    last = max(last, __shfl_xor(last, o, 64));
+    first = min(first, __shfl_xor(first, o, 64));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMax(&kbuf[0], last);
+    atomicMin(&kbuf[1], first);
+  }
   __syncthreads();
   *kfull = kbuf[1];
   return kbuf[0];
@@ -286,13 +295,13 @@ __global__ void __launch_bounds__(W8 * 64 / QG, 1) attn_fwd_kernel(AttnP p) {
   const int b = z / p.H, h = z - b * p.H;
   const uint32_t dkey = fs2_drop_key(p.seed, p.salt);
   const bool drop = p.p_drop > 0.f;
-  int kfull;
-  const int kend = build_kvalid(kval, kbuf, p, b, h, &kfull);
   const bf16* Qb = p.qkv + (long)b * p.T * p.ldq + h * DH;
   const bf16* Kb = Qb + p.D;
   const bf16* Vb = Qb + 2 * p.D;
   const float c = p.scale_log2;
 
+  // prologue: the Q fragments, tile 0's K / V DMA and the key-pad bytes issued before anything
+  // waits (one memory round trip instead of two in sequence)
   int qi[QG];
   bf16x8 qf[QG][NS];
   uint32_t dc[QG][4][2];
@@ -319,12 +328,12 @@ __global__ void __launch_bounds__(W8 * 64 / QG, 1) attn_fwd_kernel(AttnP p) {
   TileDma<DH, NT / 64> dma;
   dma.init(wave, lane, p.ldq);
   const i32x4 rsK = make_rsrc(Kb), rsV = make_rsrc(Vb);
+  dma.issue(smem, rsK, p.ldq, 0, p.T, wave);
+  dma.issue(smem + TB, rsV, p.ldq, 0, p.T, wave);
+  int kfull;
+  const int kend = build_kvalid(kval, kbuf, p, b, h, &kfull);
   const int ntile = (kend + 63) / 64;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // Q fragments resident before the ring
-  if (ntile > 0) {
-    dma.issue(smem, rsK, p.ldq, 0, p.T, wave);
-    dma.issue(smem + TB, rsV, p.ldq, 0, p.T, wave);
-  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // Q fragments and tile 0 resident
   for (int t = 0; t < ntile; ++t) {
     const int k0 = t * 64;
 #ifdef FS2_EXPERIMENTS
@@ -513,37 +522,46 @@ __global__ void __launch_bounds__(W8 * 64 / QG, 1) attn_bwd_dq_kernel(AttnP p) {
   const int b = z / p.H, h = z - b * p.H;
   const uint32_t dkey = fs2_drop_key(p.seed, p.salt);
   const bool drop = p.p_drop > 0.f;
-  int kfull;
-  const int kend = build_kvalid(kval, kbuf, p, b, h, &kfull);
   const bf16* Qb = p.qkv + (long)b * p.T * p.ldq + h * DH;
   const bf16* Kb = Qb + p.D;
   const bf16* Vb = Qb + 2 * p.D;
   const float c = p.scale_log2;
 
+  // prologue: the Q / dO / O fragments, lse, tile 0's K / V DMA and the key-pad bytes are all
+  // issued before anything waits (one memory round trip instead of three in sequence)
   int qi[QG];
-  bf16x8 qf[QG][NS], dof[QG][NS];
+  bf16x8 qf[QG][NS], dof[QG][NS], of[QG][NS];
   float nlse[QG], dsum[QG];
   uint32_t dc[QG][4][2];
 #pragma unroll
   for (int qg = 0; qg < QG; ++qg) {
     qi[qg] = blk * (16 * W8) + wave * 16 * QG + qg * 16 + (lane & 15);
     const bool in = qi[qg] < p.T;
-    float dot = 0.f;
+    const long ro = (long)b * p.T + (in ? qi[qg] : 0);
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
-      if (in) {
-        qf[qg][s] = ld_frag(Qb + (long)qi[qg] * p.ldq + 32 * s + 8 * g);
-        const long ro = (long)b * p.T + qi[qg];
-        dof[qg][s] = ld_frag(p.dout + ro * p.lddo + h * DH + 32 * s + 8 * g);
-        const bf16x8 of = ld_frag(p.o + ro * p.ldo + h * DH + 32 * s + 8 * g);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) dot += (float)dof[qg][s][e] * (float)of[e];
-      } else {
-        qf[qg][s] = bf16x8{};
-        dof[qg][s] = bf16x8{};
-      }
+      qf[qg][s] = in ? ld_frag(Qb + (long)qi[qg] * p.ldq + 32 * s + 8 * g) : bf16x8{};
+      dof[qg][s] = in ? ld_frag(p.dout + ro * p.lddo + h * DH + 32 * s + 8 * g) : bf16x8{};
+      of[qg][s] = in ? ld_frag(p.o + ro * p.ldo + h * DH + 32 * s + 8 * g) : bf16x8{};
     }
     nlse[qg] = in ? -p.lse[(long)z * p.T + qi[qg]] : 0.f;
+  }
+  // K/V tiles double-buffered through LDS-DMA: tile t+1 streams in while tile t computes
+  TileDma<DH, NT / 64> dma;
+  dma.init(wave, lane, p.ldq);
+  const i32x4 rsK = make_rsrc(Kb), rsV = make_rsrc(Vb);
+  dma.issue(smem, rsK, p.ldq, 0, p.T, wave);
+  dma.issue(smem + TB, rsV, p.ldq, 0, p.T, wave);
+  int kfull;
+  const int kend = build_kvalid(kval, kbuf, p, b, h, &kfull);
+#pragma unroll
+  for (int qg = 0; qg < QG; ++qg) {
+    const bool in = qi[qg] < p.T;
+    float dot = 0.f;
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dot += (float)dof[qg][s][e] * (float)of[qg][s][e];
     dsum[qg] = xg_sum(dot);
     const uint32_t row = (uint32_t)(z * p.T + qi[qg]);
     drop_lane_consts(dc[qg], dkey, row, g);
@@ -557,17 +575,8 @@ __global__ void __launch_bounds__(W8 * 64 / QG, 1) attn_bwd_dq_kernel(AttnP p) {
   for (int d = 0; d < ND; ++d)
 #pragma unroll
     for (int qg = 0; qg < QG; ++qg) qacc[d][qg] = f32x4{0, 0, 0, 0};
-
-  // K/V tiles double-buffered through LDS-DMA: tile t+1 streams in while tile t computes
-  TileDma<DH, NT / 64> dma;
-  dma.init(wave, lane, p.ldq);
-  const i32x4 rsK = make_rsrc(Kb), rsV = make_rsrc(Vb);
   const int ntile = (kend + 63) / 64;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // Q fragments resident before the ring
-  if (ntile > 0) {
-    dma.issue(smem, rsK, p.ldq, 0, p.T, wave);
-    dma.issue(smem + TB, rsV, p.ldq, 0, p.T, wave);
-  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // fragments and tile 0 resident
   for (int t = 0; t < ntile; ++t) {
     const int k0 = t * 64;
     const char* Ks = smem + (t & 1) * 2 * TB;
@@ -679,6 +688,9 @@ template <int DH, int W8 = 8>
 __global__ void __launch_bounds__(W8 * 64, 1) attn_bwd_dkv_kernel(AttnP p) {
   constexpr int NS = DH / 32, ND = DH / 16;
   constexpr int TB = 64 * DH * 2;
+#ifdef FS2_EXPERIMENTS
+  const uint64_t st_entry = __builtin_amdgcn_s_memtime();
+#endif
   // one LDS array (a second __shared__ object can make hipcc drain the DMA ring early):
   // [Q 0 | dO 0 | Q 1 | dO 1 | (lse, D, rowhash) 0 | (lse, D, rowhash) 1 | kval | kend, kfull]
   __shared__ __attribute__((aligned(16))) char smem[4 * TB + 1536 + TMAX + 16];
@@ -690,8 +702,6 @@ __global__ void __launch_bounds__(W8 * 64, 1) attn_bwd_dkv_kernel(AttnP p) {
   attn_block_coords(blk, z);
   const int b = z / p.H, h = z - b * p.H;
   const bool drop = p.p_drop > 0.f;
-  int kfull;
-  build_kvalid(kval, kbuf, p, b, h, &kfull);
   const bf16* Qb = p.qkv + (long)b * p.T * p.ldq + h * DH;
   const bf16* Kb = Qb + p.D;
   const bf16* Vb = Qb + 2 * p.D;
@@ -700,8 +710,10 @@ __global__ void __launch_bounds__(W8 * 64, 1) attn_bwd_dkv_kernel(AttnP p) {
 
   const int key = blk * (16 * W8) + wave * 16 + (lane & 15);   // this lane's key (B col)
   const bool kin = key < p.T;
-  const bool kok = kin && kval[key];
   const uint32_t kc = (uint32_t)(key >> 1) * FS2_ATTN_KC;
+  // prologue: the K / V fragments, tile 0's Q / dO / stats DMA and the key-pad bytes are all
+  // issued before anything waits (one memory round trip instead of three in sequence: the
+  // serial prologue took ~22 k cycles of a ~110 k-cycle block, tools/attn_stamps.py)
   bf16x8 kf[NS], vf[NS];
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
@@ -711,13 +723,11 @@ __global__ void __launch_bounds__(W8 * 64, 1) attn_bwd_dkv_kernel(AttnP p) {
   f32x4 dk[ND], dv[ND];
 #pragma unroll
   for (int d = 0; d < ND; ++d) { dk[d] = f32x4{0, 0, 0, 0}; dv[d] = f32x4{0, 0, 0, 0}; }
-  // a block whose keys are all masked contributes nothing: skip the query loop
-  const int anyk = __syncthreads_or(kok);
 
   TileDma<DH, W8> dma;
   dma.init(wave, lane, 0);
   const i32x4 rsQ = make_rsrc(Qb), rsO = make_rsrc(dOb);
-  const int ntile = anyk ? (p.T + 63) / 64 : 0;
+  const int ntile_all = (p.T + 63) / 64;
   // lse / D / row-hash rows of a tile: wave 0 streams them in by 4-byte LDS-DMA
   const long BHT = (long)p.B * p.H * p.T;
   const i32x4 rsL = make_rsrc(p.lse + (long)z * p.T), rsD = make_rsrc(p.dsum + (long)z * p.T);
@@ -730,12 +740,29 @@ __global__ void __launch_bounds__(W8 * 64, 1) attn_bwd_dkv_kernel(AttnP p) {
       blds4(rsH, vo, q0 * 4, (char*)(lsd + buf * 192 + 128));
     }
   };
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // K/V fragments resident before the ring
-  if (ntile > 0) {
+  if (ntile_all > 0) {
     issue_stats(0, 0);
     dma.issue(smem, rsQ, p.ldq, 0, p.T, wave);
     dma.issue(smem + TB, rsO, p.lddo, 0, p.T, wave);
   }
+  int kfull;
+  build_kvalid(kval, kbuf, p, b, h, &kfull);
+  const bool kok = kin && kval[key];
+  // a block whose keys are all masked contributes nothing: skip the query loop
+  const int anyk = __syncthreads_or(kok);
+  const int ntile = anyk ? ntile_all : 0;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // K/V fragments and tile 0 resident
+#ifdef FS2_EXPERIMENTS
+  // xflags 64 (diagnostic, tools/attn_stamps.py): s_memtime cycles per loop segment, summed
+  // over the tiles, written per wave after the workspace's 2*B*H*T floats
+  const bool stamps = p.xflags & 64;
+  uint64_t st_acc[6] = {0, 0, 0, 0, 0, 0};
+  uint64_t st_prev = __builtin_amdgcn_s_memtime();
+  const uint64_t st_pro = st_prev - st_entry;
+#define FS2_STAMP(i) do { if (stamps) { const uint64_t t_ = __builtin_amdgcn_s_memtime(); st_acc[i] += t_ - st_prev; st_prev = t_; } } while (0)
+#else
+#define FS2_STAMP(i) do { } while (0)
+#endif
   for (int t = 0; t < ntile; ++t) {
     const int q0 = t * 64;
     const char* Qs = smem + (t & 1) * 2 * TB;
@@ -743,6 +770,8 @@ __global__ void __launch_bounds__(W8 * 64, 1) attn_bwd_dkv_kernel(AttnP p) {
     const float* ls_s = lsd + (t & 1) * 192;
     const float* ds_s = ls_s + 64;
     const uint32_t* rh_s = (const uint32_t*)(ls_s + 128);
+    // the next tile's pieces go out in one burst here (spread between the S / dP MFMAs below
+    // they cost 2.5 k cycles per tile more, tools/attn_stamps.py)
     if (t + 1 < ntile) {
       issue_stats(q0 + 64, (t + 1) & 1);
       char* nx = smem + ((t + 1) & 1) * 2 * TB;
@@ -754,8 +783,10 @@ __global__ void __launch_bounds__(W8 * 64, 1) attn_bwd_dkv_kernel(AttnP p) {
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
+    FS2_STAMP(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
+    FS2_STAMP(1);
     // S = Q K^T, dP = dO V^T for 64 queries x this wave's 16 keys (C: col key, rows queries)
     f32x4 sacc[4], pacc[4];
 #pragma unroll
@@ -769,6 +800,7 @@ __global__ void __launch_bounds__(W8 * 64, 1) attn_bwd_dkv_kernel(AttnP p) {
         sacc[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, kf[s], sacc[qt], 0, 0, 0);
         pacc[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(oa, vf[s], pacc[qt], 0, 0, 0);
       }
+    FS2_STAMP(2);
     float pdv[4][4], dsv[4][4];
 #pragma unroll
     for (int qt = 0; qt < 4; ++qt) {
@@ -812,6 +844,7 @@ __global__ void __launch_bounds__(W8 * 64, 1) attn_bwd_dkv_kernel(AttnP p) {
     bf16x8 pa, sa;
     TrFrag ob[2], qb[2];
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    FS2_STAMP(3);
     lds_tr_frag_issue(ob[0], Os, DH * 2, 0, 0, lane);
     lds_tr_frag_issue(qb[0], Qs, DH * 2, 0, 0, lane);
     static_for<0, 2 * ND>([&](auto NI) {
@@ -831,23 +864,71 @@ __global__ void __launch_bounds__(W8 * 64, 1) attn_bwd_dkv_kernel(AttnP p) {
       dv[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, tr_val(ob[n & 1]), dv[d], 0, 0, 0);
       dk[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sa, tr_val(qb[n & 1]), dk[d], 0, 0, 0);
     });
+    FS2_STAMP(4);
     __builtin_amdgcn_s_barrier();   // every wave is done with buffer t & 1 before t+2 lands
+    FS2_STAMP(5);
   }
+#ifdef FS2_EXPERIMENTS
+  const uint64_t st_loop_end = __builtin_amdgcn_s_memtime();
+#endif
   // C layout: col = feature (lane & 15), rows = keys 4g + r of this wave's 16; a masked key's
-  // gradients are zero (its lane computed with the key unmasked)
+  // gradients are zero (its lane computed with the key unmasked).  Staged through the (now
+  // free) tile ring as [key][dK | dV] rows, then stored as 16-byte chunks of whole rows: the
+  // 2-byte stores straight from the accumulators were store-issue bound (~6 k cycles/block)
+  if (ntile > 0) {   // the loop's last barrier: every wave is done with the ring
+    constexpr int RB = 4 * DH;   // bytes per staged key row (dK | dV)
+    static_assert(16 * W8 * RB <= 4 * TB, "dK/dV staging must fit the tile ring");
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int kr = blk * (16 * W8) + wave * 16 + 4 * g + r;
-    if (kr >= p.T) continue;
-    const bool ok = kval[kr];
-    bf16* krow = p.dqkv + ((long)b * p.T + kr) * p.lddq + p.D + h * DH;
-    bf16* vrow = krow + p.D;
+    for (int r = 0; r < 4; ++r) {
+      const int kl = wave * 16 + 4 * g + r;
+      const bool ok = kval[min(blk * (16 * W8) + kl, p.T - 1)];
+      bf16* row = (bf16*)(smem + kl * RB);
 #pragma unroll
-    for (int d = 0; d < ND; ++d) {
-      krow[16 * d + (lane & 15)] = (bf16)(ok ? dk[d][r] * p.scale : 0.f);
-      vrow[16 * d + (lane & 15)] = (bf16)(ok ? dv[d][r] * p.inv_keep : 0.f);
+      for (int d = 0; d < ND; ++d) {
+        row[16 * d + (lane & 15)] = (bf16)(ok ? dk[d][r] * p.scale : 0.f);
+        row[DH + 16 * d + (lane & 15)] = (bf16)(ok ? dv[d][r] * p.inv_keep : 0.f);
+      }
+    }
+    __syncthreads();
+    constexpr int CPR = RB / 16;   // 16-byte chunks per staged row
+    for (int i = threadIdx.x; i < 16 * W8 * CPR; i += W8 * 64) {
+      const int kl = i / CPR, cc = i - kl * CPR;
+      const int kr = blk * (16 * W8) + kl;
+      if (kr >= p.T) continue;
+      const int half = cc >= CPR / 2;   // 0: dK, 1: dV
+      bf16* dst = p.dqkv + ((long)b * p.T + kr) * p.lddq + (1 + half) * p.D + h * DH +
+                  (cc - half * (CPR / 2)) * 8;
+      *(u32x4*)dst = *(const u32x4*)(smem + kl * RB + cc * 16);
+    }
+  } else {
+    // an all-masked key block stores zeros (no loop ran; the speculative tile-0 DMA retired above)
+    for (int i = threadIdx.x; i < 16 * W8 * (DH / 8) * 2; i += W8 * 64) {
+      const int kl = i / (DH / 4), cc = i - kl * (DH / 4);
+      const int kr = blk * (16 * W8) + kl;
+      if (kr >= p.T) continue;
+      const int half = cc >= DH / 8;
+      bf16* dst = p.dqkv + ((long)b * p.T + kr) * p.lddq + (1 + half) * p.D + h * DH +
+                  (cc - half * (DH / 8)) * 8;
+      *(u32x4*)dst = u32x4{0u, 0u, 0u, 0u};
     }
   }
+#ifdef FS2_EXPERIMENTS
+  if (stamps) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint64_t st_end = __builtin_amdgcn_s_memtime();
+    if (lane == 0) {
+      uint64_t* o = (uint64_t*)(p.dsum + 2L * p.B * p.H * p.T) +
+                    ((long)(blockIdx.x + gridDim.x * blockIdx.y) * W8 + wave) * 16;
+      for (int i = 0; i < 6; ++i) o[i] = st_acc[i];
+      o[6] = ntile;
+      o[7] = st_pro;
+      o[8] = st_end - st_loop_end;
+      o[9] = st_entry;
+      o[10] = st_end;
+    }
+  }
+#endif
+#undef FS2_STAMP
 }
 
 int attn_qg_fwd(int dh) { return dh <= 128 ? 2 : 1; }
@@ -958,6 +1039,7 @@ extern "C" int fs2_attn_bwd(const void* qkv, int64_t ldq, const uint8_t* key_pad
   p.inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
   p.seed = seed; p.salt = salt;
   p.thr16 = (uint32_t)(p_drop * 65536.f + 0.5f);
+  p.xflags = fs2_exp_int("FS2_ATTN_FLAGS", 0);
   hipStream_t s = (hipStream_t)stream;
   switch (dh) {
     case 64: launch_bwd<64>(p, s); break;
