@@ -23,7 +23,11 @@ def t(fn, n=10):
 def main():
     from fastspeech2 import ops, _native
     _native.load()
-    for M, N, K in ((8192, 8192, 8192), (4096, 4096, 4096), (31264, 1536, 3456), (31264, 3456, 1536)):
+    shapes = ((8192, 8192, 8192), (4096, 4096, 4096), (31264, 1536, 3456), (31264, 3456, 1536))
+    only = os.environ.get("GS_ONLY")   # comma-separated shape indices
+    if only:
+        shapes = [shapes[int(i)] for i in only.split(",")]
+    for M, N, K in shapes:
         A = (torch.rand(M, K, device="cuda") * 2 - 1).to(torch.bfloat16)
         W = (torch.rand(N, K, device="cuda") * 2 - 1).to(torch.bfloat16)
         C = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
