@@ -141,7 +141,7 @@ __global__ void add3_mask_rows_kernel(T* X, const T* Y, const T* Z, long ld, con
   if (i >= M * D) return;
   const int m = i / D;
   const long o = (long)m * ld + (i - m * D);
-  X[o] = from_f<T>(((to_f(X[o]) + to_f(Y[o])) + to_f(Z[o])) * keep[m]);
+  X[o] = from_f<T>(((to_f(X[o]) + to_f(Y[o])) + (Z ? to_f(Z[o]) : 0.f)) * keep[m]);
 }
 
 // ---------------------------------------------------------------- predictor head
@@ -501,7 +501,7 @@ extern "C" int fs2_add3_mask_rows(void* X, const void* Y, const void* Z, int64_t
   const long n = (long)M * D;
   if (n == 0) return 0;
   if (n >= 0x7fffffffL) return FS2_EINVAL;   // 32-bit element index
-  if (!X || !Y || !Z || !keep) return FS2_EINVAL;
+  if (!X || !Y || !keep) return FS2_EINVAL;   // Z may be null (a two-term sum)
   hipStream_t s = (hipStream_t)stream;
   DISPATCH_T(dtype,
     hipLaunchKernelGGL(add3_mask_rows_kernel<bf16>, dim3(nblk(n)), dim3(256), 0, s, (bf16*)X, (const bf16*)Y, (const bf16*)Z, ld, keep, M, D),

@@ -142,7 +142,7 @@ class FS2Engine:
         model._ensure_packed()
         self.dev = model._flat.device
         self.params = dict(model.named_parameters())
-        self.grads = model._grad_views
+        self.grads = dict(model._grad_views)
         self.pe_enc = model.sinusoidal_positional_embed_encoder.pe[0].float().contiguous()
         self.pe_dec = model.sinusoidal_positional_embed_decoder.pe[0].float().contiguous()
         self._ws = torch.empty(1 << 20, dtype=torch.float32, device=self.dev)
@@ -157,6 +157,7 @@ class FS2Engine:
         self._aux = torch.cuda.Stream(self.dev) if (self._side is not None and not _NO_AUX) else None
         self.w = {}
         self._wspecs = self._weight_specs()
+        self._fuse_pred_conv1()
         self._prepared_version = None
         self._wtable = None          # device descriptor table of every GEMM weight image
         self.on_grads_ready = None   # optional callback(tag) for DP overlap
@@ -260,6 +261,33 @@ class FS2Engine:
     def empty(self, *shape, dtype=None):
         return torch.empty(*shape, dtype=dtype or self.adt, device=self.dev)
 
+    # the duration and pitch predictors' conv1 (same input Z, model.py:366,379) as one conv with
+    # 2 x 384 output channels: forward and weight gradient are single N = 768 GEMMs, and the data
+    # gradient one K = 3 x 768 GEMM that also sums the two predictors' input gradients
+    PRED1 = "varPred.conv1"
+
+    def _fuse_pred_conv1(self):
+        """register the fused duration / pitch conv1 weight, bias and gradients (flat-buffer
+        views over the two adjacent parameters, model._group_key) in place of the two specs"""
+        wd, wp = "durPred.conv1.conv.weight", "pitchPred.conv1.conv.weight"
+        bd, bp = "durPred.conv1.conv.bias", "pitchPred.conv1.conv.bias"
+        self._gemm_params = set(self._wspecs)
+        if wd not in self._wspecs or self._wspecs[wd] != self._wspecs[wp]:
+            return
+        lay = {n: (o, k) for n, o, k, _, _ in self.m._layout}
+        O, C, KW = self._wspecs[wd]
+        if not (lay[wp][0] == lay[wd][0] + lay[wd][1] and lay[bp][0] == lay[bd][0] + lay[bd][1]):
+            return
+        f, gf = self.m._flat, self.m._gflat
+        ow, nw = lay[wd][0], 2 * lay[wd][1]
+        ob = lay[bd][0]
+        del self._wspecs[wd], self._wspecs[wp]
+        self._wspecs[self.PRED1] = (2 * O, C, KW)
+        self.params[self.PRED1 + ".weight"] = f[ow:ow + nw].view(2 * O, KW, C).permute(0, 2, 1)
+        self.grads[self.PRED1] = gf[ow:ow + nw].view(2 * O, KW, C).permute(0, 2, 1)
+        self.params[self.PRED1 + ".bias"] = f[ob:ob + 2 * O]
+        self._gemm_params |= {wp}
+
     def _weight_specs(self):
         """name -> (O, C, KW, ldf, ldb_rows) for every GEMM weight."""
         c = self.cfg
@@ -304,7 +332,7 @@ class FS2Engine:
                 if name not in self.w:
                     self.w[name] = (self.empty(O, ldf), self.empty(C, ldb))
                 Wf, Wb = self.w[name]
-                W = self.params[name]
+                W = self.params[name + ".weight" if name == self.PRED1 else name]
                 # conv weights are [O][KW][C] in the flat buffer (model._kw_major); the FFN
                 # conv1 data-gradient image has its taps reversed on the padded-dY path
                 okc = int(KW > 1) | (2 if self._pad_dgrad(name) else 0)
@@ -320,7 +348,7 @@ class FS2Engine:
         alignment padding (zeros in every flat buffer) are merged"""
         rng = []
         for name, off, k, _, _ in self.m._layout:
-            if name in self._wspecs:
+            if name in self._gemm_params:
                 continue
             if rng and off - (rng[-1][0] + rng[-1][1]) < 16:
                 rng[-1] = (rng[-1][0], off + k - rng[-1][0])
@@ -352,7 +380,7 @@ class FS2Engine:
         split by _adam_late; neighbours within the 16-float alignment padding merged)"""
         rng = []
         for name, off, k, _, _ in self.m._layout:
-            if name in self._wspecs or self._adam_late(name) != late:
+            if name in self._gemm_params or self._adam_late(name) != late:
                 continue
             if rng and off - (rng[-1][0] + rng[-1][1]) < 16:
                 rng[-1] = (rng[-1][0], off + k - rng[-1][0])
@@ -861,38 +889,89 @@ class FS2Engine:
         return dX
 
     # ------------------------------------------------------------------ variance predictor
-    def _pred_fwd(self, Zin, keep, B, T, name, rate, p_drop, seed, salt):
+    def _pred_fwd(self, Zin, keep, B, T, name, rate, p_drop, seed, salt, a1=None, lda1=None,
+                  salts=None):
+        """one variance predictor (model.py:208-240).  ``a1`` / ``lda1``: its conv1 output
+        already computed (the fused duration / pitch conv1, a column slice of row pitch lda1);
+        ``salts``: its two dropout salts, drawn in advance"""
         D = self.cfg.enc_d_model
         M = B * T
         P = self.params
         c = {"Zin": Zin}
-        a1 = self.empty(M, D)
-        self._fwd(Zin, D, M, T, name + ".conv1.conv.weight", a1, D,
-                  bias=P[name + ".conv1.conv.bias"], relu=1)
+        if a1 is None:
+            a1, lda1 = self.empty(M, D), D
+            self._fwd(Zin, D, M, T, name + ".conv1.conv.weight", a1, D,
+                      bias=P[name + ".conv1.conv.bias"], relu=1)
         v1 = self.empty(M, D)
         m1 = torch.empty(M, dtype=torch.float32, device=self.dev)
         r1 = torch.empty_like(m1)
-        s1 = salt()
-        ops.ln_fwd(a1, D, P[name + ".ln1.norm.weight"], P[name + ".ln1.norm.bias"], 1e-5, v1, D, m1, r1,
-                   M, D, dt=self.dt, seed=seed, p_o=p_drop, salt_o=s1, row_mask=keep)
+        s1 = salts[0] if salts else salt()
+        ops.ln_fwd(a1, lda1, P[name + ".ln1.norm.weight"], P[name + ".ln1.norm.bias"], 1e-5, v1, D, m1,
+                   r1, M, D, dt=self.dt, seed=seed, p_o=p_drop, salt_o=s1, row_mask=keep)
         a2 = self.empty(M, D)
         self._fwd(v1, D, M, T, name + ".conv2.conv.weight", a2, D,
                   bias=P[name + ".conv2.conv.bias"], relu=1)
         v2 = self.empty(M, D)
         m2 = torch.empty(M, dtype=torch.float32, device=self.dev)
         r2 = torch.empty_like(m2)
-        s2 = salt()
+        s2 = salts[1] if salts else salt()
         ops.ln_fwd(a2, D, P[name + ".ln2.norm.weight"], P[name + ".ln2.norm.bias"], 1e-5, v2, D, m2, r2,
                    M, D, dt=self.dt, seed=seed, p_o=p_drop, salt_o=s2, row_mask=keep)
         y = self.empty(B, T)
         ops.rowdot_fwd(v2, D, P[name + ".linear.w.weight"], P[name + ".linear.w.bias"], float(rate),
                        M, D, y, dt=self.dt)
-        c.update(a1=a1, v1=v1, m1=m1, r1=r1, a2=a2, v2=v2, m2=m2, r2=r2, s1=s1, s2=s2,
+        c.update(a1=a1, lda1=lda1, v1=v1, m1=m1, r1=r1, a2=a2, v2=v2, m2=m2, r2=r2, s1=s1, s2=s2,
                  rate=float(rate))
         return y, c
 
-    def _pred_bwd(self, dy, c, keep, B, T, name, p_drop, seed, residual=None, post_mask=False):
-        """returns dZin (masked by keep) [+ residual] for the predictor input."""
+    def _pred_pair_fwd(self, Zin, keep, B, T, pitch_rate, p_drop, seed, salt):
+        """duration and pitch predictors (model.py:366-381), their conv1 as one conv with 768
+        output channels over the shared input (columns 0..383 duration, 384..767 pitch); the
+        dropout salts are drawn in the sequential order (duration's two, then pitch's)"""
+        if self.PRED1 not in self._wspecs:
+            pd, dctx = self._pred_fwd(Zin, keep, B, T, "durPred", 1.0, p_drop, seed, salt)
+            pp, pctx = self._pred_fwd(Zin, keep, B, T, "pitchPred", pitch_rate, p_drop, seed, salt)
+            return pd, dctx, pp, pctx
+        D = self.cfg.enc_d_model
+        M = B * T
+        a1 = self.empty(M, 2 * D)
+        self._fwd(Zin, D, M, T, self.PRED1, a1, 2 * D, bias=self.params[self.PRED1 + ".bias"],
+                  relu=1)
+        sd = (salt(), salt())
+        sp = (salt(), salt())
+        pd, dctx = self._pred_fwd(Zin, keep, B, T, "durPred", 1.0, p_drop, seed, salt,
+                                  a1=a1[:, :D], lda1=2 * D, salts=sd)
+        pp, pctx = self._pred_fwd(Zin, keep, B, T, "pitchPred", pitch_rate, p_drop, seed, salt,
+                                  a1=a1[:, D:], lda1=2 * D, salts=sp)
+        dctx["a1_pair"] = a1
+        return pd, dctx, pp, pctx
+
+    def _pred_pair_bwd(self, d_dur, dctx, d_pitch, pctx, keep, B, T, p_drop, seed, residual=None,
+                       post_mask=False):
+        """backward of _pred_pair_fwd: dZ = keep * (dZ_dur + dZ_pitch) [+ residual, * keep]; the
+        fused conv1's data gradient sums both predictors' input gradients inside one GEMM"""
+        if "a1_pair" not in dctx:
+            dZa = self._pred_bwd(d_pitch, pctx, keep, B, T, "pitchPred", p_drop, seed,
+                                 residual=residual)
+            return self._pred_bwd(d_dur, dctx, keep, B, T, "durPred", p_drop, seed, residual=dZa,
+                                  post_mask=post_mask)
+        D = self.cfg.enc_d_model
+        M = B * T
+        da1 = self.empty(M, 2 * D)
+        self._pred_bwd(d_pitch, pctx, keep, B, T, "pitchPred", p_drop, seed, da1=da1[:, D:])
+        self._pred_bwd(d_dur, dctx, keep, B, T, "durPred", p_drop, seed, da1=da1[:, :D])
+        dZ = self.empty(M, D)
+        self._dgrad(da1, 2 * D, M, T, self.PRED1, dZ, D, row_scale=keep, residual=residual,
+                    ldr=D if residual is not None else 0,
+                    row_scale_post=keep if post_mask else None)
+        self._wgrad(da1, 2 * D, dctx["Zin"], D, M, T, self.PRED1)
+        return dZ
+
+    def _pred_bwd(self, dy, c, keep, B, T, name, p_drop, seed, residual=None, post_mask=False,
+                  da1=None):
+        """returns dZin (masked by keep) [+ residual] for the predictor input; ``da1``: write the
+        conv1 output gradient there (a column slice of the fused conv1's, row pitch 2 D) and
+        stop -- the fused conv1's own backward follows (_pred_pair_bwd)"""
         D = self.cfg.enc_d_model
         M = B * T
         P, G = self.params, self.grads
@@ -911,12 +990,17 @@ class FS2Engine:
         dv1 = self.empty(M, D)
         self._dgrad(da2, D, M, T, w2, dv1, D)
         self._wgrad(da2, D, c["v1"], D, M, T, w2)
-        da1 = self.empty(M, D)
-        ops.ln_bwd(dv1, D, c["a1"], D, c["m1"], c["r1"], P[name + ".ln1.norm.weight"],
-                   P[name + ".ln1.norm.bias"], da1, D, M, D, dt=self.dt, ws=self.ws(ops.ln_ws(M, D)),
+        fused = da1 is not None
+        if not fused:
+            da1 = self.empty(M, D)
+        ld1 = 2 * D if fused else D
+        ops.ln_bwd(dv1, D, c["a1"], c["lda1"], c["m1"], c["r1"], P[name + ".ln1.norm.weight"],
+                   P[name + ".ln1.norm.bias"], da1, ld1, M, D, dt=self.dt, ws=self.ws(ops.ln_ws(M, D)),
                    seed=seed, p_o=p_drop, salt_o=c["s1"], row_mask=keep, relu_gate_in=1,
                    dgamma=G[name + ".ln1.norm.weight"], dbeta=G[name + ".ln1.norm.bias"],
                    dcol=G[name + ".conv1.conv.bias"])
+        if fused:
+            return None
         w1 = name + ".conv1.conv.weight"
         dZ = self.empty(M, D)
         self._dgrad(da1, D, M, T, w1, dZ, D, row_scale=keep, residual=residual,
@@ -1069,8 +1153,7 @@ class FS2Engine:
         # reads durPred / pitchPred, so they run on the aux stream (same salt order as sequential)
         aux_h = (self._aux_fork(Z, keep_p) if (self._aux is not None and pitch is not None
                                                 and durations is not None) else None)
-        pd, dctx = self._pred_fwd(Z, keep_p, B, Tp, "durPred", 1.0, pv, seed, salt)
-        pp, pctx = self._pred_fwd(Z, keep_p, B, Tp, "pitchPred", pitch_rate, pv, seed, salt)
+        pd, dctx, pp, pctx = self._pred_pair_fwd(Z, keep_p, B, Tp, pitch_rate, pv, seed, salt)
         if aux_h is not None:
             self._aux_exit(aux_h)
         kwp = c.pitch_pred_kernel_size
@@ -1178,9 +1261,8 @@ class FS2Engine:
             # duration and pitch predictor backward chains depend only on the loss gradients
             # and the forward context: run them beside the PostNet / decoder backward
             aux_h = self._aux_fork(d_pitch, d_dur, keep_p)
-            dZp = self._pred_bwd(d_pitch, ctx["pctx"], keep_p, B, Tp, "pitchPred", ctx["p_var"],
-                                 seed)
-            dZd = self._pred_bwd(d_dur, ctx["dctx"], keep_p, B, Tp, "durPred", ctx["p_var"], seed)
+            dZpd = self._pred_pair_bwd(d_dur, ctx["dctx"], d_pitch, ctx["pctx"], keep_p, B, Tp,
+                                       ctx["p_var"], seed)
             self._aux_exit(aux_h)
         # mel receives the loss gradient and the PostNet residual (model.py:431)
         d_mel_total = d_mel.clone()
@@ -1216,16 +1298,15 @@ class FS2Engine:
         ops.embed1d_bwd(dZ2, ctx["a_p"], B, Tp, D, kwp, G["pitchEmbed.conv.weight"],
                         G["pitchEmbed.conv.bias"], dt=self.dt, ws=self.ws(128 * (kwp + 1) * D))
         if aux_h is not None:
-            self._aux_join(aux_h[1], dZp, dZd)
-            # dZ = keep * (dZ2 + dZp + dZd), as the sequential chain's residual epilogues, summed
-            # in fp32 with one rounding
+            self._aux_join(aux_h[1], dZpd)
+            # dZ = keep * (dZ2 + dZ_dur + dZ_pitch), as the sequential chain's residual
+            # epilogues, summed in fp32 with one rounding (the fused conv1's data gradient
+            # already holds dZ_dur + dZ_pitch)
             dZ = dZ2
-            ops.add3_mask_rows(dZ, dZp, dZd, D, keep_p, Mp, D, dt=self.dt)
+            ops.add3_mask_rows(dZ, dZpd, None, D, keep_p, Mp, D, dt=self.dt)
         else:
-            dZa = self._pred_bwd(d_pitch, ctx["pctx"], keep_p, B, Tp, "pitchPred", ctx["p_var"],
-                                 seed, residual=dZ2)
-            dZ = self._pred_bwd(d_dur, ctx["dctx"], keep_p, B, Tp, "durPred", ctx["p_var"], seed,
-                                residual=dZa, post_mask=True)
+            dZ = self._pred_pair_bwd(d_dur, ctx["dctx"], d_pitch, ctx["pctx"], keep_p, B, Tp,
+                                     ctx["p_var"], seed, residual=dZ2, post_mask=True)
         notify("variance")
         if (self.adam_split is not None and self._aux is not None and self._side is not None
                 and self.on_grads_ready is None and _ADAM_OVERLAP

@@ -152,7 +152,12 @@ def _group_key(name, n_dec, n_enc):
         i = int(name.split(".")[2])
         return (2, n_dec - 1 - i, i)
     if name.split(".")[0] in ("energyEmbed", "energyPred", "pitchEmbed", "pitchPred", "durPred"):
-        return (3, 0, 0)
+        # the duration / pitch predictors' conv1 weights, then their biases, adjacent: the
+        # engine runs the two conv1 layers (same input, model.py:366,379) as ONE conv with
+        # 2 x 384 output channels over the contiguous [2O][KW][C] weights and [2O] biases
+        sub = {"durPred.conv1.conv.weight": 0, "pitchPred.conv1.conv.weight": 1,
+               "durPred.conv1.conv.bias": 2, "pitchPred.conv1.conv.bias": 3}.get(name, 4)
+        return (3, sub, 0)
     if name.split(".")[0] in ("concat_proj", "speaker_emb") or name.startswith("encoder.norm."):
         return (4, 0, 0)
     if name.startswith("encoder.layers."):

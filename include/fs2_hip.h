@@ -231,7 +231,8 @@ int fs2_concat_bwd_spk(const void* dcat, int ldc, const int64_t* spk, int B, int
 int fs2_mask_rows(void* X, int64_t ldx, const float* keep, int M, int D, int dtype, void* stream);
 /* X = (X + Y + Z) * keep[row] over M x D (row pitch ld for all three), summed in fp32 and
  * rounded once: the join of the predictor input gradients when the duration / pitch predictor
- * backward runs on its own stream (model.py:365-403 variance adaptor backward). */
+ * backward runs on its own stream (model.py:365-403 variance adaptor backward).  Z may be null
+ * (X = (X + Y) * keep[row]). */
 int fs2_add3_mask_rows(void* X, const void* Y, const void* Z, int64_t ld, const float* keep,
                        int M, int D, int dtype, void* stream);
 

@@ -457,7 +457,7 @@ def test_split_adamw_equals_single_update(cuda, cfg_all):
                 cover[late] = mask
             assert not (cover[False] & cover[True]).any()
             for name, off, k, _, _ in m._layout:
-                if name in eng._wspecs:
+                if name in eng._gemm_params:
                     continue
                 assert bool((cover[False] | cover[True])[off:off + k].all()), name
                 assert bool(cover[eng._adam_late(name)][off:off + k].all()), name

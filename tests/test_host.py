@@ -93,6 +93,9 @@ def test_backward_groups_contiguous_and_complete():
     names = [n for n, _ in m.named_parameters()]
     keys = sorted({_group_key(n, 2, 2) for n in names})
     tags = [group_tag(k) for k in keys]
+    # a group may hold several sort keys (the variance group orders the duration / pitch
+    # conv1 weights and biases first, adjacent): consecutive keys share its tag
+    tags = [t for i, t in enumerate(tags) if i == 0 or t != tags[i - 1]]
     assert tags == ["postnet", "linear", "decoder.layers.1", "decoder.layers.0", "variance",
                     "conditioning", "encoder.layers.1", "encoder.layers.0", "prenet"]
 
