@@ -74,6 +74,7 @@ struct GemmP {
   int vec_align;  // vector epilogue possible if K were not split
   int c_row_t, c_row_pad;  // >0: output row m stored at m + (m / c_row_t) * c_row_pad (ps kernel)
   int max_ctas;            // grid budget of the persistent kernels (blocks), 8..256
+  int a_bytes, b_bytes;    // gemm_w4_kernel: readable byte extents of A and B (zeros past them)
 };
 
 __device__ __forceinline__ u32x4 add_bf16x8(u32x4 a, u32x4 b) {
@@ -1822,6 +1823,199 @@ __device__ i32x2 llvm_raw_buffer_load_v2i32(i32x4 rsrc, int voffset, int soffset
 template <int N>
 __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 
+// ------------------------------------------------------------------ gemm_w4_kernel
+// 256 x 32NF output tile on FOUR waves (2 x 2), each wave a 128 x 16NF register tile: 8 x NF
+// fragments of v_mfma_f32_16x16x32_bf16 in 32NF accumulator registers, one wave per SIMD --
+// NF = 8 is the geometry hipBLASLt runs on these shapes (MT256x256x64, 4 waves); NF = 6 the
+// 256 x 192 tile for N = 384 / 768 and for short-M shapes (more tiles for the 256 CUs).  A
+// wave reads 8 + NF fragments per 8 NF MFMAs (NF = 8: 0.25 per MFMA; the 8-wave kernels' 128 x
+// 64 wave tile: 0.375).  The
+// PMC comparison on the FFN conv1 shape (profiles/r05_gemm_vs_hipblaslt_pmc_*.json) put our
+// 8-wave kernels at ~1 VALU and ~2 SALU instructions per MFMA, hipBLASLt at 0.19 VALU: here
+// every LDS and source address is a lane constant plus an immediate or an SGPR offset.
+// K runs in stages of 32 through a 4-slot LDS-DMA ring ((256 + 32NF) x 64 B per slot: A and B
+// images, rows of 64 B); stage t+3 is issued during stage t, the fragments of stage t+1 are read
+// while stage t's 64 MFMAs run, one barrier per stage.  64-byte rows hold logical 16-byte
+// chunk c of row r at physical chunk c ^ h(r), h = [0, 3, 2, 1][(r >> 2) & 3]: conflict-free
+// for ds_read_b128's four lane groups ({0-3, 12-15, 20-27}, ...), and lane-constant for both
+// the DMA fill (piece = 16 rows) and the fragment reads (16-row fragments).
+// Plain K-major operands (A(m,k) = A[m lda + k], B(n,k) = B[n ldb + k]; rows may overlap, as
+// in the padded-domain convs), K % 64 == 0; epilogue bias / activation / c_row remap; bf16 or
+// fp32 output.  Bytes past a_bytes / b_bytes of an operand read as zeros (partial tiles).
+constexpr int W4_NT = 256;
+constexpr int W4_SLOTS = 4;
+
+// 256 accumulators live in the accumulator file only when pinned there: through the builtin,
+// the allocator parks some in VGPRs and shuttles them (~600 v_accvgpr moves per 128 MFMAs).
+// The statement is an MFMA accumulate chain (D = C, whole): no wait states between them; the
+// readers after the loop wait behind mfma_drain().
+__device__ __forceinline__ void mfma_acc(f32x4& acc, const bf16x8& a, const bf16x8& b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+__device__ __forceinline__ void mfma_drain() { asm volatile("s_nop 15\n\ts_nop 3" ::: "memory"); }
+
+template <bool C32, int NF>
+__global__ void __launch_bounds__(W4_NT, 1) gemm_w4_kernel(GemmP p) {
+  constexpr int BNW = 32 * NF;                 // block tile columns
+  constexpr int STAGE = (256 + BNW) * 64;      // bytes of one 32-deep stage (A and B images)
+  constexpr int NPB = NF / 2;                  // B pieces per wave per stage (A: 4)
+  constexpr int NP = 4 + NPB;                  // LDS-DMA pieces per wave per stage
+  __shared__ __attribute__((aligned(16))) char smem[W4_SLOTS * STAGE];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  // XCD-aware bijective remap: an XCD's blocks take consecutive tiles, which share A rows
+  const int nwg = p.tiles_m * p.tiles_n;
+  const int orig = blockIdx.x;
+  const int xcd = orig & 7, q = nwg >> 3, r8 = nwg & 7;
+  const int bid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (orig >> 3);
+  const int tm = bid / p.tiles_n, tn = bid - tm * p.tiles_n;
+  const int m0 = tm * 256, n0 = tn * BNW;
+  const int nst = p.K / 32;
+
+  // LDS-DMA piece i of an image = rows 16i .. 16i+15; lane L writes row 16i + (L >> 2) at
+  // physical chunk L & 3, i.e. logical chunk (L & 3) ^ h(L >> 2)
+  const int lc = (lane & 3) ^ ((4 - (lane >> 4)) & 3);
+  const int voa = ((lane >> 2) * (int)p.lda + lc * 8) * 2;
+  const int vob = ((lane >> 2) * (int)p.ldb + lc * 8) * 2;
+  i32x4 rsA = make_rsrc(p.A), rsB = make_rsrc(p.B);
+  rsA[2] = p.a_bytes;
+  rsB[2] = p.b_bytes;
+  const int lda2 = (int)p.lda * 2, ldb2 = (int)p.ldb * 2;
+  auto issue_stage = [&](int st) {   // K stage st into ring slot st & 3
+    char* dst = smem + (st & 3) * STAGE;
+    const int kb = st * 64;           // 32 bf16
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+      if (j < 4) {
+        const int pi = wave * 4 + j;
+        blds16(rsA, voa, (m0 + 16 * pi) * lda2 + kb, dst + pi * 1024);
+      } else {
+        const int pi = wave * NPB + j - 4;
+        blds16(rsB, vob, (n0 + 16 * pi) * ldb2 + kb, dst + 256 * 64 + pi * 1024);
+      }
+    }
+  };
+  // fragment reads: lane l takes row (l & 15) of a 16-row fragment, logical chunk l >> 4
+  const int fl = (lane & 15) * 64 + (((lane >> 4) ^ ((4 - ((lane & 15) >> 2)) & 3)) << 4);
+  const int fa = wm * 128 * 64 + fl, fb = 256 * 64 + wn * 16 * NF * 64 + fl;
+
+  f32x4 acc[8][NF];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < NF; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 af[2][8], bfr[2][NF];
+  auto read_frags = [&](int st, bf16x8 (&a)[8], bf16x8 (&b)[NF]) {
+    const char* base = smem + (st & 3) * STAGE;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] = *(const bf16x8*)(base + fa + i * 1024);
+#pragma unroll
+    for (int j = 0; j < NF; ++j) b[j] = *(const bf16x8*)(base + fb + j * 1024);
+  };
+  issue_stage(0);
+  issue_stage(1);
+  issue_stage(2);
+  vm_wait<NP>();   // stages 0, 1 landed (this wave's pieces)
+  __builtin_amdgcn_s_barrier();
+  read_frags(0, af[0], bfr[0]);
+  // stage t: issue stage t+3, read stage t+1's fragments, stage t's 64 MFMAs, then wait for
+  // this wave's pieces of stage t+1 .. t+2 and barrier (after it every wave's have landed, and
+  // no wave still reads the slot stage t+4 overwrites).  Branch-free steady state, two stages
+  // per trip so the fragment sets alternate by name; K % 64 == 0, so nst is even and >= 4.
+  auto iter = [&](int t, bf16x8 (&ac)[8], bf16x8 (&bc)[NF], bf16x8 (&an)[8], bf16x8 (&bn)[NF],
+                  int mode) {   // mode 0 steady, 1 nothing left to issue, 2 last stage
+    const char* nxt = smem + ((t + 1) & 3) * STAGE;
+    char* dst = smem + ((t + 3) & 3) * STAGE;
+    const int kb = (t + 3) * 64;
+    const int xf = XFLAGS(p);   // experiments build: 1 no barrier, 2 no DMA, 4 no fragment reads
+                                // (wrong results; which resource bounds the stage)
+    // source order is issue order (the MFMA statements are volatile): per NF-MFMA row, one
+    // LDS-DMA piece and two fragment reads of the next stage -- its B fragments first (row 0
+    // of the next stage needs all of them), then A in row order, so the first MFMAs after the
+    // barrier find their operands landed
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if (mode == 0 && i < NP && !(xf & 2)) {
+        if (i < 4) {
+          const int pi = wave * 4 + i;
+          blds16(rsA, voa, (m0 + 16 * pi) * lda2 + kb, dst + pi * 1024);
+        } else {
+          const int pi = wave * NPB + i - 4;
+          blds16(rsB, vob, (n0 + 16 * pi) * ldb2 + kb, dst + 256 * 64 + pi * 1024);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < NF; ++j) mfma_acc(acc[i][j], bc[j], ac[i]);
+      if (mode < 2 && !(xf & 4)) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int r = 2 * i + h;     // read slot: B fragments 0 .. NF-1, then A 0 .. 7
+          if (r < NF) bn[r] = *(const bf16x8*)(nxt + fb + r * 1024);
+          else if (r < NF + 8) an[r - NF] = *(const bf16x8*)(nxt + fa + (r - NF) * 1024);
+        }
+      }
+    }
+    if (mode == 0) vm_wait<NP>();
+    else if (mode == 1) vm_wait<0>();
+    if (mode < 2 && !(xf & 1)) __builtin_amdgcn_s_barrier();
+  };
+  int t = 0;
+  for (; t + 4 < nst; t += 2) {
+    iter(t, af[0], bfr[0], af[1], bfr[1], 0);
+    iter(t + 1, af[1], bfr[1], af[0], bfr[0], 0);
+  }
+  iter(t, af[0], bfr[0], af[1], bfr[1], 0);       // t = nst - 4 issues the last stage
+  iter(t + 1, af[1], bfr[1], af[0], bfr[0], 1);
+  iter(t + 2, af[0], bfr[0], af[1], bfr[1], 1);
+  iter(t + 3, af[1], bfr[1], af[0], bfr[0], 2);
+  mfma_drain();
+
+  // ---- epilogue: lane holds columns n .. n+3 (n = n0 + wn 16NF + 16 j + 4 (l >> 4)) of row
+  // m = m0 + wm 128 + 16 i + (l & 15)
+  const int g4 = (lane >> 4) * 4;
+  f32x4 bv[NF];
+#pragma unroll
+  for (int j = 0; j < NF; ++j) {
+    const int n = n0 + wn * 16 * NF + j * 16 + g4;
+    bv[j] = (p.bias && n < p.nvalid) ? *(const f32x4*)(p.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = m0 + wm * 128 + i * 16 + (lane & 15);
+    bool ok = m < p.mvalid;
+    int mo = m;
+    if (p.c_row_t) {
+      if (p.c_row_pad >= 0) {
+        mo = m + (m / p.c_row_t) * p.c_row_pad;
+      } else {   // drop the pad rows of a padded-domain result
+        const int L = p.c_row_t - p.c_row_pad, u = m / L;
+        ok = ok && m - u * L < p.c_row_t;
+        mo = m + u * p.c_row_pad;
+      }
+    }
+    if (!ok) continue;
+#pragma unroll
+    for (int j = 0; j < NF; ++j) {
+      const int n = n0 + wn * 16 * NF + j * 16 + g4;
+      if (n >= p.nvalid) continue;
+      f32x4 v = acc[i][j] + bv[j];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = epi_act(v[e], p.relu);
+      if constexpr (C32) {
+        *(f32x4*)((float*)p.C + (long)mo * p.ldc + n) = v;
+      } else {
+        u32x2 w;
+        w[0] = (unsigned)__builtin_bit_cast(unsigned short, (bf16)v[0]) |
+               ((unsigned)__builtin_bit_cast(unsigned short, (bf16)v[1]) << 16);
+        w[1] = (unsigned)__builtin_bit_cast(unsigned short, (bf16)v[2]) |
+               ((unsigned)__builtin_bit_cast(unsigned short, (bf16)v[3]) << 16);
+        *(u32x2*)((bf16*)p.C + (long)mo * p.ldc + n) = w;
+      }
+    }
+  }
+}
+
 // MI x NJ: the 16 x 16 blocks of a wave's sub-tile (waves as 4 rows x 2 columns), so one tile is
 // (64 MI) x (32 NJ): 4 x 4 = 256 x 128 (the decoder's short-K shapes), 2 x 4 = 128 x 128 and
 // 2 x 2 = 128 x 64 for the encoder / predictor shapes (M = 6400), where 256-row tiles left most
@@ -2590,6 +2784,41 @@ int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
     // persistent 256 x 256 / 256 x 192 kernel: long-K K-major GEMMs without gate / residual
     // operands (FS2_GEMM_NO_PS=1 restores the per-tile kernels for A/B runs)
     static const bool no_ps = getenv_flag("FS2_GEMM_NO_PS");
+    // the 4-wave 128 x 128-per-wave kernel: plain K-major GEMMs with wide outputs and long K
+    // (FS2_GEMM_W4=0 in the experiments build: the 8-wave kernels, for A/B runs)
+    static const bool w4_on = getenv_int("FS2_GEMM_W4", 1) != 0;
+    {
+      const long a_ext = ak ? (long)(p.M - 1) * p.lda + p.K : 0;
+      const long b_ext = bk ? (long)(p.N - 1) * p.ldb + p.K : 0;
+      const bool w4 = w4_on && ak && bk && p.conv_mode == 0 && batch == 1 && p.split_k <= 1 &&
+                      !p.accumulate && !p.gate && !p.residual && !p.row_scale && !p.row_scale_post &&
+                      p.K % 64 == 0 && p.K >= 256 && p.N >= 384 && p.M >= 2048 &&
+                      p.nvalid % 4 == 0 && p.ldc % 4 == 0 && p.vec_align &&
+                      a_ext * 2 < 0x7fffffffL && b_ext * 2 < 0x7fffffffL &&
+                      ((long)p.M + 256) * p.lda * 2 < 0x7fffffffL &&
+                      ((long)p.N + 256) * p.ldb * 2 < 0x7fffffffL;
+      if (w4) {
+        GemmP q = p;
+        q.tiles_m = (p.M + 255) / 256;
+        // tile width by rounds x width over the 256 CUs (ties to the wider tile)
+        const int t256 = q.tiles_m * ((p.N + 255) / 256), t192 = q.tiles_m * ((p.N + 191) / 192);
+        const bool w192 = (long)((t192 + 255) / 256) * 192 < (long)((t256 + 255) / 256) * 256;
+        q.tiles_n = w192 ? (p.N + 191) / 192 : (p.N + 255) / 256;
+        q.a_bytes = (int)(a_ext * 2);
+        q.b_bytes = (int)(b_ext * 2);
+        q.g4_flags = getenv_int("FS2_W4_FLAGS", 0);
+        const dim3 g(q.tiles_m * q.tiles_n);
+        if (w192) {
+          if (p.c_fp32) hipLaunchKernelGGL((gemm_w4_kernel<true, 6>), g, dim3(W4_NT), 0, s, q);
+          else hipLaunchKernelGGL((gemm_w4_kernel<false, 6>), g, dim3(W4_NT), 0, s, q);
+        } else {
+          if (p.c_fp32) hipLaunchKernelGGL((gemm_w4_kernel<true, 8>), g, dim3(W4_NT), 0, s, q);
+          else hipLaunchKernelGGL((gemm_w4_kernel<false, 8>), g, dim3(W4_NT), 0, s, q);
+        }
+        FS2_CHECK_LAUNCH();
+        return 0;
+      }
+    }
     if (p.conv_mode == 6) {
       if (!p.vec_align) return FS2_EALIGN;
       GemmP q = p;

@@ -596,6 +596,50 @@ def test_gemm_persistent_long_k(cuda, M, N, K, c32):
     assert (C2[:, N:] == 0).all()
 
 
+@pytest.mark.parametrize("M,N,K,c32,crow", [(31264, 1536, 3456, 0, None), (2100, 520, 256, 1, None),
+                                             (6000, 1024, 1536, 0, (250, 6)),
+                                             (5120, 776, 640, 1, (200, -4)), (8192, 3456, 1536, 0, None),
+                                             (31000, 1000, 512, 1, (300, 8)),
+                                             (6656, 1536, 3456, 0, (200, -8)),
+                                             (6000, 384, 1536, 1, None)])
+def test_gemm_four_wave(cuda, M, N, K, c32, crow):
+    """Plain K-major GEMMs with N >= 384, K % 64 == 0 and M >= 2048 take the 4-wave kernel
+    (gemm_w4_kernel: 128 x 128 or 128 x 96 per wave, 4-slot LDS-DMA ring): the decoder FFN
+    conv1 shape as a plain GEMM, the encoder's over its padded image (256 x 192 tiles), N = 384,
+    partial row and column tiles on both tile widths (M = 2100 / 31000, N = 520 / 776 / 1000:
+    the zero-filled operand tails), the shortest K (256 = 4 stages, the pipeline's tail only),
+    both output types, bias + ReLU, and both c_row remaps (gaps inserted every 250 / 300 rows;
+    pad rows dropped).  NaN-filled outputs: rows the remap skips stay NaN, every other row is written.
+    fp32 reference on the same bf16 values, rel 1e-2."""
+    from fastspeech2 import ops
+    torch.manual_seed(M + N + K)
+    A = torch.randn(M, K, device=cuda).to(torch.bfloat16)
+    W = (torch.randn(N, K, device=cuda) * 0.05).to(torch.bfloat16)
+    bias = torch.randn(N, device=cuda)
+    ref = torch.relu(A.float() @ W.float().t() + bias)
+    odt = torch.float32 if c32 else torch.bfloat16
+    m = torch.arange(M, device=cuda)
+    if crow is None:
+        rows, keep = m, torch.ones(M, dtype=torch.bool, device=cuda)
+        nrows = M
+    elif crow[1] > 0:
+        rows, keep = m + (m // crow[0]) * crow[1], torch.ones(M, dtype=torch.bool, device=cuda)
+        nrows = M + (M // crow[0] + 1) * crow[1]
+    else:
+        L = crow[0] - crow[1]
+        rows, keep = (m // L) * crow[0] + m % L, (m % L) < crow[0]
+        nrows = (M // L + 1) * crow[0]
+    C = torch.full((nrows, N), float("nan"), device=cuda, dtype=odt)
+    ops.gemm(M, N, K, A, K, W, K, C, N, dt=1, c_fp32=c32, bias=bias, relu=1,
+             **({"c_row": crow} if crow else {}))
+    torch.cuda.synchronize()
+    written = torch.zeros(nrows, dtype=torch.bool, device=cuda)
+    written[rows[keep]] = True
+    assert torch.isfinite(C[written].float()).all()
+    assert torch.isnan(C[~written].float()).all()
+    assert rel(C[rows[keep]], ref[keep]) < 1e-2
+
+
 @pytest.mark.parametrize("M,N,K,op", [(31264, 384, 1152, "residual"), (31264, 1536, 384, "gate"),
                                        (26000, 400, 384, "residual"), (26000, 400, 1000, "gate"),
                                        (31264, 384, 1536, None), (26000, 1152, 384, None)])
