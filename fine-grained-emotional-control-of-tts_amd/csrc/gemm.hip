@@ -74,7 +74,7 @@ struct GemmP {
   int vec_align;  // vector epilogue possible if K were not split
   int c_row_t, c_row_pad;  // >0: output row m stored at m + (m / c_row_t) * c_row_pad (ps kernel)
   int max_ctas;            // grid budget of the persistent kernels (blocks), 8..256
-  int a_bytes, b_bytes;    // gemm_w4_kernel: readable byte extents of A and B (zeros past them)
+  int a_bytes, b_bytes;    // gemm_w4b_kernel: readable byte extents of A and B (zeros past them)
 };
 
 __device__ __forceinline__ u32x4 add_bf16x8(u32x4 a, u32x4 b) {
@@ -1822,28 +1822,23 @@ __device__ i32x2 llvm_raw_buffer_load_v2i32(i32x4 rsrc, int voffset, int soffset
 
 template <int N>
 __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+template <int N>
+__device__ __forceinline__ void lgkm_wait() { asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory"); }
 
-// ------------------------------------------------------------------ gemm_w4_kernel
+// ------------------------------------------------------------------ gemm_w4b_kernel
 // 256 x 32NF output tile on FOUR waves (2 x 2), each wave a 128 x 16NF register tile: 8 x NF
 // fragments of v_mfma_f32_16x16x32_bf16 in 32NF accumulator registers, one wave per SIMD --
 // NF = 8 is the geometry hipBLASLt runs on these shapes (MT256x256x64, 4 waves); NF = 6 the
 // 256 x 192 tile for N = 384 / 768 and for short-M shapes (more tiles for the 256 CUs).  A
 // wave reads 8 + NF fragments per 8 NF MFMAs (NF = 8: 0.25 per MFMA; the 8-wave kernels' 128 x
-// 64 wave tile: 0.375).  The
-// PMC comparison on the FFN conv1 shape (profiles/r05_gemm_vs_hipblaslt_pmc_*.json) put our
-// 8-wave kernels at ~1 VALU and ~2 SALU instructions per MFMA, hipBLASLt at 0.19 VALU: here
-// every LDS and source address is a lane constant plus an immediate or an SGPR offset.
-// K runs in stages of 32 through a 4-slot LDS-DMA ring ((256 + 32NF) x 64 B per slot: A and B
-// images, rows of 64 B); stage t+3 is issued during stage t, the fragments of stage t+1 are read
-// while stage t's 64 MFMAs run, one barrier per stage.  64-byte rows hold logical 16-byte
-// chunk c of row r at physical chunk c ^ h(r), h = [0, 3, 2, 1][(r >> 2) & 3]: conflict-free
-// for ds_read_b128's four lane groups ({0-3, 12-15, 20-27}, ...), and lane-constant for both
-// the DMA fill (piece = 16 rows) and the fragment reads (16-row fragments).
-// Plain K-major operands (A(m,k) = A[m lda + k], B(n,k) = B[n ldb + k]; rows may overlap, as
-// in the padded-domain convs), K % 64 == 0; epilogue bias / activation / c_row remap; bf16 or
-// fp32 output.  Bytes past a_bytes / b_bytes of an operand read as zeros (partial tiles).
+// 64 wave tile: 0.375).  The PMC comparison on the FFN conv1 shape
+// (profiles/r05_gemm_vs_hipblaslt_pmc_*.json) put our 8-wave kernels at ~1 VALU and ~2 SALU
+// instructions per MFMA, hipBLASLt at 0.19 VALU: here every LDS and source address is a lane
+// constant plus an immediate or an SGPR offset, and the main loop holds no VALU besides the
+// MFMAs.  Plain K-major operands (A(m,k) = A[m lda + k], B(n,k) = B[n ldb + k]; rows may
+// overlap, as in the padded-domain convs), K % 128 == 0; epilogue bias / activation / c_row
+// remap; bf16 or fp32 output.  Bytes past a_bytes / b_bytes of an operand read as zeros.
 constexpr int W4_NT = 256;
-constexpr int W4_SLOTS = 4;
 
 // 256 accumulators live in the accumulator file only when pinned there: through the builtin,
 // the allocator parks some in VGPRs and shuttles them (~600 v_accvgpr moves per 128 MFMAs).
@@ -1854,125 +1849,11 @@ __device__ __forceinline__ void mfma_acc(f32x4& acc, const bf16x8& a, const bf16
 }
 __device__ __forceinline__ void mfma_drain() { asm volatile("s_nop 15\n\ts_nop 3" ::: "memory"); }
 
+// epilogue of the 4-wave kernels: lane holds columns n .. n+3 (n = n0 + wn 16NF + 16 j +
+// 4 (l >> 4)) of row m = m0 + wm 128 + 16 i + (l & 15); bias, activation, c_row remap
 template <bool C32, int NF>
-__global__ void __launch_bounds__(W4_NT, 1) gemm_w4_kernel(GemmP p) {
-  constexpr int BNW = 32 * NF;                 // block tile columns
-  constexpr int STAGE = (256 + BNW) * 64;      // bytes of one 32-deep stage (A and B images)
-  constexpr int NPB = NF / 2;                  // B pieces per wave per stage (A: 4)
-  constexpr int NP = 4 + NPB;                  // LDS-DMA pieces per wave per stage
-  __shared__ __attribute__((aligned(16))) char smem[W4_SLOTS * STAGE];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
-  // XCD-aware bijective remap: an XCD's blocks take consecutive tiles, which share A rows
-  const int nwg = p.tiles_m * p.tiles_n;
-  const int orig = blockIdx.x;
-  const int xcd = orig & 7, q = nwg >> 3, r8 = nwg & 7;
-  const int bid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (orig >> 3);
-  const int tm = bid / p.tiles_n, tn = bid - tm * p.tiles_n;
-  const int m0 = tm * 256, n0 = tn * BNW;
-  const int nst = p.K / 32;
-
-  // LDS-DMA piece i of an image = rows 16i .. 16i+15; lane L writes row 16i + (L >> 2) at
-  // physical chunk L & 3, i.e. logical chunk (L & 3) ^ h(L >> 2)
-  const int lc = (lane & 3) ^ ((4 - (lane >> 4)) & 3);
-  const int voa = ((lane >> 2) * (int)p.lda + lc * 8) * 2;
-  const int vob = ((lane >> 2) * (int)p.ldb + lc * 8) * 2;
-  i32x4 rsA = make_rsrc(p.A), rsB = make_rsrc(p.B);
-  rsA[2] = p.a_bytes;
-  rsB[2] = p.b_bytes;
-  const int lda2 = (int)p.lda * 2, ldb2 = (int)p.ldb * 2;
-  auto issue_stage = [&](int st) {   // K stage st into ring slot st & 3
-    char* dst = smem + (st & 3) * STAGE;
-    const int kb = st * 64;           // 32 bf16
-#pragma unroll
-    for (int j = 0; j < NP; ++j) {
-      if (j < 4) {
-        const int pi = wave * 4 + j;
-        blds16(rsA, voa, (m0 + 16 * pi) * lda2 + kb, dst + pi * 1024);
-      } else {
-        const int pi = wave * NPB + j - 4;
-        blds16(rsB, vob, (n0 + 16 * pi) * ldb2 + kb, dst + 256 * 64 + pi * 1024);
-      }
-    }
-  };
-  // fragment reads: lane l takes row (l & 15) of a 16-row fragment, logical chunk l >> 4
-  const int fl = (lane & 15) * 64 + (((lane >> 4) ^ ((4 - ((lane & 15) >> 2)) & 3)) << 4);
-  const int fa = wm * 128 * 64 + fl, fb = 256 * 64 + wn * 16 * NF * 64 + fl;
-
-  f32x4 acc[8][NF];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < NF; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 af[2][8], bfr[2][NF];
-  auto read_frags = [&](int st, bf16x8 (&a)[8], bf16x8 (&b)[NF]) {
-    const char* base = smem + (st & 3) * STAGE;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) a[i] = *(const bf16x8*)(base + fa + i * 1024);
-#pragma unroll
-    for (int j = 0; j < NF; ++j) b[j] = *(const bf16x8*)(base + fb + j * 1024);
-  };
-  issue_stage(0);
-  issue_stage(1);
-  issue_stage(2);
-  vm_wait<NP>();   // stages 0, 1 landed (this wave's pieces)
-  __builtin_amdgcn_s_barrier();
-  read_frags(0, af[0], bfr[0]);
-  // stage t: issue stage t+3, read stage t+1's fragments, stage t's 64 MFMAs, then wait for
-  // this wave's pieces of stage t+1 .. t+2 and barrier (after it every wave's have landed, and
-  // no wave still reads the slot stage t+4 overwrites).  Branch-free steady state, two stages
-  // per trip so the fragment sets alternate by name; K % 64 == 0, so nst is even and >= 4.
-  auto iter = [&](int t, bf16x8 (&ac)[8], bf16x8 (&bc)[NF], bf16x8 (&an)[8], bf16x8 (&bn)[NF],
-                  int mode) {   // mode 0 steady, 1 nothing left to issue, 2 last stage
-    const char* nxt = smem + ((t + 1) & 3) * STAGE;
-    char* dst = smem + ((t + 3) & 3) * STAGE;
-    const int kb = (t + 3) * 64;
-    const int xf = XFLAGS(p);   // experiments build: 1 no barrier, 2 no DMA, 4 no fragment reads
-                                // (wrong results; which resource bounds the stage)
-    // source order is issue order (the MFMA statements are volatile): per NF-MFMA row, one
-    // LDS-DMA piece and two fragment reads of the next stage -- its B fragments first (row 0
-    // of the next stage needs all of them), then A in row order, so the first MFMAs after the
-    // barrier find their operands landed
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      if (mode == 0 && i < NP && !(xf & 2)) {
-        if (i < 4) {
-          const int pi = wave * 4 + i;
-          blds16(rsA, voa, (m0 + 16 * pi) * lda2 + kb, dst + pi * 1024);
-        } else {
-          const int pi = wave * NPB + i - 4;
-          blds16(rsB, vob, (n0 + 16 * pi) * ldb2 + kb, dst + 256 * 64 + pi * 1024);
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < NF; ++j) mfma_acc(acc[i][j], bc[j], ac[i]);
-      if (mode < 2 && !(xf & 4)) {
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int r = 2 * i + h;     // read slot: B fragments 0 .. NF-1, then A 0 .. 7
-          if (r < NF) bn[r] = *(const bf16x8*)(nxt + fb + r * 1024);
-          else if (r < NF + 8) an[r - NF] = *(const bf16x8*)(nxt + fa + (r - NF) * 1024);
-        }
-      }
-    }
-    if (mode == 0) vm_wait<NP>();
-    else if (mode == 1) vm_wait<0>();
-    if (mode < 2 && !(xf & 1)) __builtin_amdgcn_s_barrier();
-  };
-  int t = 0;
-  for (; t + 4 < nst; t += 2) {
-    iter(t, af[0], bfr[0], af[1], bfr[1], 0);
-    iter(t + 1, af[1], bfr[1], af[0], bfr[0], 0);
-  }
-  iter(t, af[0], bfr[0], af[1], bfr[1], 0);       // t = nst - 4 issues the last stage
-  iter(t + 1, af[1], bfr[1], af[0], bfr[0], 1);
-  iter(t + 2, af[0], bfr[0], af[1], bfr[1], 1);
-  iter(t + 3, af[1], bfr[1], af[0], bfr[0], 2);
-  mfma_drain();
-
-  // ---- epilogue: lane holds columns n .. n+3 (n = n0 + wn 16NF + 16 j + 4 (l >> 4)) of row
-  // m = m0 + wm 128 + 16 i + (l & 15)
+__device__ __forceinline__ void w4_epilogue(const GemmP& p, f32x4 (&acc)[8][NF], int m0, int n0,
+                                            int wm, int wn, int lane) {
   const int g4 = (lane >> 4) * 4;
   f32x4 bv[NF];
 #pragma unroll
@@ -2014,6 +1895,156 @@ __global__ void __launch_bounds__(W4_NT, 1) gemm_w4_kernel(GemmP p) {
       }
     }
   }
+}
+
+// K in stages of 64 with 128-byte LDS rows, so every LDS-DMA instruction fetches 8 whole
+// 128-byte lines (a 32-deep, 4-slot version fetching 16 half lines per instruction measured
+// 1330 vs 978 us at 8192^3 and 375 vs 344 us on the FFN conv1 shape).  Two slots of (256 + 32NF)
+// x 128 B (NF = 8: 128 KB); a stage is two 32-deep halves.  During half 0 of stage s the
+// fragments of half 1 are read (B first); a barrier after row 3 (every wave's B reads of the
+// slot retired by a counted lgkmcnt) releases the slot's B image, so the B pieces of stage s+2
+// are issued over rows 4-7; then vmcnt (stage s+1 landed), lgkmcnt(0) and the second barrier
+// release the A image, whose pieces of stage s+2 go out over half 1 while the fragments of
+// (s+1, 0) are read.  On the FFN conv1 shape: 344-347 us; issuing all of a stage's DMA at the
+// start of half 1 436 us, two pieces per row over half 1 only (one barrier per stage) 375 us,
+// A and B swapped (the last pieces with 1.5 halves to land instead of 1) 357 us -- the vector
+// memory path's throughput bounds it, not its latency.  Wave-cycles waiting (SQ_WAIT_ANY):
+// 22 % against hipBLASLt's 7 % on the same instruction mix (SQ_ACTIVE_INST_LDS / _VMEM within
+// 10 %), MFMA busy 50 vs 76 %.  Row r of an image holds logical chunk c at
+// physical chunk c ^ (r & 7): conflict-free for the fragment reads' ds_read_b128 lane groups
+// ({0-3, 12-15, 20-27}, ...), and lane-constant for a DMA piece (8 rows x 8 chunks).
+// FS2_W4_FLAGS (experiments build; results wrong): 1 no barriers, 2 no DMA, 4 no fragment
+// reads -- on the FFN conv1 shape 364 -> 361 / 306 / 331 us, both of the last two 272.
+template <bool C32, int NF>
+__global__ void __launch_bounds__(W4_NT, 1) gemm_w4b_kernel(GemmP p) {
+  constexpr int BNW = 32 * NF;                 // block tile columns
+  constexpr int STAGE = (256 + BNW) * 128;     // bytes of one 64-deep stage (A and B images)
+  constexpr int NP = 8 + NF;                   // LDS-DMA pieces per wave per stage (A 8, B NF)
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int nwg = p.tiles_m * p.tiles_n;
+  const int orig = blockIdx.x;
+  const int xcd = orig & 7, q = nwg >> 3, r8 = nwg & 7;
+  const int bid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (orig >> 3);
+  const int tm = bid / p.tiles_n, tn = bid - tm * p.tiles_n;
+  const int m0 = tm * 256, n0 = tn * BNW;
+  const int nst = p.K / 64;
+
+  // DMA piece i of an image = rows 8i .. 8i+7; lane L writes row 8i + (L >> 3) at physical
+  // chunk L & 7 = logical chunk (L & 7) ^ (L >> 3)
+  const int lc = (lane & 7) ^ (lane >> 3);
+  const int voa = ((lane >> 3) * (int)p.lda + lc * 8) * 2;
+  const int vob = ((lane >> 3) * (int)p.ldb + lc * 8) * 2;
+  i32x4 rsA = make_rsrc(p.A), rsB = make_rsrc(p.B);
+  rsA[2] = p.a_bytes;
+  rsB[2] = p.b_bytes;
+  const int lda8 = (int)p.lda * 16, ldb8 = (int)p.ldb * 16;   // bytes per 8 rows
+  const int sa0 = m0 * (int)p.lda * 2, sb0 = n0 * (int)p.ldb * 2;
+  // DMA piece j (0 .. NP-1) of this wave for the stage at K byte offset kb, into slot base dst
+  auto dma = [&](int j, int kb, char* dst) {
+    if (j < 8) {
+      const int pi = wave * 8 + j;
+      blds16(rsA, voa, sa0 + pi * lda8 + kb, dst + pi * 1024);
+    } else {
+      const int pi = wave * NF + j - 8;
+      blds16(rsB, vob, sb0 + pi * ldb8 + kb, dst + 256 * 128 + pi * 1024);
+    }
+  };
+  // fragment reads: lane l, row (l & 15) of a 16-row fragment, logical chunk 4h + (l >> 4)
+  const int fr = (lane & 15) * 128;
+  const int fl0 = fr + (((lane >> 4) ^ (lane & 7)) << 4);
+  const int fl1 = fr + (((4 + (lane >> 4)) ^ (lane & 7)) << 4);
+  const int fa = wm * 128 * 128, fb = 256 * 128 + wn * 16 * NF * 128;
+
+  f32x4 acc[8][NF];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < NF; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 af[2][8], bfr[2][NF];   // [0]: half 0 of a stage, [1]: half 1
+
+#pragma unroll
+  for (int j = 0; j < NP; ++j) dma(j, 0, smem);
+#pragma unroll
+  for (int j = 0; j < NP; ++j) dma(j, 128, smem + STAGE);
+  vm_wait<NP>();   // stage 0 landed (this wave's pieces)
+  __builtin_amdgcn_s_barrier();
+  {
+    const char* b0 = smem + fl0;
+#pragma unroll
+    for (int j = 0; j < NF; ++j) bfr[0][j] = *(const bf16x8*)(b0 + fb + j * 2048);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) af[0][i] = *(const bf16x8*)(b0 + fa + i * 2048);
+  }
+  const int xf = XFLAGS(p);   // experiments build: 1 no barrier, 2 no DMA, 4 no fragment reads
+
+  // one stage; SL = its slot (compile-time).  Every stage has the same body: the last two
+  // issue DMA for stages nst, nst+1 (K offsets past the row: bytes of the next row, or zeros
+  // past the operand's extent) into slots no one reads again, and the last reads fragments it
+  // never uses -- a branch-free loop, whose accumulators stay in place across the back edge
+  auto stage = [&](int s, auto SLc) {
+    constexpr int SL = decltype(SLc)::value;
+    char* slot = smem + SL * STAGE;
+    const char* nslot = smem + (SL ^ 1) * STAGE;
+    // half 0: MFMAs on set 0; reads of this stage's half 1 into set 1, B first (three per
+    // row: B in rows 0-2, A in rows 2-5); a barrier after row 3 (every wave's B reads of this
+    // slot retired: 12 reads issued, NF of them B) releases the slot's B image, whose pieces of
+    // stage s+2 go out over rows 4-7
+    const int kb = (s + 2) * 128;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if (i >= 4 && !(xf & 2)) {
+#pragma unroll
+        for (int t = 0; t < NF; ++t)
+          if (t * 4 / NF == i - 4) dma(8 + t, kb, slot);
+      }
+#pragma unroll
+      for (int j = 0; j < NF; ++j) mfma_acc(acc[i][j], bfr[0][j], af[0][i]);
+      if (!(xf & 4)) {
+#pragma unroll
+        for (int h = 0; h < 3; ++h) {
+          const int r = 3 * i + h;
+          if (r < NF) bfr[1][r] = *(const bf16x8*)(slot + fl1 + fb + r * 2048);
+          else if (r < NF + 8) af[1][r - NF] = *(const bf16x8*)(slot + fl1 + fa + (r - NF) * 2048);
+        }
+      }
+      if (i == 3) {
+        lgkm_wait<12 - NF>();
+        if (!(xf & 1)) __builtin_amdgcn_s_barrier();
+      }
+    }
+    vm_wait<NF>();   // stage s+1 landed; the B pieces of s+2 may be in flight
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this slot's reads done
+    if (!(xf & 1)) __builtin_amdgcn_s_barrier();
+    // half 1: MFMAs on set 1; the A pieces of stage s+2 into this slot, one per row; reads of
+    // (s+1, half 0), B first
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if (!(xf & 2)) dma(i, kb, slot);
+#pragma unroll
+      for (int j = 0; j < NF; ++j) mfma_acc(acc[i][j], bfr[1][j], af[1][i]);
+      if (!(xf & 4)) {
+#pragma unroll
+        for (int h = 0; h < 3; ++h) {
+          const int r = 3 * i + h;
+          if (r < NF) bfr[0][r] = *(const bf16x8*)(nslot + fl0 + fb + r * 2048);
+          else if (r < NF + 8) af[0][r - NF] = *(const bf16x8*)(nslot + fl0 + fa + (r - NF) * 2048);
+        }
+      }
+    }
+  };
+  // two stages per trip (slots 0, 1); K % 128 == 0, so nst is even.  Each trip ends in
+  // mfma_drain(): should the compiler copy accumulators on the exit edge, its v_accvgpr reads
+  // are spaced from the MFMA statements that wrote them (it does not see them as MFMAs).
+  for (int s = 0; s < nst; s += 2) {
+    stage(s, std::integral_constant<int, 0>{});
+    stage(s + 1, std::integral_constant<int, 1>{});
+    mfma_drain();
+  }
+  vm_wait<0>();   // the last stages' DMA (never read) has landed before the block ends
+  w4_epilogue<C32, NF>(p, acc, m0, n0, wm, wn, lane);
 }
 
 // MI x NJ: the 16 x 16 blocks of a wave's sub-tile (waves as 4 rows x 2 columns), so one tile is
@@ -2787,16 +2818,17 @@ int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
     // the 4-wave 128 x 128-per-wave kernel: plain K-major GEMMs with wide outputs and long K
     // (FS2_GEMM_W4=0 in the experiments build: the 8-wave kernels, for A/B runs)
     static const bool w4_on = getenv_int("FS2_GEMM_W4", 1) != 0;
+    static const int w4_min_k = getenv_int("FS2_W4_MIN_K", 1024);
     {
       const long a_ext = ak ? (long)(p.M - 1) * p.lda + p.K : 0;
       const long b_ext = bk ? (long)(p.N - 1) * p.ldb + p.K : 0;
       const bool w4 = w4_on && ak && bk && p.conv_mode == 0 && batch == 1 && p.split_k <= 1 &&
                       !p.accumulate && !p.gate && !p.residual && !p.row_scale && !p.row_scale_post &&
-                      p.K % 64 == 0 && p.K >= 256 && p.N >= 384 && p.M >= 2048 &&
+                      p.K % 128 == 0 && p.K >= max(256, w4_min_k) && p.N >= 384 && p.M >= 2048 &&
                       p.nvalid % 4 == 0 && p.ldc % 4 == 0 && p.vec_align &&
                       a_ext * 2 < 0x7fffffffL && b_ext * 2 < 0x7fffffffL &&
-                      ((long)p.M + 256) * p.lda * 2 < 0x7fffffffL &&
-                      ((long)p.N + 256) * p.ldb * 2 < 0x7fffffffL;
+                      ((long)p.M + 257) * p.lda * 2 < 0x7fffffffL &&
+                      ((long)p.N + 257) * p.ldb * 2 < 0x7fffffffL;
       if (w4) {
         GemmP q = p;
         q.tiles_m = (p.M + 255) / 256;
@@ -2809,11 +2841,11 @@ int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
         q.g4_flags = getenv_int("FS2_W4_FLAGS", 0);
         const dim3 g(q.tiles_m * q.tiles_n);
         if (w192) {
-          if (p.c_fp32) hipLaunchKernelGGL((gemm_w4_kernel<true, 6>), g, dim3(W4_NT), 0, s, q);
-          else hipLaunchKernelGGL((gemm_w4_kernel<false, 6>), g, dim3(W4_NT), 0, s, q);
+          if (p.c_fp32) hipLaunchKernelGGL((gemm_w4b_kernel<true, 6>), g, dim3(W4_NT), 0, s, q);
+          else hipLaunchKernelGGL((gemm_w4b_kernel<false, 6>), g, dim3(W4_NT), 0, s, q);
         } else {
-          if (p.c_fp32) hipLaunchKernelGGL((gemm_w4_kernel<true, 8>), g, dim3(W4_NT), 0, s, q);
-          else hipLaunchKernelGGL((gemm_w4_kernel<false, 8>), g, dim3(W4_NT), 0, s, q);
+          if (p.c_fp32) hipLaunchKernelGGL((gemm_w4b_kernel<true, 8>), g, dim3(W4_NT), 0, s, q);
+          else hipLaunchKernelGGL((gemm_w4b_kernel<false, 8>), g, dim3(W4_NT), 0, s, q);
         }
         FS2_CHECK_LAUNCH();
         return 0;

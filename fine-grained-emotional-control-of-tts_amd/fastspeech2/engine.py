@@ -77,7 +77,7 @@ _KM_WGRAD = N.exp_int("FS2_KM_WGRAD", 1)
 # decoder FFN conv1 data gradient over the zero-padded dY image (engine._pad_dgrad)
 _PAD_DGRAD = N.exp_int("FS2_PAD_DGRAD", 1)
 # FFN conv1 forward over a reflect-padded X image (engine._pad_fwd)
-_PAD_FWD = N.exp_int("FS2_PAD_FWD", 1)
+_PAD_FWD = N.exp_int("FS2_PAD_FWD", 2)
 # serial mode for per-call-site timing (bench.py --detail runs with the experiments library)
 _NO_SIDE = N.exp_flag("FS2_NO_SIDE_STREAM")
 _NO_AUX = N.exp_flag("FS2_NO_AUX_STREAM")
@@ -457,11 +457,11 @@ class FS2Engine:
         decoder 374 -> 305 us, encoder 100 -> 89 standalone (the implicit conv's per-K-tile
         reflect rows and tap offsets are gone from the loader)"""
         O, C, KW = self._wspecs[wname]
-        # encoder only: the decoder's (M = 31264) measured no faster in the step on the product
-        # library (same box: 315-317 vs 314-315 us for gemm256_kernel's implicit conv) and the
-        # image copy costs 7 us; the encoder's gained 97 -> 91 us.  FS2_PAD_FWD=2 (experiments
-        # build): both.
-        if _PAD_FWD != 2 and not wname.startswith("encoder."):
+        # both stacks: over the image the decoder's conv1 is a plain GEMM for the 4-wave kernel
+        # (gemm_w4b_kernel), step 17.54 -> 17.35 ms on one box (tools/step_ab.sh, 3 rounds);
+        # on the 8-wave implicit conv it had measured no faster.  FS2_PAD_FWD=1 (experiments
+        # build): encoder only.
+        if _PAD_FWD == 1 and not wname.startswith("encoder."):
             return False
         P = (KW - 1) // 2
         return (self.dt == 1 and _PAD_FWD and KW > 1 and C % 64 == 0 and P < T and

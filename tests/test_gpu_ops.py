@@ -596,20 +596,20 @@ def test_gemm_persistent_long_k(cuda, M, N, K, c32):
     assert (C2[:, N:] == 0).all()
 
 
-@pytest.mark.parametrize("M,N,K,c32,crow", [(31264, 1536, 3456, 0, None), (2100, 520, 256, 1, None),
+@pytest.mark.parametrize("M,N,K,c32,crow", [(31264, 1536, 3456, 0, None), (2100, 520, 1024, 1, None),
                                              (6000, 1024, 1536, 0, (250, 6)),
-                                             (5120, 776, 640, 1, (200, -4)), (8192, 3456, 1536, 0, None),
-                                             (31000, 1000, 512, 1, (300, 8)),
+                                             (5120, 776, 1152, 1, (200, -4)), (8192, 3456, 1536, 0, None),
+                                             (31000, 1000, 1024, 1, (300, 8)),
                                              (6656, 1536, 3456, 0, (200, -8)),
                                              (6000, 384, 1536, 1, None)])
 def test_gemm_four_wave(cuda, M, N, K, c32, crow):
-    """Plain K-major GEMMs with N >= 384, K % 64 == 0 and M >= 2048 take the 4-wave kernel
-    (gemm_w4_kernel: 128 x 128 or 128 x 96 per wave, 4-slot LDS-DMA ring): the decoder FFN
-    conv1 shape as a plain GEMM, the encoder's over its padded image (256 x 192 tiles), N = 384,
-    partial row and column tiles on both tile widths (M = 2100 / 31000, N = 520 / 776 / 1000:
-    the zero-filled operand tails), the shortest K (256 = 4 stages, the pipeline's tail only),
-    both output types, bias + ReLU, and both c_row remaps (gaps inserted every 250 / 300 rows;
-    pad rows dropped).  NaN-filled outputs: rows the remap skips stay NaN, every other row is written.
+    """Plain K-major GEMMs with N >= 384, K % 128 == 0, K >= 1024 and M >= 2048 take the 4-wave
+    kernel (gemm_w4b_kernel: 128 x 128 or 128 x 96 per wave, 64-deep stages in two LDS-DMA
+    slots): the decoder FFN conv1 shape as a plain GEMM, the encoder's over its padded image
+    (256 x 192 tiles), N = 384, partial row and column tiles on both tile widths (M = 2100 /
+    31000, N = 520 / 776 / 1000: the zero-filled operand tails), the shortest K (1024), both
+    output types, bias + ReLU, and both c_row remaps (gaps inserted every 250 / 300 rows; pad
+    rows dropped).  NaN-filled outputs: rows the remap skips stay NaN, every other row is written.
     fp32 reference on the same bf16 values, rel 1e-2."""
     from fastspeech2 import ops
     torch.manual_seed(M + N + K)

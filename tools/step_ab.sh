@@ -1,0 +1,26 @@
+# GPU: interleaved bench-step A/B runs on the experiments library.
+# Usage: bash tools/step_ab.sh ROUNDS "ENV_A" "ENV_B" ["ENV_C" ...]   (ENV "-" = no variables)
+# Prints ms/step per arm per round, then each arm's median.
+cd $GRAFT_REPO_ROOT
+EXP=$PWD/fine-grained-emotional-control-of-tts_amd/fastspeech2/libfs2_hip_exp.so
+R=$1; shift
+mkdir -p gpurun_out/ab
+for r in $(seq 1 $R); do
+  i=0
+  for e in "$@"; do
+    V=(); [ "$e" != "-" ] && V=($e)
+    env FS2_HIP_LIB=$EXP "${V[@]}" timeout -k 10 200 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-extractor --no-fp32-leg --no-config2-leg > gpurun_out/ab/b.json 2> gpurun_out/ab/b.err || { tail -20 gpurun_out/ab/b.err; exit 1; }
+    ms=$(python -c "import json; print(json.load(open('gpurun_out/ab/b.json'))['ms_per_step'])")
+    echo "$r arm$i [$e] $ms" | tee -a gpurun_out/ab/log.txt
+    i=$((i+1))
+  done
+done
+python - "$@" <<'PY'
+import sys, statistics, collections
+d = collections.defaultdict(list)
+for line in open("gpurun_out/ab/log.txt"):
+    p = line.split()
+    d[p[1]].append(float(p[-1]))
+for k in sorted(d):
+    print(k, sys.argv[1 + int(k[3:])], "median %.3f" % statistics.median(d[k]), d[k])
+PY

@@ -5,6 +5,6 @@ EXP=$PWD/fine-grained-emotional-control-of-tts_amd/fastspeech2/libfs2_hip_exp.so
 timeout -k 10 300 python -u -m pytest tests -m gpu -k "${1:-four_wave or persistent_long_k}" -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
 tail -2 $O/pytest.log
 echo "== w4 (product)"; timeout -k 10 200 python -u tools/gemm_square.py 2>&1 | grep -v amdgpu.ids || exit 1
-if [ -n "$2" ]; then echo "== 8-wave (FS2_GEMM_W4=0)"; FS2_HIP_LIB=$EXP FS2_GEMM_W4=0 timeout -k 10 200 python -u tools/gemm_square.py 2>&1 | grep -v amdgpu.ids || exit 1; fi
+if [ -n "$2" ]; then echo "== $2"; FS2_HIP_LIB=$EXP env $2 timeout -k 10 200 python -u tools/gemm_square.py 2>&1 | grep -v amdgpu.ids || exit 1; fi
 C="GRBM_GUI_ACTIVE SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_INSTS_SALU"
 GS_ONLY=2 bash tools/pmc.sh w4pmc "w4" "$C" tools/gemm_square.py || exit 1
