@@ -2818,7 +2818,10 @@ int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
     // the 4-wave 128 x 128-per-wave kernel: plain K-major GEMMs with wide outputs and long K
     // (FS2_GEMM_W4=0 in the experiments build: the 8-wave kernels, for A/B runs)
     static const bool w4_on = getenv_int("FS2_GEMM_W4", 1) != 0;
-    static const int w4_min_k = getenv_int("FS2_W4_MIN_K", 1024);
+    // K >= 2048 and >= 160 tiles: the decoder conv2 forward (K = 1536) measured 52 vs 49 us on
+    // the short-K persistent kernel, the encoder's (50 tiles of 256 x 192) 43 us
+    static const int w4_min_k = getenv_int("FS2_W4_MIN_K", 2048);
+    static const int w4_min_tiles = getenv_int("FS2_W4_MIN_TILES", 160);
     {
       const long a_ext = ak ? (long)(p.M - 1) * p.lda + p.K : 0;
       const long b_ext = bk ? (long)(p.N - 1) * p.ldb + p.K : 0;
@@ -2829,12 +2832,13 @@ int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
                       a_ext * 2 < 0x7fffffffL && b_ext * 2 < 0x7fffffffL &&
                       ((long)p.M + 257) * p.lda * 2 < 0x7fffffffL &&
                       ((long)p.N + 257) * p.ldb * 2 < 0x7fffffffL;
-      if (w4) {
+      // tile width by rounds x width over the 256 CUs (ties to the wider tile)
+      const int tm4 = (p.M + 255) / 256;
+      const int t256 = tm4 * ((p.N + 255) / 256), t192 = tm4 * ((p.N + 191) / 192);
+      const bool w192 = (long)((t192 + 255) / 256) * 192 < (long)((t256 + 255) / 256) * 256;
+      if (w4 && (w192 ? t192 : t256) >= w4_min_tiles) {
         GemmP q = p;
-        q.tiles_m = (p.M + 255) / 256;
-        // tile width by rounds x width over the 256 CUs (ties to the wider tile)
-        const int t256 = q.tiles_m * ((p.N + 255) / 256), t192 = q.tiles_m * ((p.N + 191) / 192);
-        const bool w192 = (long)((t192 + 255) / 256) * 192 < (long)((t256 + 255) / 256) * 256;
+        q.tiles_m = tm4;
         q.tiles_n = w192 ? (p.N + 191) / 192 : (p.N + 255) / 256;
         q.a_bytes = (int)(a_ext * 2);
         q.b_bytes = (int)(b_ext * 2);

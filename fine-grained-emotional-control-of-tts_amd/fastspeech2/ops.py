@@ -5,7 +5,10 @@ pointers, passes torch's *current* HIP stream, and raises if the native call rep
 error.  Tensors are owned by torch's caching allocator; the kernels never allocate.
 """
 
+import collections
 import ctypes
+import os
+import sys
 
 import torch
 
@@ -35,6 +38,35 @@ def round_up(x, m):
     return (x + m - 1) // m * m
 
 
+# FS2_GEMM_TRACE=1: count fs2_gemm calls by (shape, operand flags, calling engine line); the
+# table is printed to stderr at exit (tools/gemm_sites.sh) -- which call sites take which kernel
+_TRACE = collections.Counter() if os.environ.get("FS2_GEMM_TRACE") else None
+
+
+def _trace(d, conv):
+    f = sys._getframe(2)
+    while f is not None and os.path.basename(f.f_code.co_filename) == "ops.py":
+        f = f.f_back
+    site = f"{f.f_code.co_name}:{f.f_lineno}" if f is not None else "?"
+    flags = "".join(k for k, v in (("a", not d.a_kmajor), ("b", not d.b_kmajor), ("f", d.c_fp32),
+                                   ("B", d.bias), ("r", d.relu), ("g", d.gate), ("R", d.residual),
+                                   ("s", d.row_scale), ("S", d.row_scale_post),
+                                   ("+", d.accumulate), ("c", d.c_row_t)) if v)
+    _TRACE[(d.M, d.N, d.K, conv[0] if conv else 0, d.split_k, d.batch, flags, site)] += 1
+
+
+def _trace_dump():
+    for k, n in sorted(_TRACE.items(), key=lambda x: -x[0][0] * x[0][1] * x[0][2] * x[1]):
+        M, N_, K, cm, sk, b, fl, site = k
+        print(f"gemm {n:4d}x M {M:6d} N {N_:5d} K {K:6d} conv {cm} split {sk} batch {b:4d} "
+              f"[{fl}] {site}", file=sys.stderr)
+
+
+if _TRACE is not None:
+    import atexit
+    atexit.register(_trace_dump)
+
+
 def gemm(M, N_, K, A, lda, B, ldb, C, ldc, *, dt, a_kmajor=1, b_kmajor=1, conv=None, c_fp32=0,
          c_conv_kw=0, bias=None, relu=0, gate=None, ldg=0, row_scale=None, residual=None, ldr=0,
          row_scale_post=None, accumulate=0, split_k=1, split_stride=0, kvalid=0, mvalid=0,
@@ -59,6 +91,8 @@ def gemm(M, N_, K, A, lda, B, ldb, C, ldc, *, dt, a_kmajor=1, b_kmajor=1, conv=N
     d.batch, d.batch_div = batch, batch_div
     if strides is not None:
         (d.sA1, d.sA2, d.sB1, d.sB2, d.sC1, d.sC2, d.sR1, d.sR2) = strides
+    if _TRACE is not None:
+        _trace(d, conv)
     _chk(N.lib().fs2_gemm(ctypes.byref(d), _s()), "fs2_gemm")
 
 

@@ -596,21 +596,22 @@ def test_gemm_persistent_long_k(cuda, M, N, K, c32):
     assert (C2[:, N:] == 0).all()
 
 
-@pytest.mark.parametrize("M,N,K,c32,crow", [(31264, 1536, 3456, 0, None), (2100, 520, 1024, 1, None),
-                                             (6000, 1024, 1536, 0, (250, 6)),
-                                             (5120, 776, 1152, 1, (200, -4)), (8192, 3456, 1536, 0, None),
-                                             (31000, 1000, 1024, 1, (300, 8)),
+@pytest.mark.parametrize("M,N,K,c32,crow", [(31264, 1536, 3456, 0, None),
+                                             (31000, 1000, 2048, 1, (300, 8)),
+                                             (20000, 520, 2048, 1, None),
                                              (6656, 1536, 3456, 0, (200, -8)),
-                                             (6000, 384, 1536, 1, None)])
+                                             (31520, 384, 4096, 1, None),
+                                             (12000, 776, 2304, 0, (200, -4))])
 def test_gemm_four_wave(cuda, M, N, K, c32, crow):
-    """Plain K-major GEMMs with N >= 384, K % 128 == 0, K >= 1024 and M >= 2048 take the 4-wave
-    kernel (gemm_w4b_kernel: 128 x 128 or 128 x 96 per wave, 64-deep stages in two LDS-DMA
-    slots): the decoder FFN conv1 shape as a plain GEMM, the encoder's over its padded image
-    (256 x 192 tiles), N = 384, partial row and column tiles on both tile widths (M = 2100 /
-    31000, N = 520 / 776 / 1000: the zero-filled operand tails), the shortest K (1024), both
-    output types, bias + ReLU, and both c_row remaps (gaps inserted every 250 / 300 rows; pad
-    rows dropped).  NaN-filled outputs: rows the remap skips stay NaN, every other row is written.
-    fp32 reference on the same bf16 values, rel 1e-2."""
+    """Plain K-major GEMMs with N >= 384, K % 128 == 0, K >= 2048, M >= 2048 and >= 160 tiles
+    take the 4-wave kernel (gemm_w4b_kernel: 128 x 128 or 128 x 96 per wave, 64-deep stages in
+    two LDS-DMA slots): the decoder FFN conv1 forward shape (256 x 256 tiles), the encoder's
+    over its padded image and the decoder conv1 data gradient's N = 384 (256 x 192 tiles),
+    partial row and column tiles on both tile widths (M = 31000 / 20000 / 12000, N = 1000 / 520
+    / 776: the zero-filled operand tails), both output types, bias + ReLU, and both c_row
+    remaps (gaps inserted every 300 rows; pad rows dropped).  NaN-filled outputs: rows the
+    remap skips stay NaN, every other row is written.  fp32 reference on the same bf16 values,
+    rel 1e-2."""
     from fastspeech2 import ops
     torch.manual_seed(M + N + K)
     A = torch.randn(M, K, device=cuda).to(torch.bfloat16)
