@@ -426,7 +426,7 @@ def main():
         n, ms = ks.get("ffn_conv1_fwd.decoder", (0, float("nan")))
         kflop = 2.0 * (args.batch * Tm) * F * (KW * D)
         achieved = kflop / (ms * 1e-3) / 1e12 if n else None
-        traffic, traffic_src = (pmc_traffic("roofline", "gemm256r_kernel<1, true, 64>")
+        traffic, traffic_src = (pmc_traffic("roofline", "gemm_w4b_kernel<false, 8>")
                                 if not args.scaled else (None, None))
         # second entry: the decoder FFN conv1 weight gradient, the largest GEMM bucket of the
         # step (2 M F 9D per launch like the forward); it runs on the side stream beside the
@@ -454,7 +454,7 @@ def main():
                                    + (", single speaker" if args.single_speaker else ""),
                        "global_batch": args.batch * world, "seq_len": Tm,
                        "valid_mel_frames_per_step": frames_all, "parallelism": f"dp{world}"},
-            "roofline": {"bound": "mfma", "kernel": "decoder FFN conv1 (k=9) implicit-GEMM fwd (gemm256r_kernel<1, true, 64>: 256x256 tiles, full-row LDS-DMA regions, reflect conv in the loader, bias + ReLU in a register-direct epilogue)",
+            "roofline": {"bound": "mfma", "kernel": "decoder FFN conv1 (k=9) fwd: a plain GEMM with overlapping A rows over the reflect-padded token image (gemm_w4b_kernel<false, 8>: 256x256 tiles on 4 waves of 128x128, 64-deep stages through 2 LDS-DMA slots, bias + ReLU + pad-row drop in the epilogue); flop counted on the B*T_mel valid rows, the image copy (fs2_pad_rows) is a separate launch",
                          "achieved": achieved, "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": (achieved / MFMA_BF16_PEAK_TFLOPS) if achieved else None,
                          "traffic": traffic, "traffic_source": traffic_src,
@@ -467,7 +467,7 @@ def main():
             "roofline_conv1_wgrad": {
                 "bound": "mfma", "kernel": "decoder FFN conv1 (k=9) weight gradient: K-major GEMM "
                                            "over channel-major padded dY / X images (conv_mode 6, "
-                                           "gemm_ps_kernel<0, 64, 0, 1>), 3 split-K fp32 slices; "
+                                           "gemm_ps_kernel<0, 64, 0, 1>), split-K fp32 slices; "
                                            "the two image transposes are separate launches",
                 "achieved": wach, "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": (wach / MFMA_BF16_PEAK_TFLOPS) if wach else None,

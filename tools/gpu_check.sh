@@ -20,8 +20,9 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-extractor --no-fp32-leg --no-config2-leg \
   > $O/prof_bench.json 2> $O/prof.err || { echo "rocprof failed"; tail -20 $O/prof.err; exit 1; }
 python $R/tools/rocprof_summary.py stats $O/prof 17 $O/kernel_stats.txt | head -40
-# roofline kernel: the decoder FFN conv1 forward (implicit reflect conv on gemm256r_kernel)
-python $R/tools/rocprof_summary.py kernel $O/prof "gemm256r_kernel<1, true, 64>" 377856 100 | tee $O/roofline_kernel_trace.txt
+# roofline kernel: the decoder FFN conv1 forward (4-wave kernel over the reflect-padded image:
+# 124 x 6 tiles of 256 x 256)
+python $R/tools/rocprof_summary.py kernel $O/prof "gemm_w4b_kernel<false, 8>" 190464 100 | tee $O/roofline_kernel_trace.txt
 # second roofline kernel: the decoder FFN conv1 weight gradient (conv_mode 6 on the persistent
 # kernel: 84 tiles x 2 splits on the 208-CU side-stream budget -> 168 blocks of 512; the encoder's, same grid, runs < 200 us)
 python $R/tools/rocprof_summary.py kernel $O/prof "gemm_ps_kernel<0, 64, 0, 1>" 86016 200 | tee $O/wgrad_kernel_trace.txt
@@ -32,9 +33,9 @@ if [ "$3" == "pmc" ]; then
     timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d $O/pmc_$C -o run -- python $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extractor --no-fp32-leg --no-config2-leg \
       > $O/pmc_$C.log 2>&1 || { echo "pmc $C failed"; tail -20 $O/pmc_$C.log; exit 1; }
   done
-  python $R/tools/rocprof_summary.py traffic $O/pmc_FETCH_SIZE $O/pmc_WRITE_SIZE "gemm256r_kernel<1, true, 64>" 377856 100 $O/roofline_traffic.json
+  python $R/tools/rocprof_summary.py traffic $O/pmc_FETCH_SIZE $O/pmc_WRITE_SIZE "gemm_w4b_kernel<false, 8>" 190464 100 $O/roofline_traffic.json
   python $R/tools/rocprof_summary.py traffic $O/pmc_FETCH_SIZE $O/pmc_WRITE_SIZE "gemm_ps_kernel<0, 64, 0, 1>" 86016 200 $O/wgrad_traffic.json
-  python $R/tools/rocprof_summary.py traffic $O/pmc_FETCH_SIZE $O/pmc_WRITE_SIZE "gemm_ps_kernel<0, 48, 0, 0>" 126976 200 $O/ps_dgrad_traffic.json
+  python $R/tools/rocprof_summary.py traffic $O/pmc_FETCH_SIZE $O/pmc_WRITE_SIZE "gemm_w4b_kernel<true, 6>" 63488 100 $O/dgrad_traffic.json
 fi
 if [ "$4" == "detail" ]; then
   cd $R && timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-extractor --no-fp32-leg --no-config2-leg --detail > $O/detail.json 2> $O/detail.txt || { echo "detail failed"; tail -20 $O/detail.txt; exit 1; }
