@@ -75,6 +75,7 @@ struct GemmP {
   int c_row_t, c_row_pad;  // >0: output row m stored at m + (m / c_row_t) * c_row_pad (ps kernel)
   int max_ctas;            // grid budget of the persistent kernels (blocks), 8..256
   int a_bytes, b_bytes;    // gemm_w4b_kernel: readable byte extents of A and B (zeros past them)
+  int a_kw;                // gemm_w4b_kernel: tap-inner K order of an overlapping-row A (desc a_kw)
 };
 
 __device__ __forceinline__ u32x4 add_bf16x8(u32x4 a, u32x4 b) {
@@ -1942,11 +1943,19 @@ __global__ void __launch_bounds__(W4_NT, 1) gemm_w4b_kernel(GemmP p) {
   rsB[2] = p.b_bytes;
   const int lda8 = (int)p.lda * 16, ldb8 = (int)p.ldb * 16;   // bytes per 8 rows
   const int sa0 = m0 * (int)p.lda * 2, sb0 = n0 * (int)p.ldb * 2;
-  // DMA piece j (0 .. NP-1) of this wave for the stage at K byte offset kb, into slot base dst
-  auto dma = [&](int j, int kb, char* dst) {
+  // A's byte offset of K-stage st: st * 128, or in the tap-inner order (a_kw) the image row
+  // (st % a_kw) further down, channel chunk st / a_kw
+  auto aoff = [&](int st) {
+    if (!p.a_kw) return st * 128;
+    const int q64 = st / p.a_kw;
+    return ((st - q64 * p.a_kw) * (int)p.lda + q64 * 64) * 2;
+  };
+  // DMA piece j (0 .. NP-1) of this wave for the stage at A / B byte offsets ka / kb, into slot
+  // base dst
+  auto dma = [&](int j, int ka, int kb, char* dst) {
     if (j < 8) {
       const int pi = wave * 8 + j;
-      blds16(rsA, voa, sa0 + pi * lda8 + kb, dst + pi * 1024);
+      blds16(rsA, voa, sa0 + pi * lda8 + ka, dst + pi * 1024);
     } else {
       const int pi = wave * NF + j - 8;
       blds16(rsB, vob, sb0 + pi * ldb8 + kb, dst + 256 * 128 + pi * 1024);
@@ -1965,10 +1974,11 @@ __global__ void __launch_bounds__(W4_NT, 1) gemm_w4b_kernel(GemmP p) {
     for (int j = 0; j < NF; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   bf16x8 af[2][8], bfr[2][NF];   // [0]: half 0 of a stage, [1]: half 1
 
+  const int ka1 = aoff(1);
 #pragma unroll
-  for (int j = 0; j < NP; ++j) dma(j, 0, smem);
+  for (int j = 0; j < NP; ++j) dma(j, 0, 0, smem);
 #pragma unroll
-  for (int j = 0; j < NP; ++j) dma(j, 128, smem + STAGE);
+  for (int j = 0; j < NP; ++j) dma(j, ka1, 128, smem + STAGE);
   vm_wait<NP>();   // stage 0 landed (this wave's pieces)
   __builtin_amdgcn_s_barrier();
   {
@@ -1992,13 +2002,13 @@ __global__ void __launch_bounds__(W4_NT, 1) gemm_w4b_kernel(GemmP p) {
     // row: B in rows 0-2, A in rows 2-5); a barrier after row 3 (every wave's B reads of this
     // slot retired: 12 reads issued, NF of them B) releases the slot's B image, whose pieces of
     // stage s+2 go out over rows 4-7
-    const int kb = (s + 2) * 128;
+    const int kb = (s + 2) * 128, ka = aoff(s + 2);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       if (i >= 4 && !(xf & 2)) {
 #pragma unroll
         for (int t = 0; t < NF; ++t)
-          if (t * 4 / NF == i - 4) dma(8 + t, kb, slot);
+          if (t * 4 / NF == i - 4) dma(8 + t, ka, kb, slot);
       }
 #pragma unroll
       for (int j = 0; j < NF; ++j) mfma_acc(acc[i][j], bfr[0][j], af[0][i]);
@@ -2022,7 +2032,7 @@ __global__ void __launch_bounds__(W4_NT, 1) gemm_w4b_kernel(GemmP p) {
     // (s+1, half 0), B first
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      if (!(xf & 2)) dma(i, kb, slot);
+      if (!(xf & 2)) dma(i, ka, kb, slot);
 #pragma unroll
       for (int j = 0; j < NF; ++j) mfma_acc(acc[i][j], bfr[1][j], af[1][i]);
       if (!(xf & 4)) {
@@ -2827,7 +2837,8 @@ int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
       const long b_ext = bk ? (long)(p.N - 1) * p.ldb + p.K : 0;
       const bool w4 = w4_on && ak && bk && p.conv_mode == 0 && batch == 1 && p.split_k <= 1 &&
                       !p.accumulate && !p.gate && !p.residual && !p.row_scale && !p.row_scale_post &&
-                      p.K % 128 == 0 && p.K >= max(256, w4_min_k) && p.N >= 384 && p.M >= 2048 &&
+                      p.K % 128 == 0 && p.K >= (p.a_kw ? 256 : max(256, w4_min_k)) &&
+                      (p.a_kw || (p.N >= 384 && p.M >= 2048)) &&
                       p.nvalid % 4 == 0 && p.ldc % 4 == 0 && p.vec_align &&
                       a_ext * 2 < 0x7fffffffL && b_ext * 2 < 0x7fffffffL &&
                       ((long)p.M + 257) * p.lda * 2 < 0x7fffffffL &&
@@ -2836,7 +2847,8 @@ int launch_gemm(const GemmP& p, int gz, hipStream_t s, int ak, int bk) {
       const int tm4 = (p.M + 255) / 256;
       const int t256 = tm4 * ((p.N + 255) / 256), t192 = tm4 * ((p.N + 191) / 192);
       const bool w192 = (long)((t192 + 255) / 256) * 192 < (long)((t256 + 255) / 256) * 256;
-      if (w4 && (w192 ? t192 : t256) >= w4_min_tiles) {
+      if (p.a_kw && !w4) return FS2_EINVAL;   // the tap-inner order exists on this kernel only
+      if (w4 && ((w192 ? t192 : t256) >= w4_min_tiles || p.a_kw)) {
         GemmP q = p;
         q.tiles_m = tm4;
         q.tiles_n = w192 ? (p.N + 191) / 192 : (p.N + 255) / 256;
@@ -3127,6 +3139,11 @@ extern "C" int fs2_gemm(const fs2_gemm_desc* d, void* stream) {
   p.c_row_t = d->c_row_t > 0 ? d->c_row_t : 0;
   p.c_row_pad = p.c_row_t ? d->c_row_pad : 0;
   p.max_ctas = d->max_ctas > 0 && d->max_ctas < 256 ? max(8, d->max_ctas / 8 * 8) : 256;
+  p.a_kw = d->a_kw > 0 ? d->a_kw : 0;
+  if (p.a_kw && (d->dtype != FS2_BF16 || !d->a_kmajor || !d->b_kmajor || d->conv_mode ||
+                 batch > 1 || p.split_k > 1 || p.c_row_t || p.lda % 64 ||
+                 (long)p.a_kw * p.lda != p.K))
+    return FS2_EINVAL;
   if (p.c_row_t && (d->dtype != FS2_BF16 || !d->a_kmajor || !d->b_kmajor ||
                     p.conv_mode || batch > 1 || p.split_k > 1 || p.accumulate || p.c_conv_kw))
     return FS2_EINVAL;

@@ -86,7 +86,15 @@ __global__ void weight_prep_kernel(const float* W, int O, int C, int KW, int okc
       const int c = (int)(i / ldb), col = (int)(i - (long)c * ldb);
       float v = 0.f;
       if (col < KW * O) {
-        const int jb = col / O, o = col - jb * O;
+        int jb, o;
+        if (okc & 4) {   // tap-inner 64-channel chunks (wb_col)
+          const int ch = col / (KW * 64), r = col - ch * (KW * 64);
+          jb = r >> 6;
+          o = ch * 64 + (r & 63);
+        } else {
+          jb = col / O;
+          o = col - jb * O;
+        }
         const int j = (okc & 2) ? KW - 1 - jb : jb;   // bit 1: Wb's taps reversed
         v = (okc & 1) ? W[((long)o * KW + j) * C + c] : W[((long)o * C + c) * KW + j];
       }
@@ -98,6 +106,13 @@ __global__ void weight_prep_kernel(const float* W, int O, int C, int KW, int okc
 // tap index of Wb (w_okc bit 1: taps reversed)
 __device__ __forceinline__ int wb_tap(const fs2_wprep_desc& d, int j) {
   return (d.w_okc & 2) ? d.KW - 1 - j : j;
+}
+// Wb column of (tap j, output channel o): j*O + o, or with w_okc bit 2 (O % 64 == 0) the
+// tap-inner order of 64-channel chunks, (o / 64)*(KW*64) + j*64 + o % 64 -- the K order in which
+// the padded-dY data gradient reads its image rows one tap apart in consecutive 64-deep stages
+// (fs2_gemm_desc.a_kw)
+__device__ __forceinline__ long wb_col(int okc, int KW, int O, int j, int o) {
+  return (okc & 4) ? (long)(o >> 6) * (KW * 64) + j * 64 + (o & 63) : (long)j * O + o;
 }
 
 // one block per 64x64 tile (o, k = j*C + c) of one weight's forward image; the weight is found
@@ -149,7 +164,7 @@ __global__ void __launch_bounds__(256) weight_prep_batched_kernel(const fs2_wpre
     const int kl = i >> 6, ol = i & 63, o = o0 + ol, k = k0 + kl;
     if (o >= d.O || k >= KC) continue;
     const int j = wb_tap(d, jcs[kl] >> 16), c = jcs[kl] & 0xffff;
-    Wb[(long)c * d.ldb + (long)j * d.O + o] = from_f<T>(tile[ol][kl]);
+    Wb[(long)c * d.ldb + wb_col(d.w_okc, d.KW, d.O, j, o)] = from_f<T>(tile[ol][kl]);
   }
 }
 
@@ -248,7 +263,7 @@ __global__ void __launch_bounds__(256) adamw_prep_tiles_kernel(const fs2_wprep_d
             ((unsigned)__builtin_bit_cast(unsigned short, (bf16)tile[ol + 1][kl]) << 16);
       h.y = (unsigned)__builtin_bit_cast(unsigned short, (bf16)tile[ol + 2][kl]) |
             ((unsigned)__builtin_bit_cast(unsigned short, (bf16)tile[ol + 3][kl]) << 16);
-      *(uint2*)(Wb + (long)c * d.ldb + (long)j * d.O + o) = h;
+      *(uint2*)(Wb + (long)c * d.ldb + wb_col(d.w_okc, d.KW, d.O, j, o)) = h;
     }
     return;
   }
@@ -273,7 +288,7 @@ __global__ void __launch_bounds__(256) adamw_prep_tiles_kernel(const fs2_wprep_d
     const int kl = i >> 6, ol = i & 63, o = o0 + ol, k = k0 + kl;
     if (o >= d.O || k >= KC) continue;
     const int j = wb_tap(d, jcs[kl] >> 16), c = jcs[kl] & 0xffff;
-    Wb[(long)c * d.ldb + (long)j * d.O + o] = from_f<T>(tile[ol][kl]);
+    Wb[(long)c * d.ldb + wb_col(d.w_okc, d.KW, d.O, j, o)] = from_f<T>(tile[ol][kl]);
   }
 }
 

@@ -64,6 +64,7 @@ class GemmDesc(ctypes.Structure):
         ("sB2", ctypes.c_int64), ("sC1", ctypes.c_int64), ("sC2", ctypes.c_int64),
         ("sR1", ctypes.c_int64), ("sR2", ctypes.c_int64), ("conv_dil", ctypes.c_int),
         ("c_row_t", ctypes.c_int), ("c_row_pad", ctypes.c_int), ("max_ctas", ctypes.c_int),
+        ("a_kw", ctypes.c_int),
     ]
 
 

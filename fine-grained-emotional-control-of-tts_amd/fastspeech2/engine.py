@@ -78,6 +78,8 @@ _KM_WGRAD = N.exp_int("FS2_KM_WGRAD", 1)
 _PAD_DGRAD = N.exp_int("FS2_PAD_DGRAD", 1)
 # FFN conv1 forward over a reflect-padded X image (engine._pad_fwd)
 _PAD_FWD = N.exp_int("FS2_PAD_FWD", 2)
+# decoder FFN conv1 data gradient in the tap-inner K order (engine._tap_inner)
+_TAP_INNER = N.exp_int("FS2_TAP_INNER", 1)
 # serial mode for per-call-site timing (bench.py --detail runs with the experiments library)
 _NO_SIDE = N.exp_flag("FS2_NO_SIDE_STREAM")
 _NO_AUX = N.exp_flag("FS2_NO_AUX_STREAM")
@@ -334,8 +336,11 @@ class FS2Engine:
                 Wf, Wb = self.w[name]
                 W = self.params[name + ".weight" if name == self.PRED1 else name]
                 # conv weights are [O][KW][C] in the flat buffer (model._kw_major); the FFN
-                # conv1 data-gradient image has its taps reversed on the padded-dY path
-                okc = int(KW > 1) | (2 if self._pad_dgrad(name) else 0)
+                # conv1 data-gradient image has its taps reversed on the padded-dY path, and
+                # its columns in tap-inner 64-channel chunks where that GEMM reads the image
+                # in that order (_tap_inner)
+                okc = int(KW > 1) | (2 if self._pad_dgrad(name) else 0) | \
+                    (4 if self._tap_inner(name) else 0)
                 entries.append((W, O, C, KW, okc, Wf, ldf, Wb, ldb))
                 self._wentries[name] = entries[-1]
             self._wtable = ops.weight_prep_table(entries)
@@ -489,6 +494,17 @@ class FS2Engine:
         O, C, KW = self._wspecs[wname]
         return KW > 1 and self._km_ok(O, C, KW, KW, None)
 
+    def _tap_inner(self, wname):
+        """the decoder FFN conv1 data gradient over the padded dY image in the tap-inner K order
+        (fs2_gemm_desc.a_kw, Wb built with w_okc bit 2): consecutive 64-deep K-stages read image
+        rows one tap apart, so the 96 MB image is fetched from HBM about once instead of once
+        per tap (995 MB per launch in the natural order, profiles/r05e_dgrad_traffic.json).
+        Always the 4-wave kernel, unsplit; the encoder's (M = 6656) keeps its split-K path."""
+        if not (_TAP_INNER and self._pad_dgrad(wname) and wname.startswith("decoder.")):
+            return False
+        O, C, KW = self._wspecs[wname]
+        return O % 64 == 0 and (KW * O) % 128 == 0
+
     def _pad_dgrad_fits(self, wname, B, T):
         """the padded data gradient's GEMM within the persistent kernel's 32-bit offsets"""
         O, C, KW = self._wspecs[wname]
@@ -540,14 +556,17 @@ class FS2Engine:
         P = (KW - 1) // 2
         B = M // T
         Mp = B * (T + 2 * P)
-        split = dgrad_split(Mp, C, KW * O, self.dt)
+        ti = isinstance(dY, tuple) and self._tap_inner(wname)
+        split = 1 if ti else dgrad_split(Mp, C, KW * O, self.dt)
         Xpad = torch.empty(split, Mp, C, dtype=torch.float32, device=self.dev)
         if isinstance(dY, tuple):
             # padded dY image (_dy_image): row m of the padded domain reads image rows
-            # m .. m + 2P, i.e. A(m, k) = image[m * O + k] against the tap-reversed Wb
+            # m .. m + 2P, i.e. A(m, k) = image[m * O + k] against the tap-reversed Wb (in the
+            # tap-inner order: k = (64-channel chunk, tap, channel), fs2_gemm_desc.a_kw)
             img = dY[0]
             ops.gemm(Mp, C, KW * O, img, O, Wb, KW * O, Xpad, C, dt=self.dt, c_fp32=1,
-                     split_k=split, split_stride=Mp * C if split > 1 else 0)
+                     split_k=split, split_stride=Mp * C if split > 1 else 0,
+                     a_kw=KW if ti else 0)
         else:
             ops.gemm(Mp, C, KW * O, dY, lddy, Wb, KW * O, Xpad, C, dt=self.dt, conv=(4, T, KW, O),
                      c_fp32=1, split_k=split, split_stride=Mp * C if split > 1 else 0)

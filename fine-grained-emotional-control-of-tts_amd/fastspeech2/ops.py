@@ -70,9 +70,11 @@ if _TRACE is not None:
 def gemm(M, N_, K, A, lda, B, ldb, C, ldc, *, dt, a_kmajor=1, b_kmajor=1, conv=None, c_fp32=0,
          c_conv_kw=0, bias=None, relu=0, gate=None, ldg=0, row_scale=None, residual=None, ldr=0,
          row_scale_post=None, accumulate=0, split_k=1, split_stride=0, kvalid=0, mvalid=0,
-         nvalid=0, batch=1, batch_div=1, strides=None, conv_dil=1, c_row=None, max_ctas=0):
+         nvalid=0, batch=1, batch_div=1, strides=None, conv_dil=1, c_row=None, max_ctas=0,
+         a_kw=0):
     d = N.GemmDesc()
     d.conv_dil = conv_dil
+    d.a_kw = a_kw             # tap-inner K order of an overlapping-row A (fs2_gemm_desc.a_kw)
     d.max_ctas = max_ctas     # persistent-kernel grid budget (0: one block per CU)
     if c_row is not None:     # (T, pad): output row m stored at m + (m // T) * pad
         d.c_row_t, d.c_row_pad = c_row

@@ -93,6 +93,13 @@ typedef struct fs2_gemm_desc {
    * (model.py:279-441 backward) beside the data-gradient chain -- leaves 256 - max_ctas CUs to
    * the other stream's kernels; 8..255, rounded down to 8.  Results do not depend on it.     */
   int max_ctas;
+  /* a_kw > 0: tap-inner K order for a plain K-major A whose rows overlap (the conv1 data
+   * gradient over the padded dY image, lda = the image's channel count Ci, K = a_kw * Ci,
+   * Ci % 64 == 0): k = (chunk q, tap j, i) -> A(m, k) = A[(m + j)*lda + 64 q + i], i < 64 --
+   * consecutive 64-deep K-stages read image rows one tap apart, so each row is fetched from HBM
+   * about once instead of once per tap.  B must be in the same order (fs2_weight_prep w_okc
+   * bit 2).  bf16, no split / batch / conv / c_row; always the 4-wave kernel.               */
+  int a_kw;
 } fs2_gemm_desc;
 
 int fs2_gemm(const fs2_gemm_desc* d, void* stream);
@@ -310,7 +317,8 @@ int fs2_adamw(float* param, const float* grad, float* exp_avg, float* exp_avg_sq
  * [O][C][KW] (w_okc bit 0 clear) or [O][KW][C] (bit 0 set, the flat-buffer layout of conv
  * weights).  w_okc bit 1: Wb's taps reversed, Wb[C][KW-1-j][O] -- the order in which the conv
  * data gradient over a zero-padded token-major dY image is a plain K-major GEMM whose A rows
- * overlap (A(m, k) = image[m*O + k], lda = O). */
+ * overlap (A(m, k) = image[m*O + k], lda = O).  w_okc bit 2 (O % 64 == 0): Wb's columns in
+ * tap-inner 64-channel chunks, column (o/64)*KW*64 + j*64 + o%64 (fs2_gemm_desc.a_kw). */
 int fs2_weight_prep(const float* W, int O, int C, int KW, int w_okc, void* Wf, int ldf, void* Wb,
                     int ldb, int dtype, void* stream);
 

@@ -1003,15 +1003,42 @@ def test_weight_prep_reversed_taps(cuda):
     assert torch.equal(Wb, ref_b)
 
 
+@pytest.mark.parametrize("O,C,KW", [(1536, 384, 9), (192, 72, 5), (128, 40, 3)])
+def test_weight_prep_tap_inner(cuda, O, C, KW):
+    """w_okc bit 2: Wb's columns in tap-inner 64-channel chunks, (o/64)*KW*64 + j*64 + o%64
+    (with bit 1: taps reversed), in fs2_weight_prep_batched, fs2_weight_prep and the fused AdamW
+    image pass at a zero step -- exactly the bf16 rounding of the permuted image."""
+    from fastspeech2 import ops
+    torch.manual_seed(O + KW)
+    W = torch.randn(O, KW, C, device=cuda)
+    ldf = ops.round_up(KW * C, 8)
+    nat = W.flip(1).permute(2, 1, 0)                      # [C][j][O], taps reversed
+    ref_b = nat.reshape(C, KW, O // 64, 64).permute(0, 2, 1, 3).reshape(C, KW * O)
+    ref_b = ref_b.to(torch.bfloat16)
+    Wf = torch.empty(O, ldf, device=cuda, dtype=torch.bfloat16)
+    Wb = torch.full((C, KW * O), float("nan"), device=cuda).to(torch.bfloat16)
+    table = ops.weight_prep_table([(W, O, C, KW, 7, Wf, ldf, Wb, KW * O)])
+    ops.weight_prep_batched(*table, dt=1)
+    torch.cuda.synchronize()
+    assert torch.equal(Wb, ref_b)
+    Wb.fill_(float("nan"))
+    ops.weight_prep(W, O, C, KW, Wf, ldf, Wb, KW * O, dt=1, w_okc=7)
+    torch.cuda.synchronize()
+    assert torch.equal(Wb, ref_b)
+
+
 @pytest.mark.parametrize("B,T,O,C,KW", [(32, 977, 1536, 384, 9), (3, 37, 256, 128, 9),
-                                         (2, 50, 192, 256, 5)])
+                                         (2, 50, 192, 256, 5), (4, 120, 128, 384, 3)])
 def test_conv_dgrad_padded_image(cuda, B, T, O, C, KW):
     """The FFN conv1 data gradient over a zero-padded token-major dY image: (1) a gated GEMM
     writes its rows into the image's data rows (fs2_gemm c_row = (T, 2P)), leaving the zero
     pad rows untouched; (2) the plain K-major GEMM over the image with overlapping A rows
     (lda = O) against the tap-reversed Wb equals the shift-conv GEMM (conv_mode 4) over
     token-major dY with the natural Wb -- the same products in another K order (fp32 rel
-    1e-5).  Decoder shape, a ragged small one, a k = 5 one."""
+    1e-5); (3) so does the tap-inner K order (a_kw, 64-channel chunks outer, taps inner, Wb
+    built with w_okc bit 2) on the 4-wave kernel, where K % 128 == 0.  Decoder shape, a ragged
+    small one (one partial row tile), a k = 5 one (K % 128 != 0: natural order only), a k = 3
+    one (two chunks of three taps)."""
     from fastspeech2 import ops
     torch.manual_seed(B * T + KW)
     P = (KW - 1) // 2
@@ -1051,6 +1078,15 @@ def test_conv_dgrad_padded_image(cuda, B, T, O, C, KW):
     torch.cuda.synchronize()
     assert torch.isfinite(X0).all()
     assert rel(X0, X4) < 1e-5
+    # (3) the tap-inner K order (fs2_gemm_desc.a_kw, Wb with w_okc bit 2; the 4-wave kernel)
+    if O % 64 == 0 and (KW * O) % 128 == 0:
+        Wt = torch.empty(C, KW * O, device=cuda, dtype=bf)
+        ops.weight_prep(Wm, O, C, KW, Wf, ldf, Wt, KW * O, dt=1, w_okc=7)
+        Xt = torch.full((Mp, C), float("nan"), device=cuda)
+        ops.gemm(Mp, C, KW * O, img, O, Wt, KW * O, Xt, C, dt=1, c_fp32=1, a_kw=KW)
+        torch.cuda.synchronize()
+        assert torch.isfinite(Xt).all()
+        assert rel(Xt, X4) < 1e-5
 
 
 @pytest.mark.parametrize("B,T,C,O,KW", [(32, 977, 384, 1536, 9), (32, 200, 384, 1536, 9),
