@@ -3141,7 +3141,7 @@ extern "C" int fs2_gemm(const fs2_gemm_desc* d, void* stream) {
   p.max_ctas = d->max_ctas > 0 && d->max_ctas < 256 ? max(8, d->max_ctas / 8 * 8) : 256;
   p.a_kw = d->a_kw > 0 ? d->a_kw : 0;
   if (p.a_kw && (d->dtype != FS2_BF16 || !d->a_kmajor || !d->b_kmajor || d->conv_mode ||
-                 batch > 1 || p.split_k > 1 || p.c_row_t || p.lda % 64 ||
+                 batch > 1 || p.split_k > 1 || p.lda % 64 ||
                  (long)p.a_kw * p.lda != p.K))
     return FS2_EINVAL;
   if (p.c_row_t && (d->dtype != FS2_BF16 || !d->a_kmajor || !d->b_kmajor ||

@@ -75,8 +75,16 @@ __global__ void weight_prep_kernel(const float* W, int O, int C, int KW, int okc
     const int o = (int)(i / ldf), col = (int)(i - (long)o * ldf);
     float v = 0.f;
     if (col < KW * C) {
-      const int j = col / C, c = col - j * C;
-      v = (okc & 1) ? W[(long)o * KW * C + col] : W[((long)o * C + c) * KW + j];
+      int j, c;
+      if (okc & 8) {   // tap-inner 64-channel chunks (wf_col)
+        const int ch = col / (KW * 64), r = col - ch * (KW * 64);
+        j = r >> 6;
+        c = ch * 64 + (r & 63);
+      } else {
+        j = col / C;
+        c = col - j * C;
+      }
+      v = (okc & 1) ? W[((long)o * KW + j) * C + c] : W[((long)o * C + c) * KW + j];
     }
     Wf[i] = from_f<T>(v);
   }
@@ -113,6 +121,11 @@ __device__ __forceinline__ int wb_tap(const fs2_wprep_desc& d, int j) {
 // (fs2_gemm_desc.a_kw)
 __device__ __forceinline__ long wb_col(int okc, int KW, int O, int j, int o) {
   return (okc & 4) ? (long)(o >> 6) * (KW * 64) + j * 64 + (o & 63) : (long)j * O + o;
+}
+// Wf column of (tap j, input channel c): k = j*C + c, or with w_okc bit 3 (C % 64 == 0) the same
+// tap-inner chunk order (the padded-image conv forward, fs2_gemm_desc.a_kw)
+__device__ __forceinline__ int wf_col(int okc, int KW, int k, int j, int c) {
+  return (okc & 8) ? (c >> 6) * (KW * 64) + j * 64 + (c & 63) : k;
 }
 
 // one block per 64x64 tile (o, k = j*C + c) of one weight's forward image; the weight is found
@@ -153,7 +166,8 @@ __global__ void __launch_bounds__(256) weight_prep_batched_kernel(const fs2_wpre
       const int j = jcs[kl] >> 16, c = jcs[kl] & 0xffff;
       v = (d.w_okc & 1) ? d.W[(long)o * KC + k] : d.W[((long)o * d.C + c) * d.KW + j];
     }
-    Wf[(long)o * d.ldf + k] = from_f<T>(v);
+    const int kf = k < KC ? wf_col(d.w_okc, d.KW, k, jcs[kl] >> 16, jcs[kl] & 0xffff) : k;
+    Wf[(long)o * d.ldf + kf] = from_f<T>(v);
     tile[ol][kl] = v;
   }
   if (!d.Wb) return;
@@ -247,7 +261,8 @@ __global__ void __launch_bounds__(256) adamw_prep_tiles_kernel(const fs2_wprep_d
             ((unsigned)__builtin_bit_cast(unsigned short, (bf16)w[1]) << 16);
       h.y = (unsigned)__builtin_bit_cast(unsigned short, (bf16)w[2]) |
             ((unsigned)__builtin_bit_cast(unsigned short, (bf16)w[3]) << 16);
-      *(uint2*)(Wf + (long)o * d.ldf + k) = h;
+      const int kf = k < KC ? wf_col(d.w_okc, d.KW, k, jcs[kl] >> 16, jcs[kl] & 0xffff) : k;
+      *(uint2*)(Wf + (long)o * d.ldf + kf) = h;
 #pragma unroll
       for (int q = 0; q < 4; ++q) tile[ol][kl + q] = w[q];
     }
@@ -279,7 +294,8 @@ __global__ void __launch_bounds__(256) adamw_prep_tiles_kernel(const fs2_wprep_d
       pb[e] = pi; mb[e] = mi; vb[e] = vi;
       v = pi;
     }
-    Wf[(long)o * d.ldf + k] = from_f<T>(v);
+    const int kf = k < KC ? wf_col(d.w_okc, d.KW, k, jcs[kl] >> 16, jcs[kl] & 0xffff) : k;
+    Wf[(long)o * d.ldf + kf] = from_f<T>(v);
     tile[ol][kl] = v;
   }
   if (!d.Wb) return;

@@ -78,8 +78,11 @@ _KM_WGRAD = N.exp_int("FS2_KM_WGRAD", 1)
 _PAD_DGRAD = N.exp_int("FS2_PAD_DGRAD", 1)
 # FFN conv1 forward over a reflect-padded X image (engine._pad_fwd)
 _PAD_FWD = N.exp_int("FS2_PAD_FWD", 2)
-# decoder FFN conv1 data gradient in the tap-inner K order (engine._tap_inner)
+# decoder FFN conv1 data gradient in the tap-inner K order (engine._tap_inner); the FFN conv1
+# forward in that order (engine._tap_inner_fwd): off -- 316-318 vs 314 us for the decoder's in
+# the step, step 17.42 vs 17.37 ms (experiments library, 2 x 2 interleaved)
 _TAP_INNER = N.exp_int("FS2_TAP_INNER", 1)
+_TAP_INNER_FWD = N.exp_int("FS2_TAP_INNER_FWD", 0)
 # serial mode for per-call-site timing (bench.py --detail runs with the experiments library)
 _NO_SIDE = N.exp_flag("FS2_NO_SIDE_STREAM")
 _NO_AUX = N.exp_flag("FS2_NO_AUX_STREAM")
@@ -340,7 +343,8 @@ class FS2Engine:
                 # its columns in tap-inner 64-channel chunks where that GEMM reads the image
                 # in that order (_tap_inner)
                 okc = int(KW > 1) | (2 if self._pad_dgrad(name) else 0) | \
-                    (4 if self._tap_inner(name) else 0)
+                    (4 if self._tap_inner(name) else 0) | \
+                    (8 if self._tap_inner_fwd(name) else 0)
                 entries.append((W, O, C, KW, okc, Wf, ldf, Wb, ldb))
                 self._wentries[name] = entries[-1]
             self._wtable = ops.weight_prep_table(entries)
@@ -444,14 +448,20 @@ class FS2Engine:
         tag = self._dtag("fwd", wname, T)
         if tag:
             self._tic(tag)
+        ti = self._tap_inner_fwd(wname)
         if isinstance(X, tuple):
             # reflect-padded X image (_pad_fwd): the conv over the padded domain is a plain
-            # K-major GEMM with overlapping rows, A(m, k=(j,c)) = image[m*C + k]; the pad rows'
+            # K-major GEMM with overlapping rows, A(m, k=(j,c)) = image[m*C + k] (in the
+            # tap-inner order with a Wf built that way, fs2_gemm_desc.a_kw); the pad rows'
             # results are dropped by the epilogue (c_row = (T, -2P))
             P = (KW - 1) // 2
             Mp = (M // T) * (T + 2 * P)
-            ops.gemm(Mp, O, K, X[0], C, Wf, K, out, ldo, dt=self.dt, c_row=(T, -2 * P), **epi)
+            ops.gemm(Mp, O, K, X[0], C, Wf, K, out, ldo, dt=self.dt, c_row=(T, -2 * P),
+                     a_kw=KW if ti else 0, **epi)
         else:
+            if ti:
+                raise ValueError(f"{wname}: its forward image is in the tap-inner order of the "
+                                 "padded-image path, which this batch cannot take")
             ops.gemm(M, O, K, X, ldx, Wf, K, out, ldo, dt=self.dt, conv=conv, **epi)
         if tag:
             self._toc(tag)
@@ -469,6 +479,8 @@ class FS2Engine:
         if _PAD_FWD == 1 and not wname.startswith("encoder."):
             return False
         P = (KW - 1) // 2
+        if self._tap_inner_fwd(wname):   # the 4-wave kernel: 32-bit offsets to 2.8 M rows
+            return P < T
         return (self.dt == 1 and _PAD_FWD and KW > 1 and C % 64 == 0 and P < T and
                 self.w[wname][0].shape[1] == KW * C and
                 ps_plain_ok((M // T) * (T + 2 * P), C, O, KW * C, M, O, 2))
@@ -504,6 +516,19 @@ class FS2Engine:
             return False
         O, C, KW = self._wspecs[wname]
         return O % 64 == 0 and (KW * O) % 128 == 0
+
+    def _tap_inner_fwd(self, wname):
+        """the FFN conv1 forward over the reflect-padded X image in the tap-inner K order (Wf
+        built with w_okc bit 3), both stacks: the image's rows are fetched about once instead of
+        once per tap.  Needs the padded path on every batch (_pad_fwd's conditions other than
+        P < T, which the reference's reflect padding requires anyway)."""
+        if not (_TAP_INNER_FWD and self.dt == 1 and _PAD_FWD and ".pos_ffn.0." in wname):
+            return False
+        if _PAD_FWD == 1 and not wname.startswith("encoder."):
+            return False
+        O, C, KW = self._wspecs[wname]
+        return KW > 1 and C % 64 == 0 and (KW * C) % 128 == 0 and \
+            self.w[wname][0].shape[1] == KW * C
 
     def _pad_dgrad_fits(self, wname, B, T):
         """the padded data gradient's GEMM within the persistent kernel's 32-bit offsets"""

@@ -98,7 +98,8 @@ typedef struct fs2_gemm_desc {
    * Ci % 64 == 0): k = (chunk q, tap j, i) -> A(m, k) = A[(m + j)*lda + 64 q + i], i < 64 --
    * consecutive 64-deep K-stages read image rows one tap apart, so each row is fetched from HBM
    * about once instead of once per tap.  B must be in the same order (fs2_weight_prep w_okc
-   * bit 2).  bf16, no split / batch / conv / c_row; always the 4-wave kernel.               */
+   * bit 2; the forward's Wf: bit 3).  bf16, no split / batch / conv; always the 4-wave
+   * kernel.                                                                                 */
   int a_kw;
 } fs2_gemm_desc;
 
@@ -318,7 +319,8 @@ int fs2_adamw(float* param, const float* grad, float* exp_avg, float* exp_avg_sq
  * weights).  w_okc bit 1: Wb's taps reversed, Wb[C][KW-1-j][O] -- the order in which the conv
  * data gradient over a zero-padded token-major dY image is a plain K-major GEMM whose A rows
  * overlap (A(m, k) = image[m*O + k], lda = O).  w_okc bit 2 (O % 64 == 0): Wb's columns in
- * tap-inner 64-channel chunks, column (o/64)*KW*64 + j*64 + o%64 (fs2_gemm_desc.a_kw). */
+ * tap-inner 64-channel chunks, column (o/64)*KW*64 + j*64 + o%64 (fs2_gemm_desc.a_kw); bit 3
+ * (C % 64 == 0, ldf == KW*C): Wf's columns the same way, (c/64)*KW*64 + j*64 + c%64. */
 int fs2_weight_prep(const float* W, int O, int C, int KW, int w_okc, void* Wf, int ldf, void* Wb,
                     int ldb, int dtype, void* stream);
 

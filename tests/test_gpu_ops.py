@@ -1003,28 +1003,37 @@ def test_weight_prep_reversed_taps(cuda):
     assert torch.equal(Wb, ref_b)
 
 
-@pytest.mark.parametrize("O,C,KW", [(1536, 384, 9), (192, 72, 5), (128, 40, 3)])
+@pytest.mark.parametrize("O,C,KW", [(1536, 384, 9), (192, 72, 5), (128, 40, 3), (256, 128, 9)])
 def test_weight_prep_tap_inner(cuda, O, C, KW):
     """w_okc bit 2: Wb's columns in tap-inner 64-channel chunks, (o/64)*KW*64 + j*64 + o%64
-    (with bit 1: taps reversed), in fs2_weight_prep_batched, fs2_weight_prep and the fused AdamW
-    image pass at a zero step -- exactly the bf16 rounding of the permuted image."""
+    (with bit 1: taps reversed); bit 3 (C % 64 == 0): Wf's columns the same way over c -- in
+    fs2_weight_prep_batched and fs2_weight_prep, exactly the bf16 rounding of the permuted
+    images."""
     from fastspeech2 import ops
     torch.manual_seed(O + KW)
     W = torch.randn(O, KW, C, device=cuda)
     ldf = ops.round_up(KW * C, 8)
+    okc = 7 | (8 if C % 64 == 0 else 0)
     nat = W.flip(1).permute(2, 1, 0)                      # [C][j][O], taps reversed
     ref_b = nat.reshape(C, KW, O // 64, 64).permute(0, 2, 1, 3).reshape(C, KW * O)
     ref_b = ref_b.to(torch.bfloat16)
-    Wf = torch.empty(O, ldf, device=cuda, dtype=torch.bfloat16)
+    if okc & 8:
+        ref_f = W.view(O, KW, C // 64, 64).permute(0, 2, 1, 3).reshape(O, KW * C)
+    else:
+        ref_f = torch.zeros(O, ldf, device=cuda)
+        ref_f[:, :KW * C] = W.reshape(O, KW * C)
+    ref_f = ref_f.to(torch.bfloat16)
+    Wf = torch.full((O, ldf), float("nan"), device=cuda).to(torch.bfloat16)
     Wb = torch.full((C, KW * O), float("nan"), device=cuda).to(torch.bfloat16)
-    table = ops.weight_prep_table([(W, O, C, KW, 7, Wf, ldf, Wb, KW * O)])
+    table = ops.weight_prep_table([(W, O, C, KW, okc, Wf, ldf, Wb, KW * O)])
     ops.weight_prep_batched(*table, dt=1)
     torch.cuda.synchronize()
-    assert torch.equal(Wb, ref_b)
+    assert torch.equal(Wb, ref_b) and torch.equal(Wf, ref_f)
     Wb.fill_(float("nan"))
-    ops.weight_prep(W, O, C, KW, Wf, ldf, Wb, KW * O, dt=1, w_okc=7)
+    Wf.fill_(float("nan"))
+    ops.weight_prep(W, O, C, KW, Wf, ldf, Wb, KW * O, dt=1, w_okc=okc)
     torch.cuda.synchronize()
-    assert torch.equal(Wb, ref_b)
+    assert torch.equal(Wb, ref_b) and torch.equal(Wf, ref_f)
 
 
 @pytest.mark.parametrize("B,T,O,C,KW", [(32, 977, 1536, 384, 9), (3, 37, 256, 128, 9),
@@ -1096,8 +1105,8 @@ def test_conv_fwd_padded_image(cuda, B, T, C, O, KW):
     reflect-padded token-major image (checked exactly against torch's reflect pad), then a
     plain K-major GEMM with overlapping rows (lda = C) drops each utterance's 2P pad rows in
     its epilogue (c_row = (T, -2P)) -- equal to the implicit reflect conv (conv_mode 1) with
-    bias + ReLU (bf16 outputs, rel 1e-2: two kernels, one sum order).  Every token row is
-    written (NaN-filled output)."""
+    bias + ReLU (bf16 outputs, rel 1e-2: two kernels, one sum order), and so does the
+    tap-inner K order where C % 64 == 0.  Every token row is written (NaN-filled output)."""
     from fastspeech2 import ops
     torch.manual_seed(B + T + KW)
     P = (KW - 1) // 2
@@ -1120,6 +1129,16 @@ def test_conv_fwd_padded_image(cuda, B, T, C, O, KW):
     torch.cuda.synchronize()
     assert torch.isfinite(Y0.float()).all()
     assert rel(Y0, Y1) < 1e-2
+    # the tap-inner K order (fs2_gemm_desc.a_kw; W's columns in 64-channel chunks, as
+    # fs2_weight_prep w_okc bit 3 builds them) on the 4-wave kernel
+    if C % 64 == 0 and (KW * C) % 128 == 0:
+        Wt = W.view(O, KW, C // 64, 64).permute(0, 2, 1, 3).reshape(O, KW * C).contiguous()
+        Y2 = torch.full((M, O), float("nan"), device=cuda, dtype=bf)
+        ops.gemm(B * L, O, KW * C, img, C, Wt, KW * C, Y2, O, dt=1, bias=bias, relu=1,
+                 c_row=(T, -2 * P), a_kw=KW)
+        torch.cuda.synchronize()
+        assert torch.isfinite(Y2.float()).all()
+        assert rel(Y2, Y1) < 1e-2
 
 
 @pytest.mark.parametrize("dt,code", [(torch.float32, 0), (torch.bfloat16, 1)])

@@ -10,7 +10,7 @@ for r in $(seq 1 $R); do
   for e in "$@"; do
     V=(); [ "$e" != "-" ] && V=($e)
     env FS2_HIP_LIB=$EXP "${V[@]}" timeout -k 10 200 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-extractor --no-fp32-leg --no-config2-leg > gpurun_out/ab/b.json 2> gpurun_out/ab/b.err || { tail -20 gpurun_out/ab/b.err; exit 1; }
-    ms=$(python -c "import json; print(json.load(open('gpurun_out/ab/b.json'))['ms_per_step'])")
+    ms=$(python -c "import json; d=json.load(open('gpurun_out/ab/b.json')); print(' '.join('%s=%.1f' % (k.split('.')[0][9:] + k.split('.')[1][:3], v * 1e3) for k, v in d.get('kernel_ms', {}).items()), d['ms_per_step'])")
     echo "$r arm$i [$e] $ms" | tee -a gpurun_out/ab/log.txt
     i=$((i+1))
   done
