@@ -596,14 +596,14 @@ __global__ void __launch_bounds__(256) ln_bwd_rows_kernel(LnBwdP p, float* part,
   }
 }
 
-// out_k[d] (+)= sum_b part[b][k*D + d] for k < npart: 16 columns x 64 row-slices per block
-// (1024 threads), fixed-order combine through LDS (deterministic).  With 16 row-slices each
+// out_k[d] (+)= sum_b part[b][k*D + d] for k < npart: 16 columns x SL row-slices per block
+// (16 SL threads), fixed-order combine through LDS (deterministic).  With 16 row-slices each
 // thread walked ~61 partial rows of a decoder LayerNorm backward in sequence: 7.6 us per call,
 // 62 calls per step.
-__global__ void __launch_bounds__(1024) reduce_parts_kernel(const float* part, int nb, int D,
-                                                           int npart, float* o0, float* o1,
-                                                           float* o2, int accumulate) {
-  constexpr int SL = 64;
+template <int SL>
+__global__ void __launch_bounds__(SL * 16) reduce_parts_kernel(const float* part, int nb, int D,
+                                                              int npart, float* o0, float* o1,
+                                                              float* o2, int accumulate) {
   __shared__ float red[SL][17];
   const int c = threadIdx.x & 15, sl = threadIdx.x >> 4;
   const int ncols = npart * D;
@@ -625,6 +625,22 @@ __global__ void __launch_bounds__(1024) reduce_parts_kernel(const float* part, i
     float* o = k == 0 ? o0 : (k == 1 ? o1 : o2);
     o[d] = accumulate ? o[d] + t : t;
   }
+}
+
+// 16 row-slices (256 threads): a block that fits beside the side stream's GEMM blocks on a
+// busy CU, each thread walking 4x the rows of the 1024-thread form, whose blocks waited for a
+// whole free CU (21-27 us per call in the step against 4 standalone).  Step 17.25 -> 17.14 ms
+// (3 x 3 interleaved; 64 threads: 17.36).  FS2_RP_SL=64 (experiments build): the 1024-thread form.
+void launch_reduce_parts(hipStream_t st, const float* part, int nb, int D, int npart, float* o0,
+                         float* o1, float* o2, int accumulate) {
+  static const int sl = fs2_exp_int("FS2_RP_SL", 16);
+  const dim3 g((npart * D + 15) / 16);
+  if (sl == 16)
+    hipLaunchKernelGGL(reduce_parts_kernel<16>, g, dim3(256), 0, st, part, nb, D, npart, o0, o1,
+                       o2, accumulate);
+  else
+    hipLaunchKernelGGL(reduce_parts_kernel<64>, g, dim3(1024), 0, st, part, nb, D, npart, o0, o1,
+                       o2, accumulate);
 }
 
 // column sums, 16-B loads: thread = (row sub-lane, column chunk of VEC)
@@ -972,8 +988,7 @@ extern "C" int fs2_ln_bwd(const void* dy, int64_t lddy, const void* s, int64_t l
     float* o0 = dgamma ? dgamma : dcol;
     float* o1 = dgamma ? dbeta : nullptr;
     float* o2 = dgamma ? dcol : nullptr;
-    hipLaunchKernelGGL(reduce_parts_kernel, dim3((npart * D + 15) / 16), dim3(1024), 0, st,
-                       workspace, nb, D, npart, o0, o1, o2, 1);
+    launch_reduce_parts(st, workspace, nb, D, npart, o0, o1, o2, 1);
     FS2_CHECK_LAUNCH();
   }
   return 0;
@@ -1001,8 +1016,7 @@ extern "C" int fs2_colsum(const void* X, int64_t ldx, int M, int N, int dtype, f
   } else {
     return FS2_EINVAL;
   }
-  hipLaunchKernelGGL(reduce_parts_kernel, dim3((N + 15) / 16), dim3(1024), 0, st, workspace, nb, N,
-                     1, out, nullptr, nullptr, accumulate);
+  launch_reduce_parts(st, workspace, nb, N, 1, out, nullptr, nullptr, accumulate);
   FS2_CHECK_LAUNCH();
   return 0;
 }
@@ -1071,8 +1085,7 @@ extern "C" int fs2_pad_transpose(const void* X, int64_t ldx, int B, int T, int C
                      C, P, reflect, (bf16*)out, (long)ldo, ncols, colsum ? workspace : nullptr);
   FS2_CHECK_LAUNCH();
   if (colsum) {   // colsum[c] += sum over the token blocks' partials (fixed order)
-    hipLaunchKernelGGL(reduce_parts_kernel, dim3((C + 15) / 16), dim3(1024), 0, s, workspace,
-                       (int)grid.x, C, 1, colsum, nullptr, nullptr, 1);
+    launch_reduce_parts(s, workspace, (int)grid.x, C, 1, colsum, nullptr, nullptr, 1);
     FS2_CHECK_LAUNCH();
   }
   return 0;
