@@ -21,6 +21,9 @@ struct LnFwdP {
   char* s_out; const float* gamma; const float* beta; float eps; int do_tanh;
   float p_o; uint32_t salt_o; const float* row_mask; const char* post_add; long ldp;
   char* y; long ldy; float* mean; float* rstd; int M, D; uint32_t seed;
+  // optional reflect-padded token-major copy of y (the bf16 rows kernels; fs2_pad_rows layout,
+  // row pitch D): token (b, t) at image row b*(T+2P) + P + t, and mirrored into the pad rows
+  char* img; int img_t, img_p;
 };
 
 template <typename T>
@@ -159,6 +162,13 @@ __global__ void __launch_bounds__(256) ln_fwd_rows_kernel(LnFwdP p) {
         o[e] = q;
       }
       vstore<bf16>((bf16*)p.y + (long)row * p.ldy + d0, o);
+      if (p.img) {   // padded index i holds token reflect(i - P): i = P + t, P - t, P + 2(T-1) - t
+        const int T = p.img_t, P = p.img_p, b = row / T, t = row - b * T;
+        bf16* ib = (bf16*)p.img + (long)b * (T + 2 * P) * p.D + d0;
+        vstore<bf16>(ib + (long)(P + t) * p.D, o);
+        if (t >= 1 && t <= P) vstore<bf16>(ib + (long)(P - t) * p.D, o);
+        if (t >= T - 1 - P && t <= T - 2) vstore<bf16>(ib + (long)(P + 2 * (T - 1) - t) * p.D, o);
+      }
     }
   }
 }
@@ -905,12 +915,16 @@ extern "C" int fs2_ln_fwd(const void* x, int64_t ldx, const void* r, int64_t ldr
                           float eps, int do_tanh, float p_o, uint32_t salt_o,
                           const float* row_mask, const void* post_add, int64_t ldp, void* y,
                           int64_t ldy, float* mean, float* rstd, int M, int D, int dtype,
-                          uint32_t seed, void* stream) {
+                          uint32_t seed, void* img, int img_t, int img_p, void* stream) {
   if (M <= 0) return 0;
   if (D <= 0 || D > 64 * MAXJ || !x || !y || !gamma || !beta || !mean || !rstd) return FS2_EINVAL;
+  if (img && (dtype != FS2_BF16 || img_t <= 0 || M % img_t || img_p < 0 || img_p >= img_t ||
+              (D % 8) || !a16(img)))
+    return FS2_EINVAL;
   LnFwdP p{(const char*)x, ldx, (const char*)r, ldr, p_r, salt_r, (char*)s_out, gamma, beta,
            eps, do_tanh, p_o, salt_o, row_mask, (const char*)post_add, ldp, (char*)y, ldy, mean,
-           rstd, M, D, seed};
+           rstd, M, D, seed, nullptr, img_t, img_p};
+  bool img_done = false;
   dim3 grid((M + 3) / 4);
   hipStream_t s = (hipStream_t)stream;
   const int V = dtype == FS2_BF16 ? 8 : 4;
@@ -920,10 +934,15 @@ extern "C" int fs2_ln_fwd(const void* x, int64_t ldx, const void* r, int64_t ldr
                    (!s_out || a16(s_out)) && (!post_add || (a16(post_add) && ldp % V == 0));
   if (dtype == FS2_BF16) {
     if (!vec) hipLaunchKernelGGL(ln_fwd_kernel<bf16>, grid, dim3(256), 0, s, p);
-    else if (nch == 1 && ln_fwd_rows() == 2 && a16(gamma) && a16(beta))
+    else if (nch == 1 && ln_fwd_rows() == 2 && a16(gamma) && a16(beta)) {
+      p.img = (char*)img;
+      img_done = true;
       hipLaunchKernelGGL((ln_fwd_rows_kernel<2>), dim3((M + 7) / 8), dim3(256), 0, s, p);
-    else if (nch == 1 && ln_fwd_rows() == 4 && a16(gamma) && a16(beta))
+    } else if (nch == 1 && ln_fwd_rows() == 4 && a16(gamma) && a16(beta)) {
+      p.img = (char*)img;
+      img_done = true;
       hipLaunchKernelGGL((ln_fwd_rows_kernel<4>), dim3((M + 15) / 16), dim3(256), 0, s, p);
+    }
     else if (nch == 1) hipLaunchKernelGGL((ln_fwd_vec_kernel<bf16, 1>), grid, dim3(256), 0, s, p);
     else if (nch == 2) hipLaunchKernelGGL((ln_fwd_vec_kernel<bf16, 2>), grid, dim3(256), 0, s, p);
     else hipLaunchKernelGGL((ln_fwd_vec_kernel<bf16, 4>), grid, dim3(256), 0, s, p);
@@ -936,6 +955,8 @@ extern "C" int fs2_ln_fwd(const void* x, int64_t ldx, const void* r, int64_t ldr
     return FS2_EINVAL;
   }
   FS2_CHECK_LAUNCH();
+  if (img && !img_done)   // the other kernels: the image from y in a second pass
+    return fs2_pad_rows(y, ldy, M / img_t, img_t, D, img_p, 1, 0, img, D, dtype, stream);
   return 0;
 }
 

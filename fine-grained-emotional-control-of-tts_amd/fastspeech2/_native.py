@@ -112,7 +112,7 @@ SIGNATURES = {
     "fs2_pad_transpose": (I, [P, I64, I, I, I, I, I, P, I64, I, P, P, I, P]),
     "fs2_pad_rows": (I, [P, I64, I, I, I, I, I, I, P, I64, I, P]),
     "fs2_ln_fwd": (I, [P, I64, P, I64, Fl, U32, P, P, P, Fl, I, Fl, U32, P, P, I64, P, I64, P, P,
-                       I, I, I, U32, P]),
+                       I, I, I, U32, P, I, I, P]),
     "fs2_ln_bwd": (I, [P, I64, P, I64, P, P, P, P, I, Fl, U32, P, I, P, I64, P, Fl, U32, P, P, P,
                        I, I, I, U32, P, P]),
     "fs2_ln_workspace_floats": (I64, [I, I]),

@@ -82,6 +82,9 @@ _PAD_FWD = N.exp_int("FS2_PAD_FWD", 2)
 # forward in that order (engine._tap_inner_fwd): off -- 316-318 vs 314 us for the decoder's in
 # the step, step 17.42 vs 17.37 ms (experiments library, 2 x 2 interleaved)
 _TAP_INNER = N.exp_int("FS2_TAP_INNER", 1)
+# the FFN conv1 forward's padded image written by the LayerNorm before it (FS2_LN_IMG=0,
+# experiments build: a separate fs2_pad_rows pass)
+_LN_IMG = N.exp_int("FS2_LN_IMG", 1)
 _TAP_INNER_FWD = N.exp_int("FS2_TAP_INNER_FWD", 0)
 # serial mode for per-call-site timing (bench.py --detail runs with the experiments library)
 _NO_SIDE = N.exp_flag("FS2_NO_SIDE_STREAM")
@@ -802,24 +805,27 @@ class FS2Engine:
         mean1 = torch.empty(M, dtype=torch.float32, device=self.dev)
         rstd1 = torch.empty_like(mean1)
         s_r1 = salt()
-        ops.ln_fwd(X, D, P[prefix + "norm1.norm.weight"], P[prefix + "norm1.norm.bias"], 1e-6, X1, D,
-                   mean1, rstd1, M, D, dt=self.dt, seed=seed, r=Ao, ldr=D, p_r=p_drop, salt_r=s_r1,
-                   s_out=s1)
-        del Ao
         w1 = prefix + "pos_ffn.0.conv.weight"
         F, _, KW1 = self._wspecs[w1]
-        Hc = self.empty(M, F)
-        X1in = X1
-        if self._pad_fwd(w1, M, T):
-            P1 = (KW1 - 1) // 2
-            img = self.empty(B * (T + 2 * P1) + 2 * P1, D)
+        P1 = (KW1 - 1) // 2
+        # the FFN conv1 forward's reflect-padded X1 image, written by the LayerNorm that makes
+        # X1 (fs2_ln_fwd img).  Its 2P tail rows stay unwritten: only the dropped pad-row
+        # outputs of the last utterance read them (c_row = (T, -2P); each output row sums its
+        # own 2P+1 image rows)
+        img = self.empty(B * (T + 2 * P1) + 2 * P1, D) if self._pad_fwd(w1, M, T) else None
+        ops.ln_fwd(X, D, P[prefix + "norm1.norm.weight"], P[prefix + "norm1.norm.bias"], 1e-6, X1, D,
+                   mean1, rstd1, M, D, dt=self.dt, seed=seed, r=Ao, ldr=D, p_r=p_drop, salt_r=s_r1,
+                   s_out=s1, img=img if _LN_IMG else None, img_t=T, img_p=P1)
+        if img is not None and not _LN_IMG:
             ops.pad_rows(X1, D, B, T, D, P1, 1, 2 * P1, img, D, dt=self.dt)
-            X1in = (img,)
+        del Ao
+        Hc = self.empty(M, F)
+        X1in = X1 if img is None else (img,)
         tag = "ffn_conv1_fwd." + prefix.split(".")[0]
         self._tic(tag)
         self._fwd(X1in, D, M, T, w1, Hc, F, bias=P[prefix + "pos_ffn.0.conv.bias"], relu=1)
         self._toc(tag)
-        del X1in
+        del X1in, img
         Y = self.empty(M, D)
         self._fwd(Hc, F, M, T, prefix + "pos_ffn.2.conv.weight", Y, D,
                   bias=P[prefix + "pos_ffn.2.conv.bias"])

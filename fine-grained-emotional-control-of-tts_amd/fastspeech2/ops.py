@@ -134,10 +134,13 @@ def colsum_ws(M, N_):
 
 def ln_fwd(x, ldx, gamma, beta, eps, y, ldy, mean, rstd, M, D, *, dt, seed=0, r=None, ldr=0,
            p_r=0.0, salt_r=0, s_out=None, do_tanh=0, p_o=0.0, salt_o=0, row_mask=None,
-           post_add=None, ldp=0):
+           post_add=None, ldp=0, img=None, img_t=0, img_p=0):
+    """``img``: also y's reflect-padded token-major image (fs2_pad_rows layout, img_t tokens
+    per utterance, img_p pad rows each side)"""
     _chk(N.lib().fs2_ln_fwd(_p(x), ldx, _p(r), ldr, p_r, salt_r, _p(s_out), _p(gamma), _p(beta),
                             eps, do_tanh, p_o, salt_o, _p(row_mask), _p(post_add), ldp, _p(y), ldy,
-                            _p(mean), _p(rstd), M, D, dt, seed & 0xffffffff, _s()), "fs2_ln_fwd")
+                            _p(mean), _p(rstd), M, D, dt, seed & 0xffffffff, _p(img), img_t, img_p,
+                            _s()), "fs2_ln_fwd")
 
 
 def ln_bwd(dy, lddy, s, lds, mean, rstd, gamma, beta, ds, ldds, M, D, *, dt, ws, seed=0,

@@ -152,11 +152,15 @@ int64_t fs2_colsum_workspace_floats(int M, int N);
  *   y = LN(s)*gamma + beta         (eps per call: 1e-6 FFT, 1e-5 predictors/PostNet)
  *   y = tanh(y) (opt) ; y = drop(y; p_o) ; y *= row_mask (opt) ; y += post_add (opt)
  * ------------------------------------------------------------------------------------------ */
+/* img (optional, bf16, M % img_t == 0, img_p < img_t): also y's reflect-padded token-major
+ * image as fs2_pad_rows(y, ..., img_t, D, img_p, reflect 1, tail 0) writes it (row pitch D) --
+ * the FFN conv1 forward's operand, written by the LayerNorm that produces its input
+ * (SB Conv1d "same"+reflect, App. A.1) instead of a separate pass.                        */
 int fs2_ln_fwd(const void* x, int64_t ldx, const void* r, int64_t ldr, float p_r, uint32_t salt_r,
                void* s_out, const float* gamma, const float* beta, float eps, int do_tanh,
                float p_o, uint32_t salt_o, const float* row_mask, const void* post_add,
                int64_t ldp, void* y, int64_t ldy, float* mean, float* rstd, int M, int D,
-               int dtype, uint32_t seed, void* stream);
+               int dtype, uint32_t seed, void* img, int img_t, int img_p, void* stream);
 
 /* backward of fs2_ln_fwd; dgamma/dbeta (+)= column sums (fp32).  ds = dL/ds (optionally
  * gated by (s > 0) for a ReLU that produced s), dr = ds * dropmask_r / (1 - p_r).

@@ -1098,6 +1098,39 @@ def test_conv_dgrad_padded_image(cuda, B, T, O, C, KW):
         assert rel(Xt, X4) < 1e-5
 
 
+@pytest.mark.parametrize("B,T,D,P", [(32, 977, 384, 4), (32, 200, 384, 4), (3, 7, 384, 4),
+                                     (2, 50, 1024, 2), (4, 9, 80, 4)])
+def test_ln_fwd_padded_image(cuda, B, T, D, P):
+    """fs2_ln_fwd's img output: the LayerNorm output y, bit-identical to a call without it, and
+    its reflect-padded token-major image, exactly what fs2_pad_rows makes from y (pad rows
+    mirrored; T = 7 and 9 with P = 4: every row of a short utterance lands in a pad row too).
+    D = 1024 takes the one-row vector kernel and the image from a second pass."""
+    from fastspeech2 import ops
+    torch.manual_seed(B * T + D)
+    bf = torch.bfloat16
+    M, L = B * T, T + 2 * P
+    x = torch.randn(M, D, device=cuda).to(bf)
+    r = torch.randn(M, D, device=cuda).to(bf)
+    g = torch.randn(D, device=cuda)
+    b = torch.randn(D, device=cuda)
+    outs = []
+    for with_img in (False, True):
+        y = torch.empty(M, D, device=cuda, dtype=bf)
+        s = torch.empty(M, D, device=cuda, dtype=bf)
+        mean = torch.empty(M, device=cuda)
+        rstd = torch.empty(M, device=cuda)
+        img = torch.full((B * L, D), float("nan"), device=cuda, dtype=bf) if with_img else None
+        ops.ln_fwd(x, D, g, b, 1e-6, y, D, mean, rstd, M, D, dt=1, seed=3, r=r, ldr=D, p_r=0.1,
+                   salt_r=5, s_out=s, img=img, img_t=T, img_p=P)
+        outs.append((y, s, img))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    ref = torch.full((B * L, D), float("nan"), device=cuda, dtype=bf)
+    ops.pad_rows(outs[1][0], D, B, T, D, P, 1, 0, ref, D, dt=1)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[1][2], ref)
+
+
 @pytest.mark.parametrize("B,T,C,O,KW", [(32, 977, 384, 1536, 9), (32, 200, 384, 1536, 9),
                                          (3, 37, 128, 256, 9), (2, 50, 192, 320, 5)])
 def test_conv_fwd_padded_image(cuda, B, T, C, O, KW):
