@@ -85,8 +85,8 @@ typedef struct fs2_gemm_desc {
    * the zero-padded dY image of the conv1 data gradient.  c_row_pad < 0: the inverse -- rows m
    * of a padded domain (L = c_row_t - c_row_pad rows per utterance) with m mod L < c_row_t are
    * stored at m - (m / L) * (-c_row_pad), the others dropped (a conv forward over the padded
-   * domain, fs2_pad_rows).  bf16, both K-major, no split / batch / conv; runs on the
-   * persistent 256-row kernel (FS2_EINVAL where that kernel does not apply).                */
+   * domain, fs2_pad_rows).  bf16, both K-major, no split / batch / conv; runs on the 4-wave
+   * or the persistent 256-row kernel (FS2_EINVAL where neither applies).                    */
   int c_row_t, c_row_pad;
   /* grid budget of the persistent GEMM kernels for this call (0 or >= 256: one block per CU):
    * a GEMM enqueued beside a latency-critical stream -- the weight gradients of the train step
