@@ -55,7 +55,27 @@ def test_gemm_host_validation_rejects_bad_args():
     d.split_k, d.c_fp32 = 2, 0
     assert lib.fs2_gemm(ctypes.byref(d), None) == -1          # split-K needs an fp32 output
     d.split_k = 1
+    # tap-inner K order (a_kw): K must equal a_kw * lda with lda % 64 == 0, K-major, no conv
+    d.M, d.N, d.K, d.lda, d.ldb, d.a_kw = 16, 16, 9 * 48, 48, 9 * 48, 9
+    assert lib.fs2_gemm(ctypes.byref(d), None) == -1          # lda 48 % 64 != 0
+    d.K, d.lda, d.ldb, d.a_kw = 9 * 64, 64, 9 * 64, 8
+    assert lib.fs2_gemm(ctypes.byref(d), None) == -1          # K != a_kw * lda
+    d.a_kw, d.conv_mode, d.conv_t, d.conv_kw, d.conv_c = 9, 1, 16, 9, 64
+    assert lib.fs2_gemm(ctypes.byref(d), None) == -1          # no implicit conv with a_kw
+    d.conv_mode, d.a_kw = 0, 0
     assert lib.fs2_loss_fwd_bwd(None, None) == -1
+
+
+def test_ctypes_argument_counts_match_header():
+    """every prototype in include/fs2_hip.h has as many parameters as its ctypes signature in
+    fastspeech2/_native.py (a parameter added on one side only shifts every later argument)"""
+    from fastspeech2 import _native
+    src = open(os.path.join(ROOT, "include", "fs2_hip.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    for name, args in re.findall(r"\b(fs2_[a-z0-9_]+)\s*\(([^;{]*?)\)\s*;", src, flags=re.S):
+        args = args.strip()
+        n = 0 if args in ("", "void") else args.count(",") + 1
+        assert n == len(_native.SIGNATURES[name][1]), name
 
 
 def _tiny_cfg():
