@@ -78,10 +78,12 @@ _KM_WGRAD = N.exp_int("FS2_KM_WGRAD", 1)
 _PAD_DGRAD = N.exp_int("FS2_PAD_DGRAD", 1)
 # FFN conv1 forward over a reflect-padded X image (engine._pad_fwd)
 _PAD_FWD = N.exp_int("FS2_PAD_FWD", 2)
-# decoder FFN conv1 data gradient in the tap-inner K order (engine._tap_inner); the FFN conv1
-# forward in that order (engine._tap_inner_fwd): off -- 316-318 vs 314 us for the decoder's in
-# the step, step 17.42 vs 17.37 ms (experiments library, 2 x 2 interleaved)
-_TAP_INNER = N.exp_int("FS2_TAP_INNER", 1)
+# decoder FFN conv1 data gradient in the tap-inner K order (engine._tap_inner): off -- 11 %
+# faster standalone and 190 instead of 995 MB read, but the step measured 0.03-0.08 ms slower
+# with it in three same-box A/Bs (17.18 vs 17.13 ms on the final tree); the FFN conv1 forward in
+# that order (engine._tap_inner_fwd): off -- 316-318 vs 314 us for the decoder's in the step,
+# step 17.42 vs 17.37 ms (experiments library, 2 x 2 interleaved)
+_TAP_INNER = N.exp_int("FS2_TAP_INNER", 0)
 # the FFN conv1 forward's padded image written by the LayerNorm before it (FS2_LN_IMG=0,
 # experiments build: a separate fs2_pad_rows pass)
 _LN_IMG = N.exp_int("FS2_LN_IMG", 1)
