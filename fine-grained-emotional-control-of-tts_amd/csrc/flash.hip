@@ -186,6 +186,42 @@ __device__ __forceinline__ bf16x8 pack8(const float* a, const float* b) {
   return r;
 }
 
+// Explicit LDS addressing for the swizzled [rows][DH] tiles (chunk c of row r at c ^ (r & 7)):
+// one per-lane VGPR base per parity / residue class and the rest as the instruction's 16-bit
+// immediate offset.  Left to itself the compiler hoisted one per-lane address per fragment out
+// of the tile loop (24 row-fragment + 48 transposed-read addresses) and spilled.
+//   row fragment (16 rows from row0, 32-dim step s): row0 * RB + s * 64 + rbase[s & 1]
+//   (chunk (4s + g) ^ l7 = 4 (s ^ (l7 >> 2)) + (g ^ (l7 & 3)), l7 = lane & 7)
+__device__ __forceinline__ void row_frag_bases(int lane, int rb, int (&base)[2]) {
+  const int li = lane & 15, g = lane >> 4, l7 = lane & 7, hb = l7 >> 2;
+  const int c = li * rb + ((g ^ (l7 & 3)) << 4);
+  base[0] = c + hb * 64;    // even s: s ^ 1 = s + 1 where hb = 1
+  base[1] = c - hb * 64;    // odd s:  s ^ 1 = s - 1
+}
+template <int OFF>
+__device__ __forceinline__ bf16x8 lds_frag_at(const char* tile, int base) {
+  return *(const bf16x8*)(tile + base + OFF);
+}
+//   transposed fragment (rows rbase .. rbase + 31 as lane groups, features 16 d ..): the
+//   address is tbase[d & 3] + rbase * RB + (d & ~3) * 32 (lo) and + 16 RB (hi)
+__device__ __forceinline__ void tr_frag_bases(int lane, int rb, int (&base)[4]) {
+  const int li = lane & 15, g = lane >> 4, q = li >> 2, pp = li & 3;
+  const int x = (4 * g + q) & 7, y = x >> 1;
+  const int c = (4 * g + q) * rb + ((((pp >> 1) ^ (x & 1))) << 4) + ((pp & 1) * 4) * 2;
+#pragma unroll
+  for (int dd = 0; dd < 4; ++dd) base[dd] = c + ((dd ^ y) << 5);
+}
+// (the builtin: an asm read's result is a plain value to the compiler, which may copy it into
+// the MFMA's operand quad before the counted wait that retires it -- it did, here)
+template <int OFF, int RBYTES>
+__device__ __forceinline__ bf16x8 lds_tr_frag_at(const char* tile, int base) {
+  const char* a = tile + base + OFF;
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a);
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a + 16 * RBYTES));
+  const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
 // max / sum over the 4 lane groups (lanes l, l ^ 16, l ^ 32, l ^ 48) of a 16x16 C fragment: the
 // gfx950 permlane swaps are VALU ops (the __shfl_xor they replace went through ds_bpermute)
 __device__ __forceinline__ float xg_max(float v) {
@@ -931,6 +967,259 @@ __global__ void __launch_bounds__(W8 * 64, 1) attn_bwd_dkv_kernel(AttnP p) {
 #undef FS2_STAMP
 }
 
+// ------------------------------------------------------------------------ backward dK dV, paired
+// block: 8 waves = 4 pairs x 32 keys (128 keys); query tiles of 64 as attn_bwd_dkv_kernel.  The two
+// waves of a pair own the same 32 keys and split the work by role instead of each computing all
+// four products for 16 keys: role 0 (waves 0-3) keeps the K fragments, computes S = Q K^T, the
+// probabilities P and dV += Pd^T dO; role 1 (waves 4-7) keeps the V fragments, computes
+// dP = dO V^T and, with P handed over through LDS (fp32, one 16-byte slot per lane and 16-query
+// block), dS = P (dP' - D) and dK += dS^T Q.  Every Q / dO fragment and every transposed
+// dO^T / Q^T fragment read from LDS then feeds two MFMAs (one per 16-key group) instead of one,
+// at the register budget of the 16-key kernel (K or V fragments 48, dK or dV accumulators 96,
+// S or dP 32 per wave).  Same arithmetic and accumulation order as attn_bwd_dkv_kernel: the
+// results are bit-identical.
+template <int DH, bool DROP>
+__global__ void __launch_bounds__(512, 1) attn_bwd_dkv2_kernel(AttnP p) {
+  constexpr int NS = DH / 32, ND = DH / 16;
+  constexpr int TB = 64 * DH * 2;
+  constexpr int KB = 128;          // keys per block
+  constexpr int XB = 4 * 2 * 4 * 64 * 16;   // hand-over: [pair][kg][qt][lane] x 16 B = 32 KiB
+  // [Q 0 | dO 0 | Q 1 | dO 1 | P hand-over | (lse, D, rowhash) 0 | (lse, D, rowhash) 1 | kval | kend, kfull]
+  __shared__ __attribute__((aligned(16))) char smem[4 * TB + XB + 1536 + TMAX + 16];
+  char* xbuf = smem + 4 * TB;
+  float* lsd = (float*)(smem + 4 * TB + XB);
+  uint8_t* kval = (uint8_t*)(smem + 4 * TB + XB + 1536);
+  int* kbuf = (int*)(smem + 4 * TB + XB + 1536 + TMAX);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
+  const int role = __builtin_amdgcn_readfirstlane(wave >> 2), kw = wave & 3;
+  int blk, z;
+  attn_block_coords(blk, z);
+  const int b = z / p.H, h = z - b * p.H;
+  constexpr bool drop = DROP;   // compile-time: a runtime flag branched per element
+  const bf16* Qb = p.qkv + (long)b * p.T * p.ldq + h * DH;
+  const bf16* Kb = Qb + p.D;
+  const bf16* Vb = Qb + 2 * p.D;
+  const bf16* dOb = p.dout + (long)b * p.T * p.lddo + h * DH;
+  const float c = p.scale_log2;
+
+  int key[2];
+  uint32_t kc[2];
+#pragma unroll
+  for (int kg = 0; kg < 2; ++kg) {
+    key[kg] = blk * KB + kw * 32 + kg * 16 + (lane & 15);
+    kc[kg] = (uint32_t)(key[kg] >> 1) * FS2_ATTN_KC;
+  }
+  // role 0: K fragments (S = Q K^T); role 1: V fragments (dP = dO V^T)
+  const bf16* Rb = role ? Vb : Kb;
+  bf16x8 rf[2][NS];
+#pragma unroll
+  for (int kg = 0; kg < 2; ++kg)
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+      rf[kg][s] = key[kg] < p.T ? ld_frag(Rb + (long)key[kg] * p.ldq + 32 * s + 8 * g) : bf16x8{};
+  f32x4 acc[2][ND];   // role 0: dV, role 1: dK
+#pragma unroll
+  for (int kg = 0; kg < 2; ++kg)
+#pragma unroll
+    for (int d = 0; d < ND; ++d) acc[kg][d] = f32x4{0, 0, 0, 0};
+
+  TileDma<DH, 8> dma;
+  dma.init(wave, lane, 0);
+  const i32x4 rsQ = make_rsrc(Qb), rsO = make_rsrc(dOb);
+  const int ntile_all = (p.T + 63) / 64;
+  const long BHT = (long)p.B * p.H * p.T;
+  const i32x4 rsL = make_rsrc(p.lse + (long)z * p.T), rsD = make_rsrc(p.dsum + (long)z * p.T);
+  const i32x4 rsH = make_rsrc(p.dsum + BHT + (long)z * p.T);
+  auto issue_tile = [&](int q0, int buf) {
+    if (wave == 0) {
+      const int vo = q0 + lane < p.T ? lane * 4 : BUF_OOB;
+      blds4(rsL, vo, q0 * 4, (char*)(lsd + buf * 192));
+      blds4(rsD, vo, q0 * 4, (char*)(lsd + buf * 192 + 64));
+      blds4(rsH, vo, q0 * 4, (char*)(lsd + buf * 192 + 128));
+    }
+    char* nx = smem + buf * 2 * TB;
+    dma.issue(nx, rsQ, p.ldq, q0, p.T, wave);
+    dma.issue(nx + TB, rsO, p.lddo, q0, p.T, wave);
+  };
+  if (ntile_all > 0) issue_tile(0, 0);
+  int kfull;
+  build_kvalid(kval, kbuf, p, b, h, &kfull);
+  bool kok = false;
+#pragma unroll
+  for (int kg = 0; kg < 2; ++kg) kok = kok || (key[kg] < p.T && kval[key[kg]]);
+  const int anyk = __syncthreads_or(kok);
+  const int ntile = anyk ? ntile_all : 0;
+  // per-lane hand-over slot: [kw][kg][qt] blocks of 64 lanes x 16 B
+  char* xl = xbuf + kw * (2 * 4 * 1024) + lane * 16;
+  int rb0[2], tb0[4];
+  row_frag_bases(lane, DH * 2, rb0);
+  tr_frag_bases(lane, DH * 2, tb0);
+  for (int t = 0; t < ntile; ++t) {
+    const int q0 = t * 64;
+    const char* T1 = smem + (t & 1) * 2 * TB + role * TB;         // role 0: Q, role 1: dO
+    const char* T2 = smem + (t & 1) * 2 * TB + (role ^ 1) * TB;   // role 0: dO, role 1: Q
+    const float* ls_s = lsd + (t & 1) * 192;
+    const float* ds_s = ls_s + 64;
+    const uint32_t* rh_s = (const uint32_t*)(ls_s + 128);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // tile t (and the K/V fragments) landed
+    __builtin_amdgcn_s_barrier();   // ... for every wave; every wave is done with tile t-1
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + 1 < ntile) issue_tile(q0 + 64, (t + 1) & 1);
+    // phase 1: S (role 0) or dP (role 1) for 64 queries x 32 keys; 24 steps (s, qt) of one
+    // fragment read and two MFMAs, each read two steps ahead of its MFMAs
+    f32x4 s1[2][4];
+#pragma unroll
+    for (int kg = 0; kg < 2; ++kg)
+#pragma unroll
+      for (int qt = 0; qt < 4; ++qt) s1[kg][qt] = f32x4{0, 0, 0, 0};
+    {
+      bf16x8 fa[3];
+      const char* T1b0 = T1 + rb0[0];
+      const char* T1b1 = T1 + rb0[1];
+      auto rd = [&](auto STc) {
+        constexpr int st = decltype(STc)::value, s = st >> 2, qt = st & 3;
+        constexpr int off = qt * 16 * DH * 2 + s * 64;
+        return lds_frag_at<off>(s & 1 ? T1b1 : T1b0, 0);
+      };
+      fa[0] = rd(std::integral_constant<int, 0>{});
+      fa[1] = rd(std::integral_constant<int, 1>{});
+      static_for<0, 4 * NS>([&](auto SI) {
+        constexpr int st = decltype(SI)::value, s = st >> 2, qt = st & 3;
+        if constexpr (st + 2 < 4 * NS) {
+          fa[(st + 2) % 3] = rd(std::integral_constant<int, st + 2>{});
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+#pragma unroll
+        for (int kg = 0; kg < 2; ++kg)
+          s1[kg][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[st % 3], rf[kg][s], s1[kg][qt], 0, 0, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      });
+    }
+    // dropout draws of this lane's (query row, key) elements, identical in both roles: keys 2m
+    // and 2m+1 (lanes 2m, 2m+1) share one draw per query row; the even lane draws rows r = 0, 1
+    // and the odd lane rows 2, 3, then they swap (DPP quad_perm)
+    auto keep_bits = [&](int kg, int qt, uint32_t (&hx)[4]) {
+      const int odd = lane & 1;
+      const u32x2 rh2 = *(const u32x2*)(rh_s + qt * 16 + 4 * g + 2 * odd);
+      uint32_t mine[2], other[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) mine[e] = fs2_attn_mix(rh2[e] + kc[kg]);
+#pragma unroll
+      for (int e = 0; e < 2; ++e)
+        other[e] = (uint32_t)__builtin_amdgcn_mov_dpp((int)mine[e], 0xB1, 0xF, 0xF, false);
+      hx[0] = odd ? other[0] : mine[0];
+      hx[1] = odd ? other[1] : mine[1];
+      hx[2] = odd ? mine[0] : other[0];
+      hx[3] = odd ? mine[1] : other[1];
+    };
+    bf16x8 pk[2][2];   // role 0: Pd, role 1: dS, per (kg, 32-query half j): the phase-2 A operands
+    if (role == 0) {
+#pragma unroll
+      for (int kg = 0; kg < 2; ++kg)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          float pdv[2][4];
+#pragma unroll
+          for (int h2 = 0; h2 < 2; ++h2) {
+            const int qt = 2 * j + h2;
+            const f32x4 l4 = *(const f32x4*)(ls_s + qt * 16 + 4 * g);
+            uint32_t hx[4];
+            if constexpr (DROP) keep_bits(kg, qt, hx);
+            f32x4 pr4;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float pr = fexp2(fmaf(s1[kg][qt][r], c, -l4[r]));
+              pr4[r] = pr;
+              pdv[h2][r] = (!drop || ((hx[r] >> ((lane & 1) * 16)) & 0xffffu) >= p.thr16) ? pr : 0.f;
+            }
+            *(f32x4*)(xl + (kg * 4 + qt) * 1024) = pr4;
+          }
+          pk[kg][j] = pack8(pdv[0], pdv[1]);
+        }
+    }
+    // the P hand-over written: its LDS stores retired before the barrier (s_barrier alone does
+    // not wait for them)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (role == 1) {
+#pragma unroll
+      for (int kg = 0; kg < 2; ++kg)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          float dsv[2][4];
+#pragma unroll
+          for (int h2 = 0; h2 < 2; ++h2) {
+            const int qt = 2 * j + h2;
+            const f32x4 d4 = *(const f32x4*)(ds_s + qt * 16 + 4 * g);
+            const f32x4 pr4 = *(const f32x4*)(xl + (kg * 4 + qt) * 1024);
+            uint32_t hx[4];
+            if constexpr (DROP) keep_bits(kg, qt, hx);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              float dp = s1[kg][qt][r];
+              if constexpr (DROP) {
+                const bool keep = ((hx[r] >> ((lane & 1) * 16)) & 0xffffu) >= p.thr16;
+                dp = keep ? dp * p.inv_keep : 0.f;
+              }
+              dsv[h2][r] = pr4[r] * (dp - d4[r]);
+            }
+          }
+          pk[kg][j] = pack8(dsv[0], dsv[1]);
+        }
+    }
+    // phase 2: role 0 dV += Pd^T dO, role 1 dK += dS^T Q: the transposed tile fragments two
+    // (j, d) steps ahead of their MFMAs
+    bf16x8 tf[3];
+    auto trd = [&](auto NC) {
+      constexpr int n = decltype(NC)::value, j = n / ND, d = n % ND;
+      return lds_tr_frag_at<32 * j * DH * 2 + (d & ~3) * 32, DH * 2>(T2, tb0[d & 3]);
+    };
+    tf[0] = trd(std::integral_constant<int, 0>{});
+    tf[1] = trd(std::integral_constant<int, 1>{});
+    static_for<0, 2 * ND>([&](auto NI) {
+      constexpr int n = decltype(NI)::value, j = n / ND, d = n % ND;
+      if constexpr (n + 2 < 2 * ND) {
+        tf[(n + 2) % 3] = trd(std::integral_constant<int, n + 2>{});
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      }
+#pragma unroll
+      for (int kg = 0; kg < 2; ++kg)
+        acc[kg][d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pk[kg][j], tf[n % 3], acc[kg][d], 0, 0, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+    });
+  }
+  // the speculative tile-0 DMA of a block whose keys are all masked (no loop ran) has landed,
+  // and every wave is done with the tile ring, before the results are staged there
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  // C layout: col = feature (lane & 15), rows = keys 4g + r of the 16-key group kg; staged as
+  // [key][dK | dV] rows through the tile ring, then stored as 16-byte chunks of whole rows
+  constexpr int RB = 4 * DH;
+  static_assert(KB * RB <= 4 * TB, "dK/dV staging must fit the tile ring");
+  const float osc = ntile > 0 ? (role ? p.scale : p.inv_keep) : 0.f;
+#pragma unroll
+  for (int kg = 0; kg < 2; ++kg)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int kl = kw * 32 + kg * 16 + 4 * g + r;
+      const bool ok = kval[min(blk * KB + kl, p.T - 1)];
+      bf16* row = (bf16*)(smem + kl * RB) + (role ? 0 : DH);
+#pragma unroll
+      for (int d = 0; d < ND; ++d) row[16 * d + (lane & 15)] = (bf16)(ok ? acc[kg][d][r] * osc : 0.f);
+    }
+  __syncthreads();
+  constexpr int CPR = RB / 16;   // 16-byte chunks per staged row
+  for (int i = threadIdx.x; i < KB * CPR; i += 512) {
+    const int kl = i / CPR, cc = i - kl * CPR;
+    const int kr = blk * KB + kl;
+    if (kr >= p.T) continue;
+    const int half = cc >= CPR / 2;   // 0: dK, 1: dV
+    bf16* dst = p.dqkv + ((long)b * p.T + kr) * p.lddq + (1 + half) * p.D + h * DH +
+                (cc - half * (CPR / 2)) * 8;
+    *(u32x4*)dst = *(const u32x4*)(smem + kl * RB + cc * 16);
+  }
+}
+
 int attn_qg_fwd(int dh) { return dh <= 128 ? 2 : 1; }
 
 // half-size forward blocks (64 queries) when 128-row blocks would leave CUs idle (the
@@ -973,6 +1262,17 @@ void launch_bwd(const AttnP& p, hipStream_t s) {
   dim3 g1((p.T + 127) / 128, p.B * p.H);
   if (DH <= 64) hipLaunchKernelGGL((attn_bwd_dq_kernel<DH, 2>), g1, dim3(256), 0, s, p);
   else hipLaunchKernelGGL((attn_bwd_dq_kernel<DH, 1>), g1, dim3(512), 0, s, p);
+  // FS2_ATTN_BWD=4 (experiments build): the paired dK / dV kernel -- bit-identical, 241 -> 235
+  // us without dropout but 251 -> 263 us with it (tools/attn_ab_bwd.sh), so off
+#ifdef FS2_EXPERIMENTS
+  if constexpr (DH <= 192) {
+    if (fs2_exp_int("FS2_ATTN_BWD", 0) & 4) {
+      if (p.p_drop > 0.f) hipLaunchKernelGGL((attn_bwd_dkv2_kernel<DH, true>), g1, dim3(512), 0, s, p);
+      else hipLaunchKernelGGL((attn_bwd_dkv2_kernel<DH, false>), g1, dim3(512), 0, s, p);
+      return;
+    }
+  }
+#endif
   hipLaunchKernelGGL(attn_bwd_dkv_kernel<DH>, g1, dim3(512), 0, s, p);
 }
 

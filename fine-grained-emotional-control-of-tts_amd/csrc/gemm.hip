@@ -1951,14 +1951,18 @@ __global__ void __launch_bounds__(W4_NT, 1) gemm_w4b_kernel(GemmP p) {
     return ((st - q64 * p.a_kw) * (int)p.lda + q64 * 64) * 2;
   };
   // DMA piece j (0 .. NP-1) of this wave for the stage at A / B byte offsets ka / kb, into slot
-  // base dst
+  // base dst.  The raw-buffer range check covers voffset only (the piece's row and K offsets ride
+  // in soffset), so a lane whose row is past M (A) or N (B) -- the partial last tile -- gets
+  // voffset BUF_OOB and loads zeros instead of reading past the operand
   auto dma = [&](int j, int ka, int kb, char* dst) {
     if (j < 8) {
       const int pi = wave * 8 + j;
-      blds16(rsA, voa, sa0 + pi * lda8 + ka, dst + pi * 1024);
+      const int vo = (lane >> 3) < p.M - m0 - pi * 8 ? voa : BUF_OOB;
+      blds16(rsA, vo, sa0 + pi * lda8 + ka, dst + pi * 1024);
     } else {
       const int pi = wave * NF + j - 8;
-      blds16(rsB, vob, sb0 + pi * ldb8 + kb, dst + 256 * 128 + pi * 1024);
+      const int vo = (lane >> 3) < p.N - n0 - pi * 8 ? vob : BUF_OOB;
+      blds16(rsB, vo, sb0 + pi * ldb8 + kb, dst + 256 * 128 + pi * 1024);
     }
   };
   // fragment reads: lane l, row (l & 15) of a 16-row fragment, logical chunk 4h + (l >> 4)
@@ -2002,7 +2006,10 @@ __global__ void __launch_bounds__(W4_NT, 1) gemm_w4b_kernel(GemmP p) {
     // row: B in rows 0-2, A in rows 2-5); a barrier after row 3 (every wave's B reads of this
     // slot retired: 12 reads issued, NF of them B) releases the slot's B image, whose pieces of
     // stage s+2 go out over rows 4-7
-    const int kb = (s + 2) * 128, ka = aoff(s + 2);
+    // the last two stages' DMA (into slots no one reads again) re-fetches stage 0: K offsets past
+    // the operand would not be range-checked (soffset)
+    const bool live = s + 2 < nst;
+    const int kb = live ? (s + 2) * 128 : 0, ka = live ? aoff(s + 2) : 0;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       if (i >= 4 && !(xf & 2)) {

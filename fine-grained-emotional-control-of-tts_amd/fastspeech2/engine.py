@@ -71,6 +71,10 @@ _PS_MODES = N.exp_int("FS2_PS_MODES", 5)
 # result no longer depends on atomic ordering.  FS2_NO_WGRAD_BIG_SLICES=1 restores the atomics.
 _BIG_SLICES = not N.exp_flag("FS2_NO_WGRAD_BIG_SLICES")
 _SLICE_TARGET = N.exp_int("FS2_WGRAD_SLICE_TARGET", 240)
+# CU budget of the small weight gradients' split-K on the side stream: sliced ones fill
+# _WG_SLICE_CU CUs, the atomic ones _WG_ATOMIC_UNITS (tile, split) units (experiments build)
+_WG_SLICE_CU = N.exp_int("FS2_WG_SLICE_CU", 256)
+_WG_ATOMIC_UNITS = N.exp_int("FS2_WG_ATOMIC_UNITS", 512)
 # conv weight gradients with both operands K-major (channel-major padded images, conv_mode 6):
 # FS2_KM_WGRAD=0 restores the MN-major implicit-conv GEMM for A/B runs
 _KM_WGRAD = N.exp_int("FS2_KM_WGRAD", 1)
@@ -174,12 +178,30 @@ class FS2Engine:
         self.timer = None            # optional KernelTimer: HIP events around tagged launches
         self._km = {}                # conv_mode-6 images, reused layer after layer (side stream)
         self._img = {}               # per-layer zero-padded dY images (_dy_image)
+        self._fimg = {}              # padded FFN conv1 forward images (_fwd_image)
         # FusedTrainer.step sets adam_split = (optimizer, AdamW scalars): the backward then updates
         # the parameters whose gradients are final after the decoder (_adam_late) on the aux
         # stream while the main stream runs the encoder backward; adamw_step_split does the rest
         self.adam_split = None
         self._adam_late_done = False
+        # DP (FusedTrainer): (ready(), wait(stream)) of the gradient buckets holding the late
+        # parameters -- the late AdamW is launched from the notify hook once they are all queued,
+        # its aux stream waiting for their all-reduce
+        self.dp_late = None
+        self.n_adam_late = 0         # late AdamW launches from inside the backward (tests)
         self._adam_tabs = None
+
+    def _fwd_image(self, rows, tail, C):
+        """the FFN conv1 forward's padded image [rows + tail][C], one per shape: every layer's
+        forward rewrites its first ``rows`` rows before the GEMM reads them (main stream), and
+        the ``tail`` rows past them stay zero"""
+        key = (rows, tail, C, self.adt)
+        img = self._fimg.get(key)
+        if img is None:
+            img = self.empty(rows + tail, C)
+            img[rows:].zero_()
+            self._fimg[key] = img
+        return img
 
     def _tic(self, tag):
         if self.timer is not None:
@@ -296,7 +318,9 @@ class FS2Engine:
         self.params[self.PRED1 + ".weight"] = f[ow:ow + nw].view(2 * O, KW, C).permute(0, 2, 1)
         self.grads[self.PRED1] = gf[ow:ow + nw].view(2 * O, KW, C).permute(0, 2, 1)
         self.params[self.PRED1 + ".bias"] = f[ob:ob + 2 * O]
-        self._gemm_params |= {wp}
+        # the fused gradient view covers the same flat range as the two per-predictor conv1
+        # weight-gradient views: drop those, so nothing that walks self.grads counts it twice
+        del self.grads[wd], self.grads[wp]
 
     def _weight_specs(self):
         """name -> (O, C, KW, ldf, ldb_rows) for every GEMM weight."""
@@ -408,9 +432,14 @@ class FS2Engine:
         wt = ops.weight_prep_table(ents) if ents else (None, 0, 0)
         return wt, ops.adamw_ranges_table(self._adam_range_list(late), self.dev)
 
-    def _adam_launch_late(self):
+    def late_param_end(self):
+        """end of the late parameters in the flat buffer (they lead it: backward order)"""
+        return max(off + k for name, off, k, _, _ in self.m._layout if self._adam_late(name))
+
+    def _adam_launch_late(self, wait=None):
         """the late parameters' AdamW on the aux stream, after everything queued on the main and
-        the weight-gradient streams (their gradients); the main stream does not wait here"""
+        the weight-gradient streams (their gradients) and, under DP, after ``wait(aux)`` (the
+        all-reduce of their buckets); the main stream does not wait here"""
         opt, scal = self.adam_split
         m = self.m
         if self._wtable is None:
@@ -420,9 +449,12 @@ class FS2Engine:
         wl, rl = self._adam_tabs[1]
         h = self._aux_fork()
         self._aux.wait_stream(self._side)
+        if wait is not None:
+            wait(self._aux)
         ops.adamw_prep(wl, rl, m._flat, m._gflat, opt.exp_avg, opt.exp_avg_sq, *scal, dt=self.dt)
         self._aux_exit(h)
         self._adam_late_done = True
+        self.n_adam_late += 1
 
     def adamw_step_split(self, opt, scal):
         """the rest of a step's AdamW (FusedTrainer.step): the early parameters on the main
@@ -729,10 +761,10 @@ class FS2Engine:
         tiles = -(-O // 128) * -(-Ncols // 128)
         split = 1
         if tiles < 256:
-            split = max(1, min(-(-512 // tiles), K // (_BK[self.dt] * 4)))
+            split = max(1, min(-(-_WG_ATOMIC_UNITS // tiles), K // (_BK[self.dt] * 4)))
         conv = (3, T, KW, C) if KW > 1 else None
         ldc = C * KW
-        ns = wgrad_slices(O, Ncols, ldc, K, self.dt) if not _NO_SLICES else 1
+        ns = wgrad_slices(O, Ncols, ldc, K, self.dt, _WG_SLICE_CU) if not _NO_SLICES else 1
         if ns == 1 and _BIG_SLICES and self.dt == 1 and Ncols == ldc and O * ldc > 600_000:
             tiles = -(-O // 256) * -(-Ncols // 256)
             ns = max(1, min(-(-_SLICE_TARGET // tiles), (K // 64) // 8))
@@ -811,10 +843,10 @@ class FS2Engine:
         F, _, KW1 = self._wspecs[w1]
         P1 = (KW1 - 1) // 2
         # the FFN conv1 forward's reflect-padded X1 image, written by the LayerNorm that makes
-        # X1 (fs2_ln_fwd img).  Its 2P tail rows stay unwritten: only the dropped pad-row
-        # outputs of the last utterance read them (c_row = (T, -2P); each output row sums its
-        # own 2P+1 image rows)
-        img = self.empty(B * (T + 2 * P1) + 2 * P1, D) if self._pad_fwd(w1, M, T) else None
+        # X1 (fs2_ln_fwd img).  Its 2P tail rows are read only by the dropped pad-row outputs of
+        # the last utterance (c_row = (T, -2P); each output row sums its own 2P+1 image rows):
+        # one image per shape, reused layer after layer, its tail zeroed once at allocation
+        img = self._fwd_image(B * (T + 2 * P1), 2 * P1, D) if self._pad_fwd(w1, M, T) else None
         ops.ln_fwd(X, D, P[prefix + "norm1.norm.weight"], P[prefix + "norm1.norm.bias"], 1e-6, X1, D,
                    mean1, rstd1, M, D, dt=self.dt, seed=seed, r=Ao, ldr=D, p_r=p_drop, salt_r=s_r1,
                    s_out=s1, img=img if _LN_IMG else None, img_t=T, img_p=P1)
@@ -1304,6 +1336,10 @@ class FS2Engine:
             # on both (events), so the main stream itself never blocks on the side stream
             if self.on_grads_ready is not None:
                 self.on_grads_ready(tag, self.grad_streams())
+                if (self.dp_late is not None and self.adam_split is not None
+                        and not self._adam_late_done and self._aux is not None
+                        and self._side is not None and _ADAM_OVERLAP and self.dp_late[0]()):
+                    self._adam_launch_late(self.dp_late[1])
         d_mel = d_mel.reshape(Mm, NM).to(self.adt).contiguous()
         d_post = d_post.reshape(Mm, NM).to(self.adt).contiguous()
         d_pitch = d_pitch.reshape(Mp).to(self.adt).contiguous()

@@ -60,12 +60,37 @@ class FusedAdamW:
         ops.adamw(m._flat, m._gflat, self.exp_avg, self.exp_avg_sq, m._flat.numel(), *args)
         m.mark_params_updated()
 
+    def _layout_record(self):
+        """(name, offset, numel) of every parameter in the flat buffers the moments mirror"""
+        return [(n, int(o), int(k)) for n, o, k, _, _ in self.model._layout]
+
     def state_dict(self):
         return {"step": self.step_count, "exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq,
                 "lr": self.lr, "betas": self.betas, "eps": self.eps,
-                "weight_decay": self.weight_decay}
+                "weight_decay": self.weight_decay, "layout": self._layout_record()}
 
     def load_state_dict(self, sd):
+        """moments saved under the same flat layout load as they are; saved under another
+        layout (e.g. before a parameter-order change), each parameter's slice is moved to its
+        current offset by name -- a state without a layout record is accepted only when the
+        sizes match and no record says otherwise (older checkpoints of this layout)"""
+        lay = sd.get("layout")
+        cur = self._layout_record()
+        if lay is None or [tuple(x) for x in lay] == cur:
+            if sd["exp_avg"].numel() != self.exp_avg.numel():
+                raise ValueError("FusedAdamW state: flat size mismatch and no layout record")
+            self.exp_avg.copy_(sd["exp_avg"])
+            self.exp_avg_sq.copy_(sd["exp_avg_sq"])
+        else:
+            old = {n: (o, k) for n, o, k in lay}
+            if set(old) != {n for n, _, _ in cur}:
+                raise ValueError("FusedAdamW state: parameter names differ from this model's")
+            self.exp_avg.zero_()
+            self.exp_avg_sq.zero_()
+            for n, o, k in cur:
+                so, sk = old[n]
+                if sk != k:
+                    raise ValueError(f"FusedAdamW state: {n} has {sk} elements, model has {k}")
+                self.exp_avg[o:o + k].copy_(sd["exp_avg"][so:so + k])
+                self.exp_avg_sq[o:o + k].copy_(sd["exp_avg_sq"][so:so + k])
         self.step_count = sd["step"]
-        self.exp_avg.copy_(sd["exp_avg"])
-        self.exp_avg_sq.copy_(sd["exp_avg_sq"])

@@ -5,8 +5,10 @@
   (train.py:72-81) -- and works with ``torch.optim.AdamW`` or ``FusedAdamW``.
 * ``FusedTrainer`` is the same step without autograd bookkeeping: engine forward, fused loss,
   engine backward into the flat gradient buffer, a bucketed RCCL all-reduce (SUM, averaged in
-  the optimizer) launched per bucket as soon as the backward has produced it, then one fused
-  AdamW kernel.  One process per GPU, ``torch.distributed`` with the nccl (= RCCL) backend.
+  the optimizer) launched per bucket as soon as the backward has produced it; the fused AdamW
+  of the decoder / mel-linear / PostNet parameters runs on the aux stream during the encoder
+  backward (one process: right after the decoder; DP: once their buckets are reduced), the
+  rest after the backward (DP: after the last bucket).  One process per GPU, ``torch.distributed`` with the nccl (= RCCL) backend.
 """
 
 import os
@@ -62,21 +64,41 @@ class GradBucketer:
         self.by_tag = {}
         for i, (_, _, tag) in enumerate(self.buckets):
             self.by_tag.setdefault(tag, []).append(i)
-        self.handles = []
+        self.handles = {}          # bucket index -> async all-reduce work
         self.launched = set()
+        self.late_end = 0          # set_late(): flat end of the parameters updated early
 
     def _reduce(self, i, streams):
         s, e, _ = self.buckets[i]
         if self.comm is None:
-            self.handles.append(dist.all_reduce(self.flat[s:e], op=dist.ReduceOp.SUM,
-                                                group=self.group, async_op=True))
+            self.handles[i] = dist.all_reduce(self.flat[s:e], op=dist.ReduceOp.SUM,
+                                              group=self.group, async_op=True)
         else:
             for st in streams or [torch.cuda.current_stream(self.flat.device)]:
                 self.comm.wait_stream(st)
             with torch.cuda.stream(self.comm):
-                self.handles.append(dist.all_reduce(self.flat[s:e], op=dist.ReduceOp.SUM,
-                                                    group=self.group, async_op=True))
+                self.handles[i] = dist.all_reduce(self.flat[s:e], op=dist.ReduceOp.SUM,
+                                                  group=self.group, async_op=True)
         self.launched.add(i)
+
+    # -- the late parameters' AdamW under DP (FusedTrainer.step): the decoder / mel-linear /
+    # PostNet gradients occupy the front of the flat buffer (backward-completion order); once
+    # every bucket that holds any of them is reduced, their update may run on the engine's aux
+    # stream during the encoder backward, as the one-process step does
+    def set_late(self, end):
+        self.late_end = int(end)
+
+    def late_launched(self):
+        return self.late_end > 0 and all(i in self.launched for i, (s, _, _) in
+                                         enumerate(self.buckets) if s < self.late_end)
+
+    def wait_late(self, stream):
+        """make ``stream`` wait (stream-ordered) for the all-reduce of every bucket that holds
+        late gradients"""
+        with torch.cuda.stream(stream):
+            for i, (s, _, _) in enumerate(self.buckets):
+                if s < self.late_end:
+                    self.handles[i].wait()
 
     def ready(self, tag, streams=None):
         for i in self.by_tag.get(tag, []):
@@ -87,11 +109,11 @@ class GradBucketer:
         for i in range(len(self.buckets)):
             if i not in self.launched:   # groups that never reported (defensive)
                 self._reduce(i, streams)
-        for h in self.handles:
+        for h in self.handles.values():
             h.wait()
         if self.comm is not None:
             torch.cuda.current_stream(self.flat.device).wait_stream(self.comm)
-        self.handles, self.launched = [], set()
+        self.handles, self.launched = {}, set()
 
 
 # opt-in: measured slower on ROCm 7 / MI355X (bench A/B, profiles/r02_graph_ab.txt: B=32 21.88 ms
@@ -156,6 +178,10 @@ class FusedTrainer:
         if self.world > 1:
             self.bucketer = GradBucketer(model._gflat, model.group_ranges(), bucket_bytes)
             self.eng.on_grads_ready = self.bucketer.ready
+            # the late parameters' AdamW runs inside the backward once their buckets are
+            # reduced (engine.dp_late), as the one-process step's does after the decoder
+            self.bucketer.set_late(self.eng.late_param_end())
+            self.eng.dp_late = (self.bucketer.late_launched, self.bucketer.wait_late)
         self.seed = 0
         # DP steps stay eager: their bucketed all-reduces are issued from the backward hooks,
         # and a captured step would record none of them (its warm-up pass already fired every
@@ -210,15 +236,16 @@ class FusedTrainer:
             mlm = mel_len_max if mel_len_max is not None else batch[3].shape[1]
             loss = self._graph_for(batch, intensity, mlm).replay(batch, intensity, self.seed)
         else:
-            # one process: the AdamW scalars are fixed before the backward, which updates the
-            # decoder / PostNet parameters on the aux stream during the encoder backward
+            # the AdamW scalars are fixed before the backward, which updates the decoder /
+            # PostNet parameters on the aux stream during the encoder backward (under DP once
+            # the all-reduce of their gradient buckets is done, GradBucketer.wait_late)
             if self._torn:
                 raise RuntimeError("FusedTrainer: an earlier step failed after the decoder / "
                                    "PostNet half of its AdamW update was applied; the optimizer "
                                    "state is inconsistent -- restore it from a checkpoint")
-            split = self.bucketer is None and self.opt.fused_images()
+            split = self.opt.fused_images()
             if split:
-                scal = self.opt.begin_step(1.0)
+                scal = self.opt.begin_step(1.0 / self.world)
                 self.eng.adam_split = (self.opt, scal)
             try:
                 loss = self.forward_backward(batch, intensity, mel_len_max)
@@ -235,6 +262,8 @@ class FusedTrainer:
             finally:
                 self.eng.adam_split = None
             if split:
+                if self.bucketer is not None:
+                    self.bucketer.finish(self.eng.grad_streams())
                 self.eng.adamw_step_split(self.opt, scal)
                 return loss
         self.apply()

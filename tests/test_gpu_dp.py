@@ -3,7 +3,9 @@
 Two processes (gloo backend over GPU tensors -- RCCL cannot put two ranks on one device) each
 run ``FusedTrainer.step`` on their own shard: the engine's ``on_grads_ready`` hooks, the
 bucketed async all-reduce issued from the communication stream after it waited on the main and
-weight-gradient side streams, ``finish()`` and AdamW's ``grad_scale = 1/N``.  A single process
+weight-gradient side streams, the decoder / PostNet AdamW on the aux stream once their buckets
+are reduced (during the encoder backward, as in the one-process step), ``finish()``, the rest of
+AdamW and its ``grad_scale = 1/N``.  A single process
 then computes each shard's gradient separately with the same seeds and applies one AdamW step
 to their mean.  SURVEY 8e: the N-rank gradient equals the mean of the per-shard gradients.
 
@@ -58,6 +60,9 @@ def _worker(rank, world, port, out_dir, dtname):
     assert tr.bucketer is not None and len(tr.bucketer.buckets) > 2
     tr.step(bt, inten)
     torch.cuda.synchronize()
+    # the decoder / mel-linear / PostNet AdamW ran on the aux stream inside the backward, after
+    # the all-reduce of their buckets (the one-process schedule), not after finish()
+    assert tr.eng.n_adam_late == 1
     torch.save({"gsum": m._gflat.cpu(), "param": m._flat.cpu(),
                 "exp_avg": tr.opt.exp_avg.cpu()}, os.path.join(out_dir, f"rank{rank}.pt"))
     dist.barrier()

@@ -188,3 +188,81 @@ def test_vocoder_polyphase_transposed_conv(u):
     y = F.conv1d(x, W3, b.repeat(u), padding=1)
     y = y.reshape(2, u, O, L).permute(0, 2, 3, 1).reshape(2, O, L * u)
     torch.testing.assert_close(y, ref, rtol=1e-5, atol=1e-5)
+
+
+def _hazard_checker():
+    import importlib.util
+    p = os.path.join(ROOT, "fine-grained-emotional-control-of-tts_amd", "csrc", "check_hazards.py")
+    spec = importlib.util.spec_from_file_location("check_hazards", p)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_mfma_hazard_checker_flags_early_reads():
+    """check_hazards (run by build()): an accumulator read 3 wait states after the asm MFMA that
+    writes it is flagged, one behind an s_nop 15 / s_nop 3 drain is not, and an accumulate chain
+    on the same range needs no wait states."""
+    hz = _hazard_checker()
+    head = "0000000000001000 <_ZN12gemm_w4b_kernelILb0ELi8EEEv>:\n"
+    mfma = "  v_mfma_f32_16x16x32_bf16 a[0:3], v[0:3], v[4:7], a[0:3]\n"
+    early = head + mfma + mfma + "  v_add_u32_e32 v9, 1, v9\n  s_nop 1\n  v_accvgpr_read_b32 v10, a2\n"
+    late = head + mfma + "  s_nop 15\n  s_nop 3\n  v_accvgpr_read_b32 v10, a2\n"
+    f = hz.check(early, hz.MIN_WAIT)
+    assert len(f) == 1 and f[0][1] == 3 and "a2" in f[0][3]
+    assert hz.check(late, hz.MIN_WAIT) == []
+
+
+def test_built_objects_have_no_mfma_hazards():
+    """the gfx950 code of the built library objects passes the hazard check (skipped before a
+    build: the objects are not in the repository)"""
+    import glob
+    objs = sorted(glob.glob(os.path.join(ROOT, "fine-grained-emotional-control-of-tts_amd", "csrc",
+                                         "build", "*.o")))
+    if not objs:
+        pytest.skip("library not built")
+    hz = _hazard_checker()
+    assert hz.main(objs) == 0
+
+
+def test_fused_adamw_state_remaps_moments_by_name():
+    """FusedAdamW.state_dict records the flat layout (name, offset, numel); a state saved under
+    another parameter order (e.g. before the predictor conv1 pair moved to the front of the
+    variance group) loads with every parameter's moments at its current offset, and a state whose
+    names differ is refused instead of loading the moments onto the wrong parameters"""
+    from fastspeech2.optim import FusedAdamW
+
+    class _Packed:   # the flat-buffer view of a model (FastSpeech2 packs only on a HIP device)
+        _layout = [(f"p{i}", 16 * i * (i + 1) // 2, 16 * (i + 1), None, None) for i in range(6)]
+        _flat = torch.zeros(16 * 21)
+
+        def _ensure_packed(self):
+            pass
+
+    m = _Packed()
+    opt = FusedAdamW(m)
+    lay = opt._layout_record()
+    # an "old" layout: the first two parameters swapped in the flat buffer
+    (n0, o0, k0), (n1, o1, k1) = lay[0], lay[1]
+    old_lay = [(n1, o0, k1), (n0, o0 + k1, k0)] + [tuple(x) for x in lay[2:]]
+    old_avg = torch.zeros_like(opt.exp_avg)
+    old_sq = torch.zeros_like(opt.exp_avg_sq)
+    want_avg = torch.zeros_like(opt.exp_avg)
+    for i, (n, o, k) in enumerate(old_lay):
+        old_avg[o:o + k] = float(i + 1)
+        old_sq[o:o + k] = float(-(i + 1))
+    cur = {n: (o, k) for n, o, k in lay}
+    for i, (n, o, k) in enumerate(old_lay):
+        co, _ = cur[n]
+        want_avg[co:co + k] = float(i + 1)
+    opt.load_state_dict({"step": 7, "exp_avg": old_avg, "exp_avg_sq": old_sq, "layout": old_lay})
+    assert opt.step_count == 7
+    assert torch.equal(opt.exp_avg, want_avg) and torch.equal(opt.exp_avg_sq, -want_avg)
+    # same layout: a plain copy; round trip through state_dict
+    sd = opt.state_dict()
+    opt2 = FusedAdamW(m)
+    opt2.load_state_dict(sd)
+    assert torch.equal(opt2.exp_avg, opt.exp_avg)
+    bad = dict(sd, layout=[("nope", o, k) for _, o, k in sd["layout"]])
+    with pytest.raises(ValueError):
+        opt2.load_state_dict(bad)

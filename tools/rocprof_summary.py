@@ -11,6 +11,10 @@
         HBM bytes per launch of one kernel (dispatches matching name substring, grid size and
         a minimum duration, which separates GEMMs of the same tiling but different K)
         from two separate --pmc passes (FETCH_SIZE and WRITE_SIZE do not fit one TCC pass).
+    python tools/rocprof_summary.py pin [kind ...]
+        copy the newest committed profiles/r*_<kind>_traffic.json (default: roofline, wgrad)
+        into bench_pmc.json at the repository root, which bench.py reads on the GPU box
+        (profiles/ is not shipped there).
 
 Counter units and gfx950 corrections (MI355X_MICROARCH.md, HBM section; counter_defs.yaml):
 FETCH_SIZE and WRITE_SIZE are kilobytes (expression / 1024); on gfx950 FETCH_SIZE reports
@@ -238,6 +242,22 @@ def traffic(fdir, wdir, name_sub, grid, min_us, out=None):
     print(json.dumps(res))
 
 
+def pin(kinds=("roofline", "wgrad")):
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = {}
+    for kind in kinds:
+        hits = sorted(glob.glob(os.path.join(root, "profiles", f"r*_{kind}_traffic.json")))
+        if hits:
+            d = json.load(open(hits[-1]))
+            out[kind] = {"kernel_substr": d["kernel_substr"],
+                         "hbm_bytes_per_launch": d["hbm_bytes_per_launch"],
+                         "read_bytes_per_launch": d["read_bytes_per_launch"],
+                         "write_bytes_per_launch": d["write_bytes_per_launch"],
+                         "source": os.path.relpath(hits[-1], root)}
+    json.dump(out, open(os.path.join(root, "bench_pmc.json"), "w"), indent=1)
+    print(json.dumps(out, indent=1))
+
+
 if __name__ == "__main__":
     if sys.argv[1] == "stats":
         stats(sys.argv[2], int(sys.argv[3]), sys.argv[4] if len(sys.argv) > 4 else None)
@@ -257,5 +277,7 @@ if __name__ == "__main__":
     elif sys.argv[1] == "traffic":
         traffic(sys.argv[2], sys.argv[3], sys.argv[4], int(sys.argv[5]), float(sys.argv[6]),
                 sys.argv[7] if len(sys.argv) > 7 else None)
+    elif sys.argv[1] == "pin":
+        pin(tuple(sys.argv[2:]) or ("roofline", "wgrad"))
     else:
         raise SystemExit(__doc__)
