@@ -1851,17 +1851,22 @@ __device__ __forceinline__ void mfma_acc(f32x4& acc, const bf16x8& a, const bf16
 __device__ __forceinline__ void mfma_drain() { asm volatile("s_nop 15\n\ts_nop 3" ::: "memory"); }
 
 // epilogue of the 4-wave kernels: lane holds columns n .. n+3 (n = n0 + wn 16NF + 16 j +
-// 4 (l >> 4)) of row m = m0 + wm 128 + 16 i + (l & 15); bias, activation, c_row remap
+// 4 (l >> 4)) of row m = m0 + wm 128 + 16 i + (l & 15); bias, activation, c_row remap.  bf16
+// output: fragments j, j+1 are paired by one v_permlane16_swap per dword -- lane row g even
+// then holds columns 16 j + 4 g .. +7 and row g odd 16 (j+1) + 4 (g-1) .. +7 -- so every lane
+// stores 16 bytes per fragment pair (half the store instructions of the 8-byte form; 16-byte
+// aligned rows only, else the 8-byte stores)
 template <bool C32, int NF>
 __device__ __forceinline__ void w4_epilogue(const GemmP& p, f32x4 (&acc)[8][NF], int m0, int n0,
                                             int wm, int wn, int lane) {
-  const int g4 = (lane >> 4) * 4;
+  const int g = lane >> 4, g4 = g * 4;
   f32x4 bv[NF];
 #pragma unroll
   for (int j = 0; j < NF; ++j) {
     const int n = n0 + wn * 16 * NF + j * 16 + g4;
     bv[j] = (p.bias && n < p.nvalid) ? *(const f32x4*)(p.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
   }
+  const bool pair16 = !C32 && (NF % 2) == 0 && (p.ldc % 8) == 0 && ((uintptr_t)p.C & 15) == 0;
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int m = m0 + wm * 128 + i * 16 + (lane & 15);
@@ -1874,6 +1879,38 @@ __device__ __forceinline__ void w4_epilogue(const GemmP& p, f32x4 (&acc)[8][NF],
         const int L = p.c_row_t - p.c_row_pad, u = m / L;
         ok = ok && m - u * L < p.c_row_t;
         mo = m + u * p.c_row_pad;
+      }
+    }
+    if constexpr (!C32 && (NF % 2) == 0) {
+      if (pair16) {   // every lane takes part in the swaps; stores are guarded
+        const int odd = g & 1;
+#pragma unroll
+        for (int jj = 0; jj < NF; jj += 2) {
+          u32x2 w[2];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            f32x4 v = acc[i][jj + h] + bv[jj + h];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = epi_act(v[e], p.relu);
+            w[h][0] = (unsigned)__builtin_bit_cast(unsigned short, (bf16)v[0]) |
+                      ((unsigned)__builtin_bit_cast(unsigned short, (bf16)v[1]) << 16);
+            w[h][1] = (unsigned)__builtin_bit_cast(unsigned short, (bf16)v[2]) |
+                      ((unsigned)__builtin_bit_cast(unsigned short, (bf16)v[3]) << 16);
+          }
+#pragma unroll
+          for (int d = 0; d < 2; ++d) {
+            const auto r = __builtin_amdgcn_permlane16_swap(w[0][d], w[1][d], false, false);
+            w[0][d] = r[0];
+            w[1][d] = r[1];
+          }
+          const int n = n0 + wn * 16 * NF + (jj + odd) * 16 + 4 * (g - odd);
+          if (ok && n < p.nvalid) {
+            bf16* dst = (bf16*)p.C + (long)mo * p.ldc + n;
+            if (n + 8 <= p.nvalid) *(u32x4*)dst = u32x4{w[0][0], w[0][1], w[1][0], w[1][1]};
+            else *(u32x2*)dst = w[0];
+          }
+        }
+        continue;
       }
     }
     if (!ok) continue;
