@@ -241,6 +241,37 @@ __device__ __forceinline__ float xg_sum(float v) {
   return __builtin_bit_cast(float, (unsigned)b[0]) + __builtin_bit_cast(float, (unsigned)b[1]);
 }
 
+// Store one query row's ND 16-feature blocks (C layout: lane (l & 15) = query, features 16 d +
+// 4 g .. +3 in acc[d][qg], g = l >> 4) as bf16, scaled: blocks d, d+1 are paired by one
+// v_permlane16_swap per dword, so lane row g even holds features 16 d + 4 g .. +7 and row g odd
+// 16 (d+1) + 4 (g-1) .. +7 -- one 16-byte store per block pair instead of two 8-byte ones (the
+// 4-wave GEMM's epilogue measured 7 % faster this way).  Every lane takes part in the swaps.
+template <int ND, int QG>
+__device__ __forceinline__ void store_row_pairs(bf16* row, const f32x4 (&acc)[ND][QG], int qg,
+                                                float sc, int g, bool ok) {
+  static_assert(ND % 2 == 0, "feature blocks come in pairs");
+  const int odd = g & 1;
+#pragma unroll
+  for (int d = 0; d < ND; d += 2) {
+    u32x2 w[2];
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const f32x4 a = acc[d + hh][qg] * sc;
+      w[hh][0] = (unsigned)__builtin_bit_cast(unsigned short, (bf16)a[0]) |
+                 ((unsigned)__builtin_bit_cast(unsigned short, (bf16)a[1]) << 16);
+      w[hh][1] = (unsigned)__builtin_bit_cast(unsigned short, (bf16)a[2]) |
+                 ((unsigned)__builtin_bit_cast(unsigned short, (bf16)a[3]) << 16);
+    }
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const auto r = __builtin_amdgcn_permlane16_swap(w[0][e], w[1][e], false, false);
+      w[0][e] = r[0];
+      w[1][e] = r[1];
+    }
+    if (ok) *(u32x4*)(row + 16 * (d + odd) + 4 * (g - odd)) = u32x4{w[0][0], w[0][1], w[1][0], w[1][1]};
+  }
+}
+
 // compile-time loop: f(std::integral_constant<int, I>) for I in [I0, N)
 template <int I, int N, typename F>
 __device__ __forceinline__ void static_for(F&& f) {
@@ -523,19 +554,10 @@ __global__ void __launch_bounds__(W8 * 64 / QG, 1) attn_fwd_kernel(AttnP p) {
   for (int qg = 0; qg < QG; ++qg) {
     const float l = xg_sum(lrow[qg]);
     const float inv = p.inv_keep / l;
-    if (qi[qg] >= p.T) continue;
-    if (g == 0) p.lse[(long)z * p.T + qi[qg]] = mrow[qg] * c + log2f(l);
-    bf16* orow = p.out + ((long)b * p.T + qi[qg]) * p.ldout + h * DH;
-#pragma unroll
-    for (int d = 0; d < ND; ++d) {
-      const f32x4 a = oacc[d][qg] * inv;
-      u32x2 w;
-      w[0] = (unsigned)__builtin_bit_cast(unsigned short, (bf16)a[0]) |
-             ((unsigned)__builtin_bit_cast(unsigned short, (bf16)a[1]) << 16);
-      w[1] = (unsigned)__builtin_bit_cast(unsigned short, (bf16)a[2]) |
-             ((unsigned)__builtin_bit_cast(unsigned short, (bf16)a[3]) << 16);
-      *(u32x2*)(orow + 16 * d + 4 * g) = w;
-    }
+    const bool qok = qi[qg] < p.T;
+    if (qok && g == 0) p.lse[(long)z * p.T + qi[qg]] = mrow[qg] * c + log2f(l);
+    bf16* orow = p.out + ((long)b * p.T + (qok ? qi[qg] : 0)) * p.ldout + h * DH;
+    store_row_pairs<ND>(orow, oacc, qg, inv, g, qok);
   }
 }
 
@@ -699,18 +721,9 @@ __global__ void __launch_bounds__(W8 * 64 / QG, 1) attn_bwd_dq_kernel(AttnP p) {
   }
 #pragma unroll
   for (int qg = 0; qg < QG; ++qg) {
-    if (qi[qg] >= p.T) continue;
-    bf16* row = p.dqkv + ((long)b * p.T + qi[qg]) * p.lddq + h * DH;
-#pragma unroll
-    for (int d = 0; d < ND; ++d) {
-      const f32x4 a = qacc[d][qg] * p.scale;
-      u32x2 w;
-      w[0] = (unsigned)__builtin_bit_cast(unsigned short, (bf16)a[0]) |
-             ((unsigned)__builtin_bit_cast(unsigned short, (bf16)a[1]) << 16);
-      w[1] = (unsigned)__builtin_bit_cast(unsigned short, (bf16)a[2]) |
-             ((unsigned)__builtin_bit_cast(unsigned short, (bf16)a[3]) << 16);
-      *(u32x2*)(row + 16 * d + 4 * g) = w;
-    }
+    const bool qok = qi[qg] < p.T;
+    bf16* row = p.dqkv + ((long)b * p.T + (qok ? qi[qg] : 0)) * p.lddq + h * DH;
+    store_row_pairs<ND>(row, qacc, qg, p.scale, g, qok);
   }
 }
 
