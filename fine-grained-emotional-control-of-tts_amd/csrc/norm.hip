@@ -793,12 +793,15 @@ __global__ void __launch_bounds__(256) sum_slices_kernel(const float* ws, int ns
   ((f32x4*)out)[i] = a;
 }
 
-// rows per LayerNorm-backward block (4 waves): 32, or 16 when 32 leaves fewer than 512 blocks
-// (ln_bench, M = 6400: 20.0 -> 16.9 us; M = 31264: 38.5 vs 41.4 us with 16); FS2_LN_RPB forces
+// rows per LayerNorm-backward block (4 waves at 3 waves per SIMD): enough that the grid's
+// waves fit one round of the chip's 3 x 1024 wave slots (the decoder's M = 31264: 41 rows, 763
+// blocks -- 32 rows left a second round of 836 waves: 41.6 -> 38.8 us standalone, step 17.20 ->
+// 17.13 ms, tools/r06_probe.sh), at least 16 (M = 6400: 16.9 us; 20.0 with 8)
+// FS2_LN_RPB forces
 int ln_rpb(int M) {
   static const int r = fs2_exp_int("FS2_LN_RPB", 0);
   if (r) return std::max(4, r);
-  return (M + 31) / 32 >= 512 ? 32 : 16;
+  return std::max(16, (4 * M + 3071) / 3072);
 }
 int ln_blocks(int M) { return min(8192, max(1, (M + ln_rpb(M) - 1) / ln_rpb(M))); }
 // rows in flight per wave in the bf16 LayerNorm backward (FS2_LN_ROWS=1 selects the one-row
