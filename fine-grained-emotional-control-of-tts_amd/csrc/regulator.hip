@@ -8,6 +8,13 @@
 
 namespace {
 
+// N (a multiple of 4) fp32 values from a 16-byte aligned address
+template <int N>
+__device__ __forceinline__ void vload_f32(float* o, const float* src) {
+#pragma unroll
+  for (int q = 0; q < N / 4; ++q) vload(o + 4 * q, src + 4 * q);
+}
+
 // ---------------------------------------------------------------- embedding (K1, K2)
 template <typename T>
 __global__ void embed_fwd_kernel(const int64_t* tok, const float* table, const float* pe, int pad,
@@ -110,6 +117,87 @@ __global__ void __launch_bounds__(256) concat_bwd_utt_kernel(const T* dcat, int 
   __syncthreads();
   if (w == 0 && d < D) U[(long)b * D + d] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
 }
+// row-vector variant (wave per row, 16 B per lane; the element-wise kernel divides per element)
+template <typename T>
+__global__ void __launch_bounds__(256) concat_fwd_vec_kernel(const T* feats, const float* spk_table,
+                                                             const int64_t* spk,
+                                                             const float* inten, int T_, int D,
+                                                             int E, T* cat, int ldc, int M) {
+  constexpr int VN = Vec<T>::N;
+  const int lane = threadIdx.x & 63;
+  const int m = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (m >= M) return;
+  const float* srow = spk_table + spk[m / T_] * D;
+  for (int c = lane * VN; c < ldc; c += 64 * VN) {
+    float v[VN];
+    if (c + VN <= D) {
+      vload(v, feats + (long)m * D + c);
+    } else if (c >= D && c + VN <= 2 * D) {
+      vload_f32<VN>(v, srow + (c - D));
+    } else {
+#pragma unroll
+      for (int k = 0; k < VN; ++k) {
+        const int cc = c + k;
+        float x = 0.f;
+        if (cc < D) x = to_f(feats[(long)m * D + cc]);
+        else if (cc < 2 * D) x = srow[cc - D];
+        else if (cc < 2 * D + E) x = inten ? inten[(long)m * E + (cc - 2 * D)] : 0.f;
+        v[k] = x;
+      }
+    }
+    vstore(cat + (long)m * ldc + c, v);
+  }
+}
+
+// The vectorised row reductions below (concat, predictor head, pitch/energy embedding
+// backward) share one geometry: lane l of a wave owns the VN = 16 B / sizeof(T) adjacent
+// columns c0 = (blockIdx.y * 64 + l) * VN, so one load instruction of a wave reads a
+// 64 * VN-column row slab (1 KiB), blockIdx.y walks the slabs of a wider row and the waves of
+// a block take rows round-robin; the waves' partial sums are combined through LDS in a fixed
+// order.  The row index is wave-uniform (readfirstlane), so per-row scalars (dy, the tap
+// values a[...]) are plain uniform loads.  The earlier one-column-per-lane versions (2 B
+// loads, 32-64 dependent loads per lane) took 47-116 us in-step at M = 6400 (r06f trace).
+template <typename T>
+__device__ __forceinline__ void slab_combine_store(float (&red)[8][64 * Vec<T>::N], int nw,
+                                                   float* dst, int D, int stride, int off) {
+  // dst[col * stride + off] = fixed-order sum over the nw wave rows of red (nw = 4 or 8)
+  constexpr int SC = 64 * Vec<T>::N;
+  for (int i = threadIdx.x; i < SC; i += blockDim.x) {
+    float s = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
+    if (nw == 8) s += (red[4][i] + red[5][i]) + (red[6][i] + red[7][i]);
+    const int c = (blockIdx.y * 64 + (i & 63)) * Vec<T>::N + (i >> 6);
+    if (c < D) dst[(long)c * stride + off] = s;
+  }
+}
+
+// stage 1 (vector): U[b][d] = sum_t dcat[b,t,D+d]; grid (B, slabs), 8 waves over t
+template <typename T>
+__global__ void __launch_bounds__(512) concat_bwd_utt_vec_kernel(const T* dcat, int ldc, int T_,
+                                                                 int D, float* U) {
+  constexpr int VN = Vec<T>::N;
+  __shared__ float red[8][64 * VN];
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c0 = (blockIdx.y * 64 + lane) * VN;
+  float acc[VN];
+#pragma unroll
+  for (int k = 0; k < VN; ++k) acc[k] = 0.f;
+  if (c0 < D) {
+    const T* base = dcat + (long)blockIdx.x * T_ * ldc + D + c0;
+#pragma unroll 4
+    for (int t = wv; t < T_; t += 8) {
+      float x[VN];
+      vload(x, base + (long)t * ldc);
+#pragma unroll
+      for (int k = 0; k < VN; ++k) acc[k] += x[k];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < VN; ++k) red[wv][k * 64 + lane] = acc[k];
+  __syncthreads();
+  slab_combine_store<T>(red, 8, U + (long)blockIdx.x * D, D, 1, 0);
+}
+
 // stage 2: dspk[s][d] += sum_{b: spk[b]==s} U[b][d]  (utterance order)
 __global__ void concat_bwd_spk_kernel(const float* U, const int64_t* spk, int B, int D, int n_spk,
                                       float* dspk) {
@@ -180,6 +268,51 @@ __global__ void __launch_bounds__(256) rowdot_bwd_kernel(const T* dy, const T* u
   }
 }
 
+// vector variant: grid (row blocks, slabs), 4 waves; part as rowdot_bwd_kernel
+template <typename T>
+__global__ void __launch_bounds__(256) rowdot_bwd_vec_kernel(const T* dy, const T* u, long ldu,
+                                                             const float* w, float scale, int M,
+                                                             int D, T* du, float* part,
+                                                             int rows_per_block) {
+  constexpr int VN = Vec<T>::N, SC = 64 * VN;
+  __shared__ float red[8][SC];
+  __shared__ float gred[4];
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c0 = (blockIdx.y * 64 + lane) * VN;
+  const bool live = c0 < D;   // D % VN == 0 (host)
+  const int rbeg = blockIdx.x * rows_per_block, rend = min(M, rbeg + rows_per_block);
+  float wr[VN], acc[VN];
+#pragma unroll
+  for (int k = 0; k < VN; ++k) {
+    wr[k] = live ? w[c0 + k] : 0.f;
+    acc[k] = 0.f;
+  }
+  float gs = 0.f;
+#pragma unroll 4
+  for (int m = rbeg + wv; m < rend; m += 4) {
+    const float g = to_f(dy[m]) * scale;
+    gs += g;
+    if (live) {
+      float x[VN], o[VN];
+      vload(x, u + (long)m * ldu + c0);
+#pragma unroll
+      for (int k = 0; k < VN; ++k) {
+        acc[k] += g * x[k];
+        o[k] = g * wr[k];
+      }
+      vstore(du + (long)m * D + c0, o);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < VN; ++k) red[wv][k * 64 + lane] = acc[k];
+  if (lane == 0) gred[wv] = gs;
+  __syncthreads();
+  float* pp = part + (long)blockIdx.x * (D + 1);
+  slab_combine_store<T>(red, 4, pp, D, 1, 0);
+  if (blockIdx.y == 0 && threadIdx.x == 0) pp[D] = (gred[0] + gred[1]) + (gred[2] + gred[3]);
+}
+
 __global__ void __launch_bounds__(256) reduce_cols_kernel(const float* part, int nb, int N,
                                                           float* out, float* out2, int split) {
   // out[n] += sum_b part[b][n] for n < split; out2[n - split] += ... for n >= split.
@@ -207,44 +340,106 @@ __global__ void __launch_bounds__(256) reduce_cols_kernel(const float* part, int
 // Replicates torch CPU semantics of SB average_over_durations (App. A.10): cumsum of the
 // values accumulated in double and stored as float, cumsum of (values != 0) as int64,
 // differences gathered at the duration cumsum ends/starts, float division.
+//
+// The double cumsum is order-sensitive only when an addition rounds.  Every partial sum of
+// the row (in any grouping) is an integer multiple of 2^L, L = the lowest ulp exponent over
+// the row's non-zero values, and at most S = sum |v| in magnitude; when S < 2^(L + 52) every
+// such sum is exact in double (53-bit significand, one bit of margin for S's own rounding),
+// so a parallel scan gives the sequential result bit for bit.  Rows that fail the test (a
+// dynamic range beyond ~2^52 within one utterance, or a non-finite value) take the
+// sequential scan by one thread, as torch does.  (The sequential scan alone took 35 us per
+// call at B = 32, T_mel = 1000, r06f trace.)
 __global__ void __launch_bounds__(256) avg_over_dur_kernel(const float* vals, int Tm,
                                                            const int64_t* durs, int Tp,
                                                            float* avg, float* vcum, int* nzcum) {
-  constexpr int CH = 2048;
-  __shared__ float sv[CH];
-  __shared__ float scum[CH];
-  __shared__ int snz[CH];
+  __shared__ double sd[256];
+  __shared__ int si[256];
+  __shared__ int slo[256];
   __shared__ long long cs[1024 + 1];
-  const int b = blockIdx.x;
+  const int b = blockIdx.x, tid = threadIdx.x;
   const float* v = vals + (long)b * Tm;
   float* vc = vcum + (long)b * (Tm + 1);
   int* nc = nzcum + (long)b * (Tm + 1);
-  double acc = 0.0;
-  int cnt = 0;
-  if (threadIdx.x == 0) { vc[0] = 0.f; nc[0] = 0; }
-  for (int c0 = 0; c0 < Tm; c0 += CH) {
-    const int n = min(CH, Tm - c0);
-    for (int i = threadIdx.x; i < n; i += blockDim.x) sv[i] = v[c0 + i];
-    __syncthreads();
-    if (threadIdx.x == 0) {  // sequential: exact torch-CPU (double-accumulated) cumsum order
-      for (int i = 0; i < n; ++i) {
-        acc += (double)sv[i];
-        cnt += (sv[i] != 0.f);
-        scum[i] = (float)acc;
-        snz[i] = cnt;
-      }
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < n; i += blockDim.x) { vc[c0 + i + 1] = scum[i]; nc[c0 + i + 1] = snz[i]; }
+  // thread tid owns frames [i0, i1): row totals, |v| mass, lowest ulp exponent, non-finite flag
+  const int R = (Tm + 255) / 256;
+  const int i0 = min(Tm, tid * R), i1 = min(Tm, i0 + R);
+  double s = 0.0, sabs = 0.0;
+  int cnt = 0, lo = 1 << 20;
+  for (int i = i0; i < i1; ++i) {
+    const float x = v[i];
+    const int e = (int)((__builtin_bit_cast(uint32_t, x) >> 23) & 0xffu);
+    if (e == 255) lo = -(1 << 20);                        // inf / nan: force the fallback
+    else if (x != 0.f) lo = min(lo, e ? e - 150 : -149);
+    cnt += (x != 0.f);
+    s += (double)x;
+    sabs += fabs((double)x);
+  }
+  sd[tid] = sabs;
+  slo[tid] = lo;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) { sd[tid] += sd[tid + o]; slo[tid] = min(slo[tid], slo[tid + o]); }
     __syncthreads();
   }
-  if (threadIdx.x == 0) {
-    long long c = 0;
-    cs[0] = 0;
-    for (int p = 0; p < Tp; ++p) { c += durs[(long)b * Tp + p]; cs[p + 1] = c; }
+  const double S = sd[0];
+  const int L = slo[0];
+  const bool exact = L > -(1 << 19) && (L >= 1 << 19 || S < ldexp(1.0, min(L + 52, 1000)));
+  __syncthreads();
+  if (tid == 0) { vc[0] = 0.f; nc[0] = 0; }
+  if (exact) {
+    // inclusive Hillis-Steele scan of the per-thread totals (every partial sum exact)
+    sd[tid] = s;
+    si[tid] = cnt;
+    __syncthreads();
+    for (int o = 1; o < 256; o <<= 1) {
+      const double ds = tid >= o ? sd[tid - o] : 0.0;
+      const int di = tid >= o ? si[tid - o] : 0;
+      __syncthreads();
+      sd[tid] += ds;
+      si[tid] += di;
+      __syncthreads();
+    }
+    double acc = tid ? sd[tid - 1] : 0.0;
+    int c = tid ? si[tid - 1] : 0;
+    for (int i = i0; i < i1; ++i) {
+      const float x = v[i];
+      acc += (double)x;
+      c += (x != 0.f);
+      vc[i + 1] = (float)acc;
+      nc[i + 1] = c;
+    }
+  } else if (tid == 0) {   // sequential: exact torch-CPU (double-accumulated) cumsum order
+    double acc = 0.0;
+    int c = 0;
+    for (int i = 0; i < Tm; ++i) {
+      const float x = v[i];
+      acc += (double)x;
+      c += (x != 0.f);
+      vc[i + 1] = (float)acc;
+      nc[i + 1] = c;
+    }
+  }
+  // int64 duration cumsum (exact in any order): block scan, 256 threads x up to 4 phonemes
+  __shared__ long long dpart[256];
+  {
+    const int Rp = (Tp + 255) / 256;
+    const int q0 = min(Tp, tid * Rp), q1 = min(Tp, q0 + Rp);
+    long long loc = 0;
+    for (int p = q0; p < q1; ++p) loc += durs[(long)b * Tp + p];
+    dpart[tid] = loc;
+    __syncthreads();
+    for (int o = 1; o < 256; o <<= 1) {
+      const long long add = tid >= o ? dpart[tid - o] : 0;
+      __syncthreads();
+      dpart[tid] += add;
+      __syncthreads();
+    }
+    long long c = tid ? dpart[tid - 1] : 0;
+    if (tid == 0) cs[0] = 0;
+    for (int p = q0; p < q1; ++p) { c += durs[(long)b * Tp + p]; cs[p + 1] = c; }
   }
   __syncthreads();
-  for (int p = threadIdx.x; p < Tp; p += blockDim.x) {
+  for (int p = tid; p < Tp; p += blockDim.x) {
     long long s0 = cs[p], s1 = cs[p + 1];
     s0 = s0 < 0 ? 0 : (s0 > Tm ? Tm : s0);
     s1 = s1 < 0 ? 0 : (s1 > Tm ? Tm : s1);
@@ -269,6 +464,50 @@ __global__ void embed1d_fwd_kernel(const T* base, const float* a, const float* W
   out[i] = from_f<T>(to_f(base[i]) + s);
 }
 
+// row-vector variant: a wave walks EMB1_ROWS consecutive rows with its lanes' weight / bias
+// columns held in registers (one 16 B column vector per lane per sweep); the KW tap values
+// of a row are wave-uniform loads.  (One row per wave re-read the D x KW weights per row:
+// 24 us, slower than the element-wise kernel's 15.)
+constexpr int EMB1_ROWS = 8;
+template <typename T>
+__global__ void __launch_bounds__(256) embed1d_fwd_vec_kernel(const T* base, const float* a,
+                                                              const float* W, const float* bias,
+                                                              int T_, int D, int KW, T* out,
+                                                              int M) {
+  constexpr int VN = Vec<T>::N;
+  const int lane = threadIdx.x & 63;
+  const int m0 = (blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) * EMB1_ROWS;
+  if (m0 >= M) return;
+  const int m1 = min(M, m0 + EMB1_ROWS);
+  const int P = (KW - 1) / 2;
+  for (int c = lane * VN; c < D; c += 64 * VN) {
+    float w[8][VN], bs[VN];
+#pragma unroll
+    for (int k = 0; k < VN; ++k) {
+      bs[k] = bias[c + k];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) w[j][k] = j < KW ? W[(c + k) * KW + j] : 0.f;
+    }
+    for (int m = m0; m < m1; ++m) {
+      const int b = m / T_, t = m - b * T_;
+      float av[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) av[j] = j < KW ? a[(long)b * T_ + reflect_idx(t + j - P, T_)] : 0.f;
+      float x[VN];
+      vload(x, base + (long)m * D + c);
+#pragma unroll
+      for (int k = 0; k < VN; ++k) {
+        float s = bs[k];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (j < KW) s += w[j][k] * av[j];
+        x[k] = x[k] + s;
+      }
+      vstore(out + (long)m * D + c, x);
+    }
+  }
+}
+
 template <typename T>
 __global__ void embed1d_bwd_kernel(const T* dout, const float* a, int M, int T_, int D, int KW,
                                    int rows_per_block, float* part) {
@@ -290,6 +529,63 @@ __global__ void embed1d_bwd_kernel(const T* dout, const float* a, int M, int T_,
   pp[(long)KW * D + o] = ab;
 }
 
+// vector variant: grid (row blocks, slabs), 8 waves; part [nb][KW*D + D] holds the dW partial
+// at o*KW + j (dW's own layout) and the dbias partial at KW*D + o, so reduce_cols_kernel adds
+// both in one pass
+template <typename T>
+__global__ void __launch_bounds__(512) embed1d_bwd_vec_kernel(const T* dout, const float* a, int M,
+                                                              int T_, int D, int KW,
+                                                              int rows_per_block, float* part) {
+  constexpr int VN = Vec<T>::N;
+  __shared__ float red[8][64 * VN];
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c0 = (blockIdx.y * 64 + lane) * VN;
+  const bool live = c0 < D;
+  const int P = (KW - 1) / 2;
+  const int rbeg = blockIdx.x * rows_per_block, rend = min(M, rbeg + rows_per_block);
+  float acc[8][VN], ab[VN];
+#pragma unroll
+  for (int k = 0; k < VN; ++k) {
+    ab[k] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j][k] = 0.f;
+  }
+#pragma unroll 2
+  for (int m = rbeg + wv; m < rend; m += 8) {
+    const int b = m / T_, t = m - b * T_;
+    float x[VN];
+    if (live) vload(x, dout + (long)m * D + c0);
+    else {
+#pragma unroll
+      for (int k = 0; k < VN; ++k) x[k] = 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < VN; ++k) ab[k] += x[k];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (j < KW) {
+        const float av = a[(long)b * T_ + reflect_idx(t + j - P, T_)];
+#pragma unroll
+        for (int k = 0; k < VN; ++k) acc[j][k] += x[k] * av;
+      }
+    }
+  }
+  float* pp = part + (long)blockIdx.x * (KW + 1) * D;
+#pragma unroll
+  for (int j = 0; j <= 8; ++j) {
+    if (j <= KW) {   // block-uniform
+      if (j) __syncthreads();   // the previous round's readers are done with red
+#pragma unroll
+      for (int k = 0; k < VN; ++k)
+        red[wv][k * 64 + lane] = (j == KW) ? ab[k] : acc[j < 8 ? j : 7][k];
+      __syncthreads();
+      if (j == KW) slab_combine_store<T>(red, 8, pp + (long)KW * D, D, 1, 0);
+      else slab_combine_store<T>(red, 8, pp, D, KW, j);
+    }
+  }
+}
+
 __global__ void embed1d_reduce_kernel(const float* part, int nb, int D, int KW, float* dW,
                                       float* dbias) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;  // i over (KW+1)*D
@@ -302,22 +598,47 @@ __global__ void embed1d_reduce_kernel(const float* part, int nb, int D, int KW, 
 }
 
 // ---------------------------------------------------------------- LengthRegulator (K11)
+// durations -> frame counts -> int64 cumsum: an integer scan, exact in any order, so a block
+// scan over 256 threads x up to 4 phonemes (T_p <= 1024) replaces the one-thread loop (18 us)
 template <typename DT>
-__global__ void lr_index_kernel(const DT* durs, float pace, int Tp, int Tm, int64_t* mel_len,
-                                int32_t* cum, int32_t* frame_src) {
-  const int b = blockIdx.x;
+__global__ void __launch_bounds__(256) lr_index_kernel(const DT* durs, float pace, int Tp, int Tm,
+                                                       int64_t* mel_len, int32_t* cum,
+                                                       int32_t* frame_src) {
+  const int b = blockIdx.x, tid = threadIdx.x;
   __shared__ int32_t cs[1024];
-  if (threadIdx.x == 0) {
-    int64_t c = 0;
-    for (int p = 0; p < Tp; ++p) {
+  __shared__ long long part[256];
+  const int R = (Tp + 255) / 256;   // <= 4 (host: Tp <= 1024)
+  const int p0 = min(Tp, tid * R), p1 = min(Tp, p0 + R);
+  long long loc[4], sum = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    long long d = 0;
+    if (p0 + k < p1) {
       // torch: (pace * durs).long() -- float32 product, truncation toward zero
-      const float prod = pace * (float)durs[(long)b * Tp + p];
-      c += (int64_t)prod;
-      cs[p] = (int32_t)c;
-      cum[(long)b * Tp + p] = (int32_t)c;
+      const float prod = pace * (float)durs[(long)b * Tp + p0 + k];
+      d = (long long)prod;
     }
-    mel_len[b] = c;
+    loc[k] = d;
+    sum += d;
   }
+  part[tid] = sum;
+  __syncthreads();
+  for (int o = 1; o < 256; o <<= 1) {
+    const long long add = tid >= o ? part[tid - o] : 0;
+    __syncthreads();
+    part[tid] += add;
+    __syncthreads();
+  }
+  long long c = tid ? part[tid - 1] : 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (p0 + k < p1) {
+      c += loc[k];
+      cs[p0 + k] = (int32_t)c;
+      cum[(long)b * Tp + p0 + k] = (int32_t)c;
+    }
+  }
+  if (tid == 255) mel_len[b] = part[255];
   __syncthreads();
   if (!frame_src) return;  // lengths-only pass (host learns T_mel before sizing buffers)
   const int total = Tp > 0 ? cs[Tp - 1] : 0;
@@ -367,6 +688,68 @@ __global__ void lr_scatter_kernel(const T* dY, const int32_t* cum, const float* 
   }
 }
 
+// Row-vector variants: one wave per frame row (gather) / phoneme row (scatter), 16 B per lane
+// along the features, so the row index and its divisions are wave-uniform; same per-element
+// arithmetic (and summation order) as the element-wise kernels above.  The element-wise gather
+// spent most of its 28 us on two 64-bit divisions per element.
+template <typename T>
+__global__ void __launch_bounds__(256) lr_gather_vec_kernel(const T* X, const int32_t* fsrc,
+                                                            const float* pe, int Tp, int Tm,
+                                                            int D, T* Y, float* keep, int Mm) {
+  constexpr int VN = Vec<T>::N;
+  const int lane = threadIdx.x & 63;
+  const int m = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (m >= Mm) return;
+  const int b = m / Tm, t = m - b * Tm;
+  const int src = fsrc[m];
+  const T* xr = X + ((long)b * Tp + (src >= 0 ? src : 0)) * D;
+  const float* pr = pe + (long)t * D;
+  T* yr = Y + (long)m * D;
+  for (int c = lane * VN; c < D; c += 64 * VN) {
+    float v[VN];
+    if (src >= 0) {
+      float p[VN];
+      vload(v, xr + c);
+      vload_f32<VN>(p, pr + c);
+#pragma unroll
+      for (int k = 0; k < VN; ++k) v[k] += p[k];
+    } else {
+#pragma unroll
+      for (int k = 0; k < VN; ++k) v[k] = 0.f;
+    }
+    vstore(yr + c, v);
+  }
+  if (lane == 0 && keep) keep[m] = src >= 0 ? 1.f : 0.f;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) lr_scatter_vec_kernel(const T* dY, const int32_t* cum,
+                                                             const float* keep, int Tp, int Tm,
+                                                             int D, T* dX, int Mp) {
+  constexpr int VN = Vec<T>::N;
+  const int lane = threadIdx.x & 63;
+  const int bp = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (bp >= Mp) return;
+  const int b = bp / Tp, p = bp - b * Tp;
+  int t0 = p > 0 ? cum[bp - 1] : 0, t1 = cum[bp];
+  t0 = min(t0, Tm);
+  t1 = min(t1, Tm);
+  for (int c = lane * VN; c < D; c += 64 * VN) {
+    float s[VN];
+#pragma unroll
+    for (int k = 0; k < VN; ++k) s[k] = 0.f;
+    for (int t = t0; t < t1; ++t) {
+      const long m = (long)b * Tm + t;
+      const float kk = keep[m];
+      float x[VN];
+      vload(x, dY + m * D + c);
+#pragma unroll
+      for (int k = 0; k < VN; ++k) s[k] += x[k] * kk;
+    }
+    vstore(dX + (long)bp * D + c, s);
+  }
+}
+
 // ---------------------------------------------------------------- utilities
 template <typename T>
 __global__ void fill_kernel(T* X, long n, float v) {
@@ -397,6 +780,15 @@ inline unsigned nblk(long n, int bs = 256) { return (unsigned)((n + bs - 1) / bs
     else return FS2_EINVAL;                                 \
     FS2_CHECK_LAUNCH();                                     \
   } while (0)
+
+// the vectorised row kernels: rows of D columns at a 16-byte aligned base and a
+// row pitch of whole 16-byte vectors
+static bool vec_rows_ok(int dtype, int D, long ld, const void* p0, const void* p1) {
+  const int vn = dtype == FS2_BF16 ? 8 : 4;
+  return D % vn == 0 && ld % vn == 0 && ((uintptr_t)p0 & 15) == 0 && ((uintptr_t)p1 & 15) == 0;
+}
+static int slabs(int dtype, int D) { const int sc = 64 * (dtype == FS2_BF16 ? 8 : 4); return (D + sc - 1) / sc; }
+
 
 extern "C" int fs2_embed_fwd(const int64_t* tokens, const float* table, const float* pe,
                              int pad_idx, int B, int T, int D, void* X, float* keep, int dtype,
@@ -461,6 +853,13 @@ extern "C" int fs2_concat_fwd(const void* feats, const float* spk_table, const i
   if (n >= 0x7fffffffL) return FS2_EINVAL;   // 32-bit element index
   if (!feats || !spk_table || !spk || !cat || ldc < 2 * D + E) return FS2_EINVAL;
   hipStream_t s = (hipStream_t)stream;
+  if (vec_rows_ok(dtype, D, ldc, feats, cat) && ((uintptr_t)spk_table & 15) == 0) {
+    const int M = B * T;
+    DISPATCH_T(dtype,
+      hipLaunchKernelGGL(concat_fwd_vec_kernel<bf16>, dim3((M + 3) / 4), dim3(256), 0, s, (const bf16*)feats, spk_table, spk, intensity, T, D, E, (bf16*)cat, ldc, M),
+      hipLaunchKernelGGL(concat_fwd_vec_kernel<float>, dim3((M + 3) / 4), dim3(256), 0, s, (const float*)feats, spk_table, spk, intensity, T, D, E, (float*)cat, ldc, M));
+    return 0;
+  }
   DISPATCH_T(dtype,
     hipLaunchKernelGGL(concat_fwd_kernel<bf16>, dim3(nblk(n)), dim3(256), 0, s, (const bf16*)feats, spk_table, spk, intensity, T, D, E, (bf16*)cat, ldc, n),
     hipLaunchKernelGGL(concat_fwd_kernel<float>, dim3(nblk(n)), dim3(256), 0, s, (const float*)feats, spk_table, spk, intensity, T, D, E, (float*)cat, ldc, n));
@@ -473,6 +872,16 @@ extern "C" int fs2_concat_bwd_spk(const void* dcat, int ldc, const int64_t* spk,
   if (n_spk == 0 || D == 0 || B == 0) return 0;
   if (!dcat || !spk || !dspk || !workspace) return FS2_EINVAL;
   hipStream_t s = (hipStream_t)stream;
+  if (vec_rows_ok(dtype, D, ldc, dcat, (const char*)dcat + (long)D * (dtype == FS2_BF16 ? 2 : 4))) {
+    dim3 grid(B, slabs(dtype, D));
+    DISPATCH_T(dtype,
+      hipLaunchKernelGGL(concat_bwd_utt_vec_kernel<bf16>, grid, dim3(512), 0, s, (const bf16*)dcat, ldc, T, D, workspace),
+      hipLaunchKernelGGL(concat_bwd_utt_vec_kernel<float>, grid, dim3(512), 0, s, (const float*)dcat, ldc, T, D, workspace));
+    hipLaunchKernelGGL(concat_bwd_spk_kernel, dim3(nblk((long)n_spk * D)), dim3(256), 0, s,
+                       workspace, spk, B, D, n_spk, dspk);
+    FS2_CHECK_LAUNCH();
+    return 0;
+  }
   dim3 grid(B, (D + 63) / 64);
   DISPATCH_T(dtype,
     hipLaunchKernelGGL(concat_bwd_utt_kernel<bf16>, grid, dim3(256), 0, s, (const bf16*)dcat, ldc, T, D, workspace),
@@ -529,9 +938,16 @@ extern "C" int fs2_rowdot_bwd(const void* dy, const void* u, int64_t ldu, const 
   hipStream_t s = (hipStream_t)stream;
   const int nb = min(256, max(1, (M + 31) / 32));
   const int rpb = (M + nb - 1) / nb;
-  DISPATCH_T(dtype,
+  if (vec_rows_ok(dtype, D, ldu, u, du)) {
+    dim3 grid(nb, slabs(dtype, D));
+    DISPATCH_T(dtype,
+      hipLaunchKernelGGL(rowdot_bwd_vec_kernel<bf16>, grid, dim3(256), 0, s, (const bf16*)dy, (const bf16*)u, ldu, w, scale, M, D, (bf16*)du, workspace, rpb),
+      hipLaunchKernelGGL(rowdot_bwd_vec_kernel<float>, grid, dim3(256), 0, s, (const float*)dy, (const float*)u, ldu, w, scale, M, D, (float*)du, workspace, rpb));
+  } else {
+    DISPATCH_T(dtype,
     hipLaunchKernelGGL(rowdot_bwd_kernel<bf16>, dim3(nb), dim3(256), 0, s, (const bf16*)dy, (const bf16*)u, ldu, w, scale, M, D, (bf16*)du, workspace, rpb),
     hipLaunchKernelGGL(rowdot_bwd_kernel<float>, dim3(nb), dim3(256), 0, s, (const float*)dy, (const float*)u, ldu, w, scale, M, D, (float*)du, workspace, rpb));
+  }
   hipLaunchKernelGGL(reduce_cols_kernel, dim3((D + 1 + 15) / 16), dim3(256), 0, s, workspace, nb,
                      D + 1, dw, db, D);
   FS2_CHECK_LAUNCH();
@@ -560,6 +976,13 @@ extern "C" int fs2_embed1d_fwd(const void* base, const float* a, const float* W,
   if (n >= 0x7fffffffL) return FS2_EINVAL;   // 32-bit element index
   if (!base || !a || !W || !bias || !out || KW > 8 || (KW - 1) / 2 >= T) return FS2_EINVAL;
   hipStream_t s = (hipStream_t)stream;
+  if (vec_rows_ok(dtype, D, D, base, out)) {
+    const int M = B * T;
+    DISPATCH_T(dtype,
+      hipLaunchKernelGGL(embed1d_fwd_vec_kernel<bf16>, dim3((M + 4 * EMB1_ROWS - 1) / (4 * EMB1_ROWS)), dim3(256), 0, s, (const bf16*)base, a, W, bias, T, D, KW, (bf16*)out, M),
+      hipLaunchKernelGGL(embed1d_fwd_vec_kernel<float>, dim3((M + 4 * EMB1_ROWS - 1) / (4 * EMB1_ROWS)), dim3(256), 0, s, (const float*)base, a, W, bias, T, D, KW, (float*)out, M));
+    return 0;
+  }
   DISPATCH_T(dtype,
     hipLaunchKernelGGL(embed1d_fwd_kernel<bf16>, dim3(nblk(n)), dim3(256), 0, s, (const bf16*)base, a, W, bias, T, D, KW, (bf16*)out, n),
     hipLaunchKernelGGL(embed1d_fwd_kernel<float>, dim3(nblk(n)), dim3(256), 0, s, (const float*)base, a, W, bias, T, D, KW, (float*)out, n));
@@ -575,6 +998,15 @@ extern "C" int fs2_embed1d_bwd(const void* dout, const float* a, int B, int T, i
   hipStream_t s = (hipStream_t)stream;
   const int nb = min(128, max(1, (M + 63) / 64));
   const int rpb = (M + nb - 1) / nb;
+  if (vec_rows_ok(dtype, D, D, dout, dout)) {
+    DISPATCH_T(dtype,
+      hipLaunchKernelGGL(embed1d_bwd_vec_kernel<bf16>, dim3(nb, slabs(dtype, D)), dim3(512), 0, s, (const bf16*)dout, a, M, T, D, KW, rpb, workspace),
+      hipLaunchKernelGGL(embed1d_bwd_vec_kernel<float>, dim3(nb, slabs(dtype, D)), dim3(512), 0, s, (const float*)dout, a, M, T, D, KW, rpb, workspace));
+    hipLaunchKernelGGL(reduce_cols_kernel, dim3(((KW + 1) * D + 15) / 16), dim3(256), 0, s,
+                       workspace, nb, (KW + 1) * D, dW, dbias, KW * D);
+    FS2_CHECK_LAUNCH();
+    return 0;
+  }
   dim3 grid((D + 255) / 256, nb);
   DISPATCH_T(dtype,
     hipLaunchKernelGGL(embed1d_bwd_kernel<bf16>, grid, dim3(256), 0, s, (const bf16*)dout, a, M, T, D, KW, rpb, workspace),
@@ -607,6 +1039,13 @@ extern "C" int fs2_lr_gather(const void* X, const int32_t* frame_src, const floa
   if (n == 0) return 0;
   if (!X || !frame_src || !pe || !Y) return FS2_EINVAL;
   hipStream_t s = (hipStream_t)stream;
+  const long Mm = (long)B * Tm;
+  if (Mm < 0x7fffffffL && vec_rows_ok(dtype, D, D, X, Y) && ((uintptr_t)pe & 15) == 0) {
+    DISPATCH_T(dtype,
+      hipLaunchKernelGGL(lr_gather_vec_kernel<bf16>, dim3((Mm + 3) / 4), dim3(256), 0, s, (const bf16*)X, frame_src, pe, Tp, Tm, D, (bf16*)Y, keep, (int)Mm),
+      hipLaunchKernelGGL(lr_gather_vec_kernel<float>, dim3((Mm + 3) / 4), dim3(256), 0, s, (const float*)X, frame_src, pe, Tp, Tm, D, (float*)Y, keep, (int)Mm));
+    return 0;
+  }
   DISPATCH_T(dtype,
     hipLaunchKernelGGL(lr_gather_kernel<bf16>, dim3(nblk(n)), dim3(256), 0, s, (const bf16*)X, frame_src, pe, Tp, Tm, D, (bf16*)Y, keep, n),
     hipLaunchKernelGGL(lr_gather_kernel<float>, dim3(nblk(n)), dim3(256), 0, s, (const float*)X, frame_src, pe, Tp, Tm, D, (float*)Y, keep, n));
@@ -618,6 +1057,13 @@ extern "C" int fs2_lr_scatter(const void* dY, const int32_t* cum, const float* k
   if ((long)B * Tp == 0) return 0;
   if (!dY || !cum || !keep || !dX) return FS2_EINVAL;
   hipStream_t s = (hipStream_t)stream;
+  if (vec_rows_ok(dtype, D, D, dY, dX)) {
+    const int Mp = B * Tp;
+    DISPATCH_T(dtype,
+      hipLaunchKernelGGL(lr_scatter_vec_kernel<bf16>, dim3((Mp + 3) / 4), dim3(256), 0, s, (const bf16*)dY, cum, keep, Tp, Tm, D, (bf16*)dX, Mp),
+      hipLaunchKernelGGL(lr_scatter_vec_kernel<float>, dim3((Mp + 3) / 4), dim3(256), 0, s, (const float*)dY, cum, keep, Tp, Tm, D, (float*)dX, Mp));
+    return 0;
+  }
   DISPATCH_T(dtype,
     hipLaunchKernelGGL(lr_scatter_kernel<bf16>, dim3(B * Tp), dim3(128), 0, s, (const bf16*)dY, cum, keep, Tp, Tm, D, (bf16*)dX),
     hipLaunchKernelGGL(lr_scatter_kernel<float>, dim3(B * Tp), dim3(128), 0, s, (const float*)dY, cum, keep, Tp, Tm, D, (float*)dX));

@@ -267,6 +267,94 @@ def test_length_regulator_bit_exact(cuda, golden_dir, pace):
     assert torch.equal(dX.cpu().view(B, Tp, D), X.cpu().view(B, Tp, D) * torch.from_numpy(n)[..., None].float())
 
 
+@pytest.mark.parametrize("dt,code", [(torch.float32, 0), (torch.bfloat16, 1)])
+@pytest.mark.parametrize("B,Tp,D", [(32, 200, 384), (3, 1024, 1104), (2, 999, 20), (5, 7, 36)])
+def test_length_regulator_rows(cuda, dt, code, B, Tp, D):
+    """LengthRegulator index / gather / scatter at the bench shape and at the edges of the
+    row-vector kernels: T_p = 1024 (four phonemes per scan thread) with rows of more than one
+    64-lane column sweep (D = 1104), D = 20 (bf16: the element-wise fallback) and D = 36.
+    lr_index against the oracle bit for bit; gather exact (a copy plus the fp32 positional
+    row, rounded once); scatter against an fp32 segment sum in frame order (rel 1e-6 in fp32,
+    one bf16 rounding in bf16)."""
+    from fastspeech2 import ops
+    from oracle.lr_oracle import lr_index_np
+    g = torch.Generator().manual_seed(B * Tp + D)
+    d = torch.randint(0, 9, (B, Tp), generator=g)
+    d[0, Tp // 2:] = 0
+    ml_ref, fs_ref = lr_index_np(d.numpy(), 1.0)
+    Tm = fs_ref.shape[1]
+    dc = d.to(cuda)
+    ml = torch.empty(B, dtype=torch.int64, device=cuda)
+    cum = torch.empty(B, Tp, dtype=torch.int32, device=cuda)
+    fs = torch.empty(B, Tm, dtype=torch.int32, device=cuda)
+    ops.lr_index(dc, 0, 1.0, B, Tp, Tm, ml, cum, fs)
+    np.testing.assert_array_equal(ml.cpu().numpy(), ml_ref)
+    np.testing.assert_array_equal(fs.cpu().numpy(), fs_ref)
+    assert torch.equal(cum.cpu().long(), d.cumsum(1))
+    X = torch.randn(B * Tp, D, generator=g).to(dt).to(cuda)
+    pe = torch.randn(Tm, D, generator=g).to(cuda)
+    Y = torch.empty(B * Tm, D, device=cuda, dtype=dt)
+    keep = torch.empty(B * Tm, device=cuda)
+    ops.lr_gather(X, fs, pe, B, Tp, Tm, D, Y, keep, dt=code)
+    fsl = fs.long().view(B, Tm)
+    valid = fsl >= 0
+    src = (torch.arange(B, device=cuda)[:, None] * Tp + fsl.clamp(min=0)).view(-1)
+    ref = ((X.float()[src].view(B, Tm, D) + pe[None]) * valid[..., None]).to(dt)
+    assert torch.equal(Y.view(B, Tm, D), ref)
+    assert torch.equal(keep.view(B, Tm), valid.float())
+    dY = torch.randn(B * Tm, D, generator=g).to(dt).to(cuda)
+    dX = torch.empty(B * Tp, D, device=cuda, dtype=dt)
+    ops.lr_scatter(dY, cum, keep, B, Tp, Tm, D, dX, dt=code)
+    seg = (torch.arange(B, device=cuda)[:, None] * Tp + fsl.clamp(min=0)).view(-1)
+    w = (dY.float() * keep[:, None])[valid.view(-1)]
+    ref = torch.zeros(B * Tp, D, device=cuda).index_add_(0, seg[valid.view(-1)], w)
+    assert rel(dX, ref.to(dt)) < (1e-6 if dt == torch.float32 else 1e-2)
+
+
+@pytest.mark.parametrize("dt,code", [(torch.float32, 0), (torch.bfloat16, 1)])
+@pytest.mark.parametrize("B,T,D,E,ldc", [(32, 200, 384, 5, 776), (3, 17, 1104, 0, 2208),
+                                         (2, 9, 20, 3, 48), (2, 9, 21, 2, 44)])
+def test_concat_fwd(cuda, dt, code, B, T, D, E, ldc):
+    """fs2_concat_fwd (model.py:352-358): cat = [feats, spk_emb[spk[b]], intensity, 0-pad] per
+    row, exact.  Bench shape (ldc padded to a 16-element multiple), rows wider than one
+    64-lane sweep, D = 20 (bf16: element-wise fallback) and D = 21 (odd: fallback in both)."""
+    from fastspeech2 import ops
+    torch.manual_seed(B * T + D)
+    feats = torch.randn(B * T, D, device=cuda).to(dt)
+    table = torch.randn(4, D, device=cuda)
+    spk = torch.randint(0, 4, (B,), device=cuda)
+    inten = torch.rand(B * T, E, device=cuda) if E else None
+    cat = torch.full((B * T, ldc), 7.0, device=cuda, dtype=dt)
+    ops.concat_fwd(feats, table, spk, inten, B, T, D, E, cat, ldc, dt=code)
+    ref = torch.zeros(B * T, ldc, device=cuda)
+    ref[:, :D] = feats.float()
+    ref[:, D:2 * D] = table[spk].repeat_interleave(T, 0)
+    if E:
+        ref[:, 2 * D:2 * D + E] = inten
+    assert torch.equal(cat, ref.to(dt))
+
+
+@pytest.mark.parametrize("dt,code", [(torch.float32, 0), (torch.bfloat16, 1)])
+@pytest.mark.parametrize("B,T,D,KW", [(32, 200, 384, 3), (3, 37, 1104, 5), (2, 9, 20, 8),
+                                      (4, 5, 36, 1)])
+def test_embed1d_fwd(cuda, dt, code, B, T, D, KW):
+    """fs2_embed1d_fwd (pitch / energy embedding conv fused with the residual add, model.py:
+    226-240,384-403) against torch's reflect-padded conv1d in fp32 (rel 1e-6 in fp32, one bf16
+    rounding in bf16)."""
+    from fastspeech2 import ops
+    torch.manual_seed(B * T + D + KW)
+    a = torch.randn(B, T, device=cuda)
+    base = torch.randn(B * T, D, device=cuda).to(dt)
+    W = torch.randn(D, KW, device=cuda)
+    bias = torch.randn(D, device=cuda)
+    out = torch.empty(B * T, D, device=cuda, dtype=dt)
+    ops.embed1d_fwd(base, a, W, bias, B, T, D, KW, out, dt=code)
+    P = (KW - 1) // 2
+    x = F.pad(a[:, None, :], (P, KW - 1 - P), mode="reflect") if KW > 1 else a[:, None, :]
+    y = F.conv1d(x, W[:, None, :], bias).transpose(1, 2).reshape(B * T, D)
+    assert rel(out, (base.float() + y).to(dt)) < (1e-6 if dt == torch.float32 else 1e-2)
+
+
 def test_length_regulator_float_durations(cuda, golden_dir):
     from fastspeech2 import ops
     g = np.load(os.path.join(golden_dir, "lr_kat.npz"))
@@ -290,6 +378,36 @@ def test_avg_over_durations_bit_exact(cuda, golden_dir):
     out = torch.empty(B, Tp, device=cuda)
     ops.avg_over_durations(v, Tm, d, B, Tp, out, torch.empty(int(ops.avg_ws(B, Tm)), device=cuda))
     np.testing.assert_array_equal(out.cpu().numpy(), g["avg"])
+
+
+@pytest.mark.parametrize("kind", ["pitch", "wide", "nonfinite", "zeros"])
+def test_avg_over_durations_scan_paths(cuda, kind):
+    """fs2_avg_over_durations at the bench shape (B = 32, T_mel = 1000, T_p = 200) against the
+    oracle (oracle/lr_oracle.py, torch-CPU sequential double cumsum), bit for bit, through both
+    scan paths: "pitch" (normalised values, ~30 % unvoiced zeros: the exactness-gated parallel
+    scan), "wide" (rows mixing 1e30 and 1e-30: additions round, so the gate sends them to the
+    sequential scan), "nonfinite" (an inf / nan row: sequential), "zeros" (all-zero rows)."""
+    from fastspeech2 import ops
+    from oracle.lr_oracle import avg_over_durations_np
+    rng = np.random.default_rng({"pitch": 1, "wide": 2, "nonfinite": 3, "zeros": 4}[kind])
+    B, Tm, Tp = 32, 1000, 200
+    v = rng.standard_normal((B, Tm)).astype(np.float32)
+    v[rng.random((B, Tm)) < 0.3] = 0.0
+    if kind == "wide":
+        v[::2, ::7] *= np.float32(1e30)
+        v[::2, 3::7] *= np.float32(1e-30)
+    elif kind == "nonfinite":
+        v[3, 10] = np.inf
+        v[5, 20] = np.nan
+        v[7, 30], v[7, 31] = np.inf, -np.inf
+    elif kind == "zeros":
+        v[::3] = 0.0
+    d = rng.integers(0, 9, (B, Tp)).astype(np.int64)
+    d[1, 150:] = 0
+    out = torch.empty(B, Tp, device=cuda)
+    ops.avg_over_durations(torch.from_numpy(v).to(cuda), Tm, torch.from_numpy(d).to(cuda), B, Tp,
+                           out, torch.empty(int(ops.avg_ws(B, Tm)), device=cuda))
+    np.testing.assert_array_equal(out.cpu().numpy(), avg_over_durations_np(v, d))
 
 
 @pytest.mark.parametrize("dt,B,Tp,ties", [(torch.float32, 3, 20, False), (torch.bfloat16, 3, 20, False),
@@ -1208,10 +1326,13 @@ def test_embedding_fwd_bwd(cuda, dt, code, B, T, V):
 
 
 @pytest.mark.parametrize("dt,code", [(torch.float32, 0), (torch.bfloat16, 1)])
-@pytest.mark.parametrize("M,D,ldu", [(6400, 384, 384), (999, 256, 264)])
+@pytest.mark.parametrize("M,D,ldu", [(6400, 384, 384), (999, 256, 264), (777, 200, 203),
+                                     (130, 1104, 1112)])
 def test_rowdot_bwd(cuda, dt, code, M, D, ldu):
     """fs2_rowdot_bwd (the variance predictors' 384 -> 1 head): du = dy * scale * w per row,
-    dw / db = fixed-order column partials; against torch fp32 on the same values."""
+    dw / db = fixed-order column partials; against torch fp32 on the same values.  The bench
+    shape, a ragged one, an odd pitch (ldu = 203: the one-column-per-lane fallback) and a row
+    wider than one 64 x 16 B column slab (grid.y = 3 / 5 slabs)."""
     from fastspeech2 import ops
     torch.manual_seed(M + D)
     u = torch.randn(M, ldu, device=cuda).to(dt)
@@ -1226,6 +1347,58 @@ def test_rowdot_bwd(cuda, dt, code, M, D, ldu):
     assert rel(du, (g[:, None] * w[None, :]).to(dt)) < (1e-6 if dt == torch.float32 else 1e-2)
     assert rel(dw, (g[:, None] * u[:, :D].float()).sum(0)) < 1e-5
     assert abs(db.item() - g.sum().item()) <= 1e-4 * max(1.0, abs(g.sum().item()))
+
+
+@pytest.mark.parametrize("dt,code", [(torch.float32, 0), (torch.bfloat16, 1)])
+@pytest.mark.parametrize("B,T,D,KW", [(32, 200, 384, 3), (3, 37, 256, 5), (2, 9, 1104, 8),
+                                      (5, 17, 201, 1), (1, 4, 64, 7)])
+def test_embed1d_bwd(cuda, dt, code, B, T, D, KW):
+    """fs2_embed1d_bwd (pitch / energy embedding conv, SB Conv1d(1 -> D, k, reflect) weight and
+    bias gradients, model.py:226-240): dW[o][j] += sum dOut[b,t,o] a[b, refl(t+j-P)], dbias
+    += sum dOut, against torch autograd of the same conv in fp32 on the same (rounded) dOut.
+    Bench shape (M = 6400, D = 384, k = 3), ragged rows, a row of three 16 B slabs, D = 201
+    (odd: the one-column-per-lane fallback), k = 1 and k = 7 / 8 with T just above the reflect
+    pad."""
+    from fastspeech2 import ops
+    torch.manual_seed(B * T + D + KW)
+    M = B * T
+    a = torch.randn(B, T, device=cuda)
+    dout = torch.randn(M, D, device=cuda).to(dt)
+    dW = torch.full((D, KW), 0.25, device=cuda)
+    db = torch.full((D,), -0.5, device=cuda)
+    ws = torch.empty(128 * (KW + 1) * D, device=cuda)
+    ops.embed1d_bwd(dout, a, B, T, D, KW, dW, db, dt=code, ws=ws)
+    P = (KW - 1) // 2
+    W = torch.zeros(D, 1, KW, device=cuda, requires_grad=True)
+    bias = torch.zeros(D, device=cuda, requires_grad=True)
+    x = F.pad(a[:, None, :], (P, KW - 1 - P), mode="reflect") if KW > 1 else a[:, None, :]
+    y = F.conv1d(x, W, bias)                                   # [B][D][T]
+    y.backward(dout.float().reshape(B, T, D).transpose(1, 2))
+    assert rel(dW - 0.25, W.grad[:, 0, :]) < 1e-5
+    assert rel(db + 0.5, bias.grad) < 1e-5
+
+
+@pytest.mark.parametrize("dt,code", [(torch.float32, 0), (torch.bfloat16, 1)])
+@pytest.mark.parametrize("B,T,D,n_spk", [(32, 200, 384, 4), (3, 37, 256, 2), (4, 11, 1104, 3),
+                                         (2, 5, 201, 5)])
+def test_concat_bwd_spk(cuda, dt, code, B, T, D, n_spk):
+    """fs2_concat_bwd_spk (speaker-embedding gradient of the conditioning concat, model.py:
+    352-358): dSpk[spk[b]] += sum_t dcat[b,t,D:2D] in utterance order, against torch index_add
+    in fp32.  Bench shape, ragged, three 16 B slabs per row, and D = 201 (odd pitch: the
+    one-column-per-lane fallback); speaker 0 of n_spk = 5 gets no utterance in the last case
+    (its row must stay as it was)."""
+    from fastspeech2 import ops
+    torch.manual_seed(B * T + D)
+    dcat = torch.randn(B * T, 2 * D, device=cuda).to(dt)
+    spk = torch.randint(1 if n_spk > 4 else 0, n_spk, (B,), device=cuda)
+    dspk = torch.full((n_spk, D), 0.5, device=cuda)
+    ws = torch.empty(B * D, device=cuda)
+    ops.concat_bwd_spk(dcat, 2 * D, spk, B, T, D, n_spk, dspk, dt=code, ws=ws)
+    U = dcat.float().reshape(B, T, 2 * D)[:, :, D:].sum(1)
+    ref = torch.zeros(n_spk, D, device=cuda).index_add_(0, spk, U)
+    assert rel(dspk - 0.5, ref) < 1e-5
+    if n_spk > 4:
+        assert torch.equal(dspk[0], torch.full((D,), 0.5, device=cuda))
 
 
 def test_attention_dropout_mask_statistics(cuda, parity_log):
