@@ -179,6 +179,15 @@ int ln_fwd_rows() {
   return r;
 }
 
+// tanh for the bf16 backward's (1 - t^2) gate: exp-based, absolute error ~1e-7 (the gate's
+// error is 2|t| times that, far below the bf16 gradient it scales); tanhf's branchy
+// polynomial costs ~3x the instructions.  The forward keeps tanhf (its result is the layer's
+// output), and so do the fp32 kernels.  do_tanh == 2 (FS2_LN_TANH_EXACT, experiments build)
+// keeps tanhf in the bf16 backward too.
+__device__ __forceinline__ float tanh_gate(float x) {
+  return 1.f - 2.f * __builtin_amdgcn_rcpf(__expf(2.f * x) + 1.f);
+}
+
 struct LnBwdP {
   const char* dy; long lddy; const char* s; long lds; const float* mean; const float* rstd;
   const float* gamma; const float* beta; int do_tanh; float p_o; uint32_t salt_o;
@@ -424,7 +433,8 @@ __global__ void __launch_bounds__(256) ln_bwd_vec_kernel(LnBwdP p, float* part, 
           float gg = dv[e] * rm;
           if (p.p_o > 0.f) gg = ko[e] ? gg * inv_o : 0.f;
           if (p.do_tanh) {
-            const float t = tanhf(xh[ch][e] * gm[e] + bt[e]);
+            const float z = xh[ch][e] * gm[e] + bt[e];
+            const float t = (sizeof(T) == 2 && p.do_tanh == 1) ? tanh_gate(z) : tanhf(z);
             gg *= (1.f - t * t);
           }
           pg[ch][e] += gg * xh[ch][e];
@@ -490,10 +500,9 @@ __global__ void __launch_bounds__(256) ln_bwd_vec_kernel(LnBwdP p, float* part, 
 
 // bf16, D <= 512 (one 16-byte chunk per lane): the same per-row arithmetic and the same
 // per-wave accumulation order as ln_bwd_vec_kernel<bf16, 1> (so identical results), but each
-// wave loads R rows (r, r+4, ..., r+4(R-1)) before computing any of them.  The tanh-gated case
-// (PostNet, D = 512) measured no faster this way (94 vs 103 us) and keeps the one-row kernel.  No tanh gate (that
-// case keeps the one-row kernel).  The one-row loop
-// keeps ~1.5 KB per wave in flight and ran at 1-2 TB/s (latency bound: 15 waves per CU).
+// wave loads R rows (r, r+4, ..., r+4(R-1)) before computing any of them.  The one-row loop
+// keeps ~1.5 KB per wave in flight and ran at 1-2 TB/s (latency bound: 15 waves per CU).  The
+// tanh-gated case (PostNet) uses R = 2 (ln_tanh_rows).
 template <int R, bool TANH>
 __global__ void __launch_bounds__(256) ln_bwd_rows_kernel(LnBwdP p, float* part, int npart,
                                                           int kind0) {
@@ -559,7 +568,8 @@ __global__ void __launch_bounds__(256) ln_bwd_rows_kernel(LnBwdP p, float* part,
           float gg = dv * rm[j];
           if (p.p_o > 0.f) gg = fs2_keep_pair_bit(ho[e >> 1], ib + e, thr_o) ? gg * inv_o : 0.f;
           if constexpr (TANH) {
-            const float t = tanhf(xh[e] * gm[e] + bt[e]);
+            const float z = xh[e] * gm[e] + bt[e];
+            const float t = p.do_tanh == 1 ? tanh_gate(z) : tanhf(z);
             gg *= (1.f - t * t);
           }
           pg[e] += gg * xh[e];
@@ -806,6 +816,13 @@ int ln_rpb(int M) {
 int ln_blocks(int M) { return min(8192, max(1, (M + ln_rpb(M) - 1) / ln_rpb(M))); }
 // rows in flight per wave in the bf16 LayerNorm backward (FS2_LN_ROWS=1 selects the one-row
 // kernel for A/B runs)
+// the tanh-gated bf16 LayerNorm backward (PostNet, D = 512) through the R = 2 rows kernel:
+// 43.2 us vs 48.7 for the one-row kernel with the same exp-based gate, 57.1 with tanhf
+// (tools/r06_ln_tanh.sh, M = 31264); FS2_LN_TANH_ROWS=0 selects the one-row kernel
+int ln_tanh_rows() {
+  static const int r = fs2_exp_int("FS2_LN_TANH_ROWS", 1);
+  return r;
+}
 int ln_rows_r() {
   static const int r = fs2_exp_int("FS2_LN_ROWS", 4);
   return r;
@@ -985,6 +1002,8 @@ extern "C" int fs2_ln_bwd(const void* dy, int64_t lddy, const void* s, int64_t l
            salt_o, row_mask, relu_gate_in, (char*)ds, ldds, (char*)dr, p_r, salt_r, pg, pb, M,
            D, seed, rpb, pcl, (long)npart * D};
   hipStream_t st = (hipStream_t)stream;
+  static const int tanh_exact = fs2_exp_int("FS2_LN_TANH_EXACT", 0);
+  if (tanh_exact && do_tanh) p.do_tanh = 2;
   const int V = dtype == FS2_BF16 ? 8 : 4;
   const int nch = (D / V + 63) / 64;
   const bool vec = (D % V) == 0 && nch <= 4 && a16(dy) && (lddy % V) == 0 && a16(s) &&
@@ -994,6 +1013,7 @@ extern "C" int fs2_ln_bwd(const void* dy, int64_t lddy, const void* s, int64_t l
   const int kind0 = dgamma ? 0 : 2;
   if (dtype == FS2_BF16) {
     if (!vec) hipLaunchKernelGGL(ln_bwd_kernel<bf16>, dim3(nb), dim3(256), 0, st, p);
+    else if (nch == 1 && do_tanh && ln_tanh_rows()) hipLaunchKernelGGL((ln_bwd_rows_kernel<2, true>), dim3(nb), dim3(256), 0, st, p, part, npart, kind0);
     else if (nch == 1 && ln_rows_r() == 4 && !do_tanh) hipLaunchKernelGGL((ln_bwd_rows_kernel<4, false>), dim3(nb), dim3(256), 0, st, p, part, npart, kind0);
     else if (nch == 1 && ln_rows_r() == 2 && !do_tanh) hipLaunchKernelGGL((ln_bwd_rows_kernel<2, false>), dim3(nb), dim3(256), 0, st, p, part, npart, kind0);
     else if (nch == 1) hipLaunchKernelGGL((ln_bwd_vec_kernel<bf16, 1>), dim3(nb), dim3(256), 0, st, p, part, npart, kind0);

@@ -95,7 +95,6 @@ _TAP_INNER_FWD = N.exp_int("FS2_TAP_INNER_FWD", 0)
 # serial mode for per-call-site timing (bench.py --detail runs with the experiments library)
 _NO_SIDE = N.exp_flag("FS2_NO_SIDE_STREAM")
 _NO_AUX = N.exp_flag("FS2_NO_AUX_STREAM")
-_ZERO_MAIN = N.exp_flag("FS2_ZERO_MAIN")      # A/B: gradient zero on the main stream
 # persistent-GEMM grid budget of the weight-gradient side stream (fs2_gemm_desc.max_ctas, passed
 # with every weight-gradient GEMM enqueued there): the CUs it leaves free take the main stream's LayerNorm / reduction / short GEMM launches, which
 # otherwise queue behind side-stream blocks that hold a whole CU's registers.  Same-box sweep
@@ -185,7 +184,6 @@ class FS2Engine:
         # stream while the main stream runs the encoder backward; adamw_step_split does the rest
         self.adam_split = None
         self._adam_late_done = False
-        self._zero_pending = False   # zero_grads queued the gradient zero on the side stream
         # DP (FusedTrainer): (ready(), wait(stream)) of the gradient buckets holding the late
         # parameters -- the late AdamW is launched from the notify hook once they are all queued,
         # its aux stream waiting for their all-reduce
@@ -287,21 +285,6 @@ class FS2Engine:
         into the main stream before the variance group completes)"""
         main = torch.cuda.current_stream(self.dev)
         return [main] if self._side is None else [main, self._side]
-
-    def zero_grads(self, flat):
-        """zero the flat gradient buffer for a new step.  With a side stream this runs there,
-        beside the forward (the side stream is idle until the backward's first weight gradient;
-        the 340 MB fill took 57 us of the main stream per step, r06f trace), and backward()
-        makes the main stream wait for it before the first gradient write.  The side stream
-        first waits for everything queued on the current stream (the previous step's AdamW
-        reads of the gradients)."""
-        if self._side is None or _ZERO_MAIN or torch.cuda.is_current_stream_capturing():
-            flat.zero_()
-            return
-        self._side.wait_stream(torch.cuda.current_stream(self.dev))
-        with torch.cuda.stream(self._side):
-            flat.zero_()
-        self._zero_pending = True
 
     def side_join(self):
         if self._side is not None:
@@ -1341,9 +1324,6 @@ class FS2Engine:
     def backward(self, ctx, d_mel, d_post, d_dur, d_pitch, d_energy):
         """Backward of ``forward`` for upstream gradients of (mel, postnet, log-dur, pitch,
         energy) outputs; parameter gradients are ACCUMULATED into model._gflat."""
-        if self._zero_pending:      # zero_grads' fill on the side stream (long done by now)
-            torch.cuda.current_stream(self.dev).wait_stream(self._side)
-            self._zero_pending = False
         c = self.cfg
         D, H_e, H_d, NM = c.enc_d_model, c.enc_num_head, c.dec_num_head, c.n_mels
         B, Tp, Tm, seed = ctx["B"], ctx["Tp"], ctx["Tm"], ctx["seed"]

@@ -207,7 +207,7 @@ class FusedTrainer:
         produces them).  Returns the loss vector."""
         (phoneme, spk_ids, phon_len, mel_tgt, pitch_tgt, energy_tgt, duration_tgt, mel_len) = batch[:8]
         m = self.model
-        self.eng.zero_grads(m._gflat)
+        m._gflat.zero_()
         out, ctx = self.eng.forward(phoneme, spk_ids, duration_tgt, pitch_tgt, energy_tgt,
                                     intensity=intensity, training=True,
                                     seed=self.seed if seed is None else seed,
