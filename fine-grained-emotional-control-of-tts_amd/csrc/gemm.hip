@@ -1966,7 +1966,11 @@ __global__ void __launch_bounds__(W4_NT, 1) gemm_w4b_kernel(GemmP p) {
   const int orig = blockIdx.x;
   const int xcd = orig & 7, q = nwg >> 3, r8 = nwg & 7;
   const int bid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (orig >> 3);
-  const int tm = bid / p.tiles_n, tn = bid - tm * p.tiles_n;
+  int tm = bid / p.tiles_n, tn = bid - tm * p.tiles_n;
+  if (XFLAGS(p) & 8) {   // experiments: column-tile-major order (an XCD's blocks share B tiles)
+    tn = bid / p.tiles_m;
+    tm = bid - tn * p.tiles_m;
+  }
   const int m0 = tm * 256, n0 = tn * BNW;
   const int nst = p.K / 64;
 

@@ -64,6 +64,29 @@ def case(name, B, T, C, O, KW, splits):
         print(f"{name}: conv6 K-major S={S} Kp={Kp}  {tk:7.1f} us  {fl / tk / 1e6:6.0f} TF/s"
               f"  + transposes {tt:6.1f} us ({mb / tt * 1e-3:.2f} TB/s)  total {tk + tt:7.1f}",
               flush=True)
+    if os.environ.get("KM_BLAS"):
+        # hipBLASLt ceilings (torch.matmul, fp32 out): the plain NT GEMM of the same size with
+        # the shifted X rows materialised ([KW*C][Kp]), and the per-tap form (KW GEMMs of
+        # O x C x Kp on X's image shifted by j - P elements)
+        Kp = ops.round_up(B * (T + 2 * P), 64)
+        A = (torch.randn(O, Kp, device="cuda") * 0.5).to(bf)
+        Bf = (torch.randn(Ncols, Kp, device="cuda") * 0.5).to(bf)
+        tb = timed(lambda: torch.matmul(A, Bf.t()))
+        print(f"{name}: hipBLASLt plain {O}x{Ncols}x{Kp}  {tb:7.1f} us  {fl / tb / 1e6:6.0f} TF/s",
+              flush=True)
+        g = torch.zeros(C * Kp + 128, device="cuda", dtype=bf)
+        outp = torch.empty(O, KW, C, device="cuda")
+
+        def taps():
+            for j in range(KW):
+                xs = g.as_strided((C, Kp), (Kp, 1), 64 + j - P)
+                torch.matmul(A, xs.t(), out=outp[:, j, :])
+        try:
+            tj = timed(taps)
+            print(f"{name}: hipBLASLt {KW} tap GEMMs {O}x{C}x{Kp}  {tj:7.1f} us  {fl / tj / 1e6:6.0f} TF/s",
+                  flush=True)
+        except RuntimeError as e:
+            print(f"{name}: per-tap torch.matmul refused: {e}", flush=True)
 
 
 def main():
@@ -71,6 +94,8 @@ def main():
     _native.load()
     case("decoder conv1", 32, 977, 384, 1536, 9, (2, 3, 4))
     case("encoder conv1", 32, 200, 384, 1536, 9, (2, 3))
+    if os.environ.get("KM_BLAS"):
+        return
     case("postnet mid  ", 32, 977, 512, 512, 5, (6, 12))
     case("postnet pre  ", 32, 977, 80, 512, 5, (6, 12))
     case("postnet post ", 32, 977, 512, 80, 5, (12, 25))
