@@ -104,6 +104,9 @@ _SIDE_CTAS = N.exp_int("FS2_SIDE_CTAS", 208)
 # AdamW of the decoder / mel-linear / PostNet parameters on the aux stream during the encoder
 # backward (FusedTrainer.step, one process); FS2_ADAM_OVERLAP=0 (experiments build): one launch
 _ADAM_OVERLAP = N.exp_int("FS2_ADAM_OVERLAP", 1)
+# the energy predictor's forward and backward on the aux stream (FS2_AUX_ENERGY=0: on the main
+# stream, its backward fused into the residual epilogue, for A/B runs)
+_AUX_ENERGY = N.exp_int("FS2_AUX_ENERGY", 1)
 
 
 def ps_plain_ok(M, lda, N, ldb, out_rows, ldc, out_bytes):
@@ -1255,7 +1258,13 @@ class FS2Engine:
                         Z2, dt=self.dt)
         Z2m = Z2.clone()
         ops.mask_rows(Z2m, D, keep_p, Mp, D, dt=self.dt)
+        # with the energy target given, the energy predictor's output too only reaches the loss:
+        # it joins the duration / pitch chain on the aux stream
+        aux_e = (self._aux_fork(Z2m, keep_p) if (aux_h is not None and energy is not None
+                                                 and _AUX_ENERGY) else None)
         pe_, ectx = self._pred_fwd(Z2m, keep_p, B, Tp, "energyPred", energy_rate, pv, seed, salt)
+        if aux_e is not None:
+            self._aux_exit(aux_e)
         kwe = c.energy_pred_kernel_size
         if energy is not None:
             energy = energy.to(torch.float32).contiguous()
@@ -1307,8 +1316,9 @@ class FS2Engine:
                   row_scale=keep_m)                                                # :430
         post, pn_ctx = self._postnet_fwd(mel, B, Tm, pp_, seed, salt)            # :431
         if aux_h is not None:
-            self._aux_join(aux_h[1], pd, pp, *[t for cc in (dctx, pctx) for t in cc.values()
-                                               if isinstance(t, torch.Tensor)])
+            self._aux_join(aux_h[1], pd, pp, pe_, *[t for cc in (dctx, pctx, ectx)
+                                                    for t in cc.values()
+                                                    if isinstance(t, torch.Tensor)])
         ctx.update(keep_p=keep_p, enc_ctx=enc_ctx, Xenc_last=X, me=me, re=re_, cat=cat, ldc=ldc,
                    Z=Z, dctx=dctx, pctx=pctx, ectx=ectx, a_p=a_p, a_e=a_e, Z2m=Z2m, Tm=Tm,
                    cum=cum, keep_m=keep_m, dec_ctx=dec_ctx, Xdec_last=Xd, md=md, rd=rd, Xo=Xo,
@@ -1344,13 +1354,17 @@ class FS2Engine:
         d_post = d_post.reshape(Mm, NM).to(self.adt).contiguous()
         d_pitch = d_pitch.reshape(Mp).to(self.adt).contiguous()
         d_dur = d_dur.reshape(Mp).to(self.adt).contiguous()
-        aux_h, dZd, dZp = None, None, None
+        aux_h, dZd, dZp, dZe = None, None, None, None
+        d_energy = d_energy.reshape(Mp).to(self.adt).contiguous()
         if self._aux is not None:
-            # duration and pitch predictor backward chains depend only on the loss gradients
-            # and the forward context: run them beside the PostNet / decoder backward
-            aux_h = self._aux_fork(d_pitch, d_dur, keep_p)
+            # duration, pitch and energy predictor backward chains depend only on the loss
+            # gradients and the forward context: run them beside the PostNet / decoder backward
+            aux_h = self._aux_fork(d_pitch, d_dur, d_energy, keep_p)
             dZpd = self._pred_pair_bwd(d_dur, ctx["dctx"], d_pitch, ctx["pctx"], keep_p, B, Tp,
                                        ctx["p_var"], seed)
+            if _AUX_ENERGY:
+                dZe = self._pred_bwd(d_energy, ctx["ectx"], keep_p, B, Tp, "energyPred",
+                                     ctx["p_var"], seed)
             self._aux_exit(aux_h)
         # mel receives the loss gradient and the PostNet residual (model.py:431)
         d_mel_total = d_mel.clone()
@@ -1379,9 +1393,15 @@ class FS2Engine:
         ops.embed1d_bwd(dZ3, ctx["a_e"], B, Tp, D, kwe, G["energyEmbed.conv.weight"],
                         G["energyEmbed.conv.bias"], dt=self.dt,
                         ws=self.ws(128 * (kwe + 1) * D))
-        d_energy = d_energy.reshape(Mp).to(self.adt).contiguous()
-        dZ2 = self._pred_bwd(d_energy, ctx["ectx"], keep_p, B, Tp, "energyPred", ctx["p_var"], seed,
-                             residual=dZ3)
+        if dZe is not None:
+            # dZ2 = dZ3 + keep * dZ_energy-input (the sequential chain's residual epilogue, here
+            # one add of the aux chain's result)
+            self._aux_join(aux_h[1], dZpd, dZe)
+            dZ2 = dZ3
+            ops.add(dZ2, dZe, Mp * D, 1.0, dt=self.dt)
+        else:
+            dZ2 = self._pred_bwd(d_energy, ctx["ectx"], keep_p, B, Tp, "energyPred", ctx["p_var"],
+                                 seed, residual=dZ3)
         kwp = c.pitch_pred_kernel_size
         ops.embed1d_bwd(dZ2, ctx["a_p"], B, Tp, D, kwp, G["pitchEmbed.conv.weight"],
                         G["pitchEmbed.conv.bias"], dt=self.dt, ws=self.ws(128 * (kwp + 1) * D))
