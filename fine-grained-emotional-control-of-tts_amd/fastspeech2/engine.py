@@ -107,6 +107,9 @@ _ADAM_OVERLAP = N.exp_int("FS2_ADAM_OVERLAP", 1)
 # the energy predictor's forward and backward on the aux stream (FS2_AUX_ENERGY=0: on the main
 # stream, its backward fused into the residual epilogue, for A/B runs)
 _AUX_ENERGY = N.exp_int("FS2_AUX_ENERGY", 1)
+# the pitch / energy embedding and speaker-embedding weight gradients on the side stream
+# (FS2_SIDE_SMALL=0: on the main stream, for A/B runs)
+_SIDE_SMALL = N.exp_int("FS2_SIDE_SMALL", 1)
 
 
 def ps_plain_ok(M, lda, N, ldb, out_rows, ldc, out_bytes):
@@ -1389,29 +1392,36 @@ class FS2Engine:
         # LengthRegulator backward: segment sums (masked by the decoder input mask)
         dZ3 = self.empty(Mp, D)
         ops.lr_scatter(dX, ctx["cum"], keep_m, B, Tp, Tm, D, dZ3, dt=self.dt)
+        def wg_side(fn, *tensors):
+            # a weight-gradient-only pass on the side stream; its inputs stay unmodified after
+            h = self._side_enter(*tensors) if _SIDE_SMALL else None
+            fn()
+            self._side_exit(h)
         kwe = c.energy_pred_kernel_size
-        ops.embed1d_bwd(dZ3, ctx["a_e"], B, Tp, D, kwe, G["energyEmbed.conv.weight"],
-                        G["energyEmbed.conv.bias"], dt=self.dt,
-                        ws=self.ws(128 * (kwe + 1) * D))
+        wg_side(lambda: ops.embed1d_bwd(dZ3, ctx["a_e"], B, Tp, D, kwe, G["energyEmbed.conv.weight"],
+                                        G["energyEmbed.conv.bias"], dt=self.dt,
+                                        ws=self.ws(128 * (kwe + 1) * D)), dZ3, ctx["a_e"])
         if dZe is not None:
             # dZ2 = dZ3 + keep * dZ_energy-input (the sequential chain's residual epilogue, here
-            # one add of the aux chain's result)
+            # one add of the aux chain's result, into its buffer: dZ3 stays as the side stream
+            # reads it)
             self._aux_join(aux_h[1], dZpd, dZe)
-            dZ2 = dZ3
-            ops.add(dZ2, dZe, Mp * D, 1.0, dt=self.dt)
+            dZ2 = dZe
+            ops.add(dZ2, dZ3, Mp * D, 1.0, dt=self.dt)
         else:
             dZ2 = self._pred_bwd(d_energy, ctx["ectx"], keep_p, B, Tp, "energyPred", ctx["p_var"],
                                  seed, residual=dZ3)
         kwp = c.pitch_pred_kernel_size
-        ops.embed1d_bwd(dZ2, ctx["a_p"], B, Tp, D, kwp, G["pitchEmbed.conv.weight"],
-                        G["pitchEmbed.conv.bias"], dt=self.dt, ws=self.ws(128 * (kwp + 1) * D))
+        wg_side(lambda: ops.embed1d_bwd(dZ2, ctx["a_p"], B, Tp, D, kwp, G["pitchEmbed.conv.weight"],
+                                        G["pitchEmbed.conv.bias"], dt=self.dt,
+                                        ws=self.ws(128 * (kwp + 1) * D)), dZ2, ctx["a_p"])
         if aux_h is not None:
             self._aux_join(aux_h[1], dZpd)
-            # dZ = keep * (dZ2 + dZ_dur + dZ_pitch), as the sequential chain's residual
+            # dZ = keep * (dZ_dur + dZ_pitch + dZ2), as the sequential chain's residual
             # epilogues, summed in fp32 with one rounding (the fused conv1's data gradient
-            # already holds dZ_dur + dZ_pitch)
-            dZ = dZ2
-            ops.add3_mask_rows(dZ, dZpd, None, D, keep_p, Mp, D, dt=self.dt)
+            # already holds dZ_dur + dZ_pitch), into dZpd's buffer (dZ2 stays for the side stream)
+            dZ = dZpd
+            ops.add3_mask_rows(dZ, dZ2, None, D, keep_p, Mp, D, dt=self.dt)
         else:
             dZ = self._pred_pair_bwd(d_dur, ctx["dctx"], d_pitch, ctx["pctx"], keep_p, B, Tp,
                                      ctx["p_var"], seed, residual=dZ2, post_mask=True)
@@ -1425,8 +1435,9 @@ class FS2Engine:
         dcat = self.empty(Mp, 2 * D)
         self._dgrad(dZ, D, Mp, Tp, "concat_proj.w.weight", dcat, 2 * D, n_out=2 * D)
         self._wgrad(dZ, D, ctx["cat"], ldc, Mp, Tp, "concat_proj.w.weight", n_cols=ldc)
-        ops.concat_bwd_spk(dcat, 2 * D, ctx["speakers"], B, Tp, D, c.n_speakers,
-                           G["speaker_emb.Embedding.weight"], dt=self.dt, ws=self.ws(B * D))
+        wg_side(lambda: ops.concat_bwd_spk(dcat, 2 * D, ctx["speakers"], B, Tp, D, c.n_speakers,
+                                           G["speaker_emb.Embedding.weight"], dt=self.dt,
+                                           ws=self.ws(B * D)), dcat, ctx["speakers"])
         dXl = self.empty(Mp, D)
         ops.ln_bwd(dcat, 2 * D, ctx["Xenc_last"], D, ctx["me"], ctx["re"], P["encoder.norm.norm.weight"],
                    P["encoder.norm.norm.bias"], dXl, D, Mp, D, dt=self.dt,
