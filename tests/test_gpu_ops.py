@@ -200,6 +200,52 @@ def test_layernorm_bwd_dropout_gate(cuda, M, D):
     assert rel(dc, dr_ref.sum(0)) < 2e-2
 
 
+@pytest.mark.parametrize("M,npart", [(31264, 3), (6400, 3), (31264, 1), (2000, 2), (777, 3)])
+def test_layernorm_bwd_partial_reduction(cuda, M, npart):
+    """The bf16 LayerNorm backward's gamma / beta / column-sum reduction over per-block partial
+    rows at the decoder's M = 31264 (763 partial rows) down to M = 777: the sums against torch
+    fp32 (rel 1e-3 -- fp32 sums over M rows of bf16 inputs), added onto the outputs' previous
+    values, with the workspace poisoned with NaN beforehand, and bit-identical over repeated
+    calls (fixed summation order)."""
+    from fastspeech2 import ops
+    torch.manual_seed(M + npart)
+    D = 384
+    x = torch.randn(M, D, device=cuda).to(torch.bfloat16)
+    g = torch.randn(D, device=cuda)
+    b = torch.randn(D, device=cuda)
+    y = torch.empty(M, D, device=cuda, dtype=torch.bfloat16)
+    mean = torch.empty(M, device=cuda)
+    rstd = torch.empty(M, device=cuda)
+    ops.ln_fwd(x, D, g, b, 1e-6, y, D, mean, rstd, M, D, dt=1)
+    dy = torch.randn(M, D, device=cuda).to(torch.bfloat16)
+    ws = torch.full((int(ops.ln_ws(M, D)),), float("nan"), device=cuda)
+    ds = torch.empty(M, D, device=cuda, dtype=torch.bfloat16)
+    dr = torch.empty(M, D, device=cuda, dtype=torch.bfloat16)
+    outs = []
+    for _ in range(3):
+        dg = torch.full((D,), 0.5, device=cuda) if npart >= 2 else None
+        db = torch.full((D,), -0.25, device=cuda) if npart >= 2 else None
+        dc = torch.full((D,), 2.0, device=cuda) if npart != 2 else None
+        ops.ln_bwd(dy, D, x, D, mean, rstd, g, b, ds, D, M, D, dt=1, ws=ws, seed=5, dr=dr,
+                   p_r=0.1, salt_r=9, dgamma=dg, dbeta=db, dcol=dc)
+        outs.append([t.clone() for t in (dg, db, dc) if t is not None])
+    torch.cuda.synchronize()
+    for o in outs[1:]:
+        for a, c in zip(outs[0], o):
+            assert torch.equal(a, c)
+    xs = x.float().requires_grad_(True)
+    gr, br = g.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    F.layer_norm(xs, (D,), gr, br, 1e-6).backward(dy.float())
+    res = outs[0]
+    if npart >= 2:
+        assert rel(res[0] - 0.5, gr.grad) < 1e-3
+        assert rel(res[1] + 0.25, br.grad) < 1e-3
+    if npart != 2:        # the column sum of the fp32 dropout-masked gradient (before rounding)
+        kr = _keep_ln_np(5, 9, np.arange(M * D, dtype=np.uint64), 0.1).reshape(M, D)
+        dr_ref = xs.grad * torch.from_numpy(kr).to(cuda).float() / 0.9
+        assert rel(res[-1] - 2.0, dr_ref.sum(0)) < 1e-3
+
+
 def test_attention_mask_quirk_against_torch_mha(cuda, golden_dir):
     """The golden torch-MHA output (reference mask expression) through our kernels, fp32."""
     from fastspeech2 import ops
