@@ -75,6 +75,25 @@ __device__ __forceinline__ float wave_sum(float v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
+// the same sum through DPP -- quad_perm xor 1 / xor 2, then row_ror 4 / 8 (every lane of a
+// 16-lane row then holds the row's sum) -- and four readlanes added in a fixed order (a
+// wave-uniform result): ~30 cycles against the six dependent LDS round trips (ds_bpermute) of
+// __shfl_xor.  Every lane must be active.  Sums in a different order from wave_sum.
+template <int C>
+__device__ __forceinline__ float dpp_f32(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), C, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  v += dpp_f32<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_f32<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_f32<0x124>(v);  // row_ror:4
+  v += dpp_f32<0x128>(v);  // row_ror:8
+  const int u = __float_as_int(v);
+  return (__int_as_float(__builtin_amdgcn_readlane(u, 0)) +
+          __int_as_float(__builtin_amdgcn_readlane(u, 16))) +
+         (__int_as_float(__builtin_amdgcn_readlane(u, 32)) +
+          __int_as_float(__builtin_amdgcn_readlane(u, 48)));
+}
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));

@@ -16,6 +16,12 @@ namespace {
 
 constexpr int MAXJ = 16;  // D <= 1024
 
+template <bool DPP>
+__device__ __forceinline__ float wsum(float v) {
+  if constexpr (DPP) return wave_sum_dpp(v);
+  else return wave_sum(v);
+}
+
 struct LnFwdP {
   const char* x; long ldx; const char* r; long ldr; float p_r; uint32_t salt_r;
   char* s_out; const float* gamma; const float* beta; float eps; int do_tanh;
@@ -88,7 +94,7 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(LnFwdP p) {
 // per wave kept ~1.5 KB in flight per wave -- 48 KB per CU at full occupancy -- and ran the
 // decoder LayerNorm (96 MB) at 3.6 TB/s.  Per-row arithmetic, dropout indices and rounding
 // points are those of ln_fwd_vec_kernel<bf16, 1> (outputs bit-identical).
-template <int R>
+template <int R, bool DPP>
 __global__ void __launch_bounds__(256) ln_fwd_rows_kernel(LnFwdP p) {
   constexpr int V = 8;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -139,13 +145,13 @@ __global__ void __launch_bounds__(256) ln_fwd_rows_kernel(LnFwdP p) {
 #pragma unroll
       for (int e = 0; e < V; ++e) sum += v[j][e];
     }
-    const float mean = wave_sum(sum) / (float)p.D;
+    const float mean = wsum<DPP>(sum) / (float)p.D;
     float sq = 0.f;
     if (act) {
 #pragma unroll
       for (int e = 0; e < V; ++e) { const float c = v[j][e] - mean; sq += c * c; }
     }
-    const float var = wave_sum(sq) / (float)p.D;
+    const float var = wsum<DPP>(sq) / (float)p.D;
     const float rstd = 1.f / sqrtf(var + p.eps);
     if (lane == 0) { p.mean[row] = mean; p.rstd[row] = rstd; }
     if (act) {
@@ -173,6 +179,11 @@ __global__ void __launch_bounds__(256) ln_fwd_rows_kernel(LnFwdP p) {
   }
 }
 
+// the bf16 rows kernels' row sums through DPP (wave_sum_dpp; FS2_LN_DPP=0: __shfl_xor)
+int ln_dpp() {
+  static const int r = fs2_exp_int("FS2_LN_DPP", 1);
+  return r;
+}
 // rows per wave of the bf16 LayerNorm forward (FS2_LN_FWD_ROWS: 1 = ln_fwd_vec_kernel)
 int ln_fwd_rows() {
   static const int r = fs2_exp_int("FS2_LN_FWD_ROWS", 2);
@@ -503,7 +514,7 @@ __global__ void __launch_bounds__(256) ln_bwd_vec_kernel(LnBwdP p, float* part, 
 // wave loads R rows (r, r+4, ..., r+4(R-1)) before computing any of them.  The one-row loop
 // keeps ~1.5 KB per wave in flight and ran at 1-2 TB/s (latency bound: 15 waves per CU).  The
 // tanh-gated case (PostNet) uses R = 2 (ln_tanh_rows).
-template <int R, bool TANH>
+template <int R, bool TANH, bool DPP>
 __global__ void __launch_bounds__(256) ln_bwd_rows_kernel(LnBwdP p, float* part, int npart,
                                                           int kind0) {
   constexpr int V = 8;
@@ -582,8 +593,8 @@ __global__ void __launch_bounds__(256) ln_bwd_rows_kernel(LnBwdP p, float* part,
 #pragma unroll
         for (int e = 0; e < V; ++e) { g[e] = 0.f; xh[e] = 0.f; }
       }
-      a1 = wave_sum(a1) / (float)p.D;
-      a2 = wave_sum(a2) / (float)p.D;
+      a1 = wsum<DPP>(a1) / (float)p.D;
+      a2 = wsum<DPP>(a2) / (float)p.D;
       if (act) {
         float o[V], w[V];
 #pragma unroll
@@ -957,11 +968,11 @@ extern "C" int fs2_ln_fwd(const void* x, int64_t ldx, const void* r, int64_t ldr
     else if (nch == 1 && ln_fwd_rows() == 2 && a16(gamma) && a16(beta)) {
       p.img = (char*)img;
       img_done = true;
-      hipLaunchKernelGGL((ln_fwd_rows_kernel<2>), dim3((M + 7) / 8), dim3(256), 0, s, p);
+      hipLaunchKernelGGL((ln_dpp() ? ln_fwd_rows_kernel<2, true> : ln_fwd_rows_kernel<2, false>), dim3((M + 7) / 8), dim3(256), 0, s, p);
     } else if (nch == 1 && ln_fwd_rows() == 4 && a16(gamma) && a16(beta)) {
       p.img = (char*)img;
       img_done = true;
-      hipLaunchKernelGGL((ln_fwd_rows_kernel<4>), dim3((M + 15) / 16), dim3(256), 0, s, p);
+      hipLaunchKernelGGL((ln_dpp() ? ln_fwd_rows_kernel<4, true> : ln_fwd_rows_kernel<4, false>), dim3((M + 15) / 16), dim3(256), 0, s, p);
     }
     else if (nch == 1) hipLaunchKernelGGL((ln_fwd_vec_kernel<bf16, 1>), grid, dim3(256), 0, s, p);
     else if (nch == 2) hipLaunchKernelGGL((ln_fwd_vec_kernel<bf16, 2>), grid, dim3(256), 0, s, p);
@@ -1013,9 +1024,9 @@ extern "C" int fs2_ln_bwd(const void* dy, int64_t lddy, const void* s, int64_t l
   const int kind0 = dgamma ? 0 : 2;
   if (dtype == FS2_BF16) {
     if (!vec) hipLaunchKernelGGL(ln_bwd_kernel<bf16>, dim3(nb), dim3(256), 0, st, p);
-    else if (nch == 1 && do_tanh && ln_tanh_rows()) hipLaunchKernelGGL((ln_bwd_rows_kernel<2, true>), dim3(nb), dim3(256), 0, st, p, part, npart, kind0);
-    else if (nch == 1 && ln_rows_r() == 4 && !do_tanh) hipLaunchKernelGGL((ln_bwd_rows_kernel<4, false>), dim3(nb), dim3(256), 0, st, p, part, npart, kind0);
-    else if (nch == 1 && ln_rows_r() == 2 && !do_tanh) hipLaunchKernelGGL((ln_bwd_rows_kernel<2, false>), dim3(nb), dim3(256), 0, st, p, part, npart, kind0);
+    else if (nch == 1 && do_tanh && ln_tanh_rows()) hipLaunchKernelGGL((ln_dpp() ? ln_bwd_rows_kernel<2, true, true> : ln_bwd_rows_kernel<2, true, false>), dim3(nb), dim3(256), 0, st, p, part, npart, kind0);
+    else if (nch == 1 && ln_rows_r() == 4 && !do_tanh) hipLaunchKernelGGL((ln_dpp() ? ln_bwd_rows_kernel<4, false, true> : ln_bwd_rows_kernel<4, false, false>), dim3(nb), dim3(256), 0, st, p, part, npart, kind0);
+    else if (nch == 1 && ln_rows_r() == 2 && !do_tanh) hipLaunchKernelGGL((ln_dpp() ? ln_bwd_rows_kernel<2, false, true> : ln_bwd_rows_kernel<2, false, false>), dim3(nb), dim3(256), 0, st, p, part, npart, kind0);
     else if (nch == 1) hipLaunchKernelGGL((ln_bwd_vec_kernel<bf16, 1>), dim3(nb), dim3(256), 0, st, p, part, npart, kind0);
     else if (nch == 2) hipLaunchKernelGGL((ln_bwd_vec_kernel<bf16, 2>), dim3(nb), dim3(256), 0, st, p, part, npart, kind0);
     else hipLaunchKernelGGL((ln_bwd_vec_kernel<bf16, 4>), dim3(nb), dim3(256), 0, st, p, part, npart, kind0);
