@@ -715,6 +715,52 @@ __global__ void __launch_bounds__(256) colsum_vec_kernel(const T* X, long ldx, i
   }
 }
 
+// column sums for wide rows (N / VEC >= 32 chunks): block (row range, 64-chunk column slab),
+// wave w walks rows w, w + 4, ... with U 16-byte loads in flight; colsum_vec_kernel gave a
+// 1152-wide bf16 row (the QKV bias gradient) one sub-row per block, 144 of 256 threads each
+// walking all 64 rows 4 loads at a time (111 us for 72 MB in the step)
+template <typename T, int U>
+__global__ void __launch_bounds__(256) colsum_slab_kernel(const T* X, long ldx, int M, int N,
+                                                         int rows_per_block, float* part) {
+  constexpr int V = Vec<T>::N;
+  __shared__ float red[4][64 * V];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int cc = blockIdx.y * 64 + lane;
+  const bool act = cc * V < N;
+  const int rbeg = blockIdx.x * rows_per_block;
+  const int rend = min(M, rbeg + rows_per_block);
+  float acc[V];
+#pragma unroll
+  for (int e = 0; e < V; ++e) acc[e] = 0.f;
+  if (act) {
+    const T* x = X + (long)cc * V;
+    int m = rbeg + w;
+    for (; m + 4 * (U - 1) < rend; m += 4 * U) {
+      float a[U][V];
+#pragma unroll
+      for (int u = 0; u < U; ++u) vload<T>(a[u], x + (long)(m + 4 * u) * ldx);
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int e = 0; e < V; ++e) acc[e] += a[u][e];
+    }
+    for (; m < rend; m += 4) {
+      float a[V];
+      vload<T>(a, x + (long)m * ldx);
+#pragma unroll
+      for (int e = 0; e < V; ++e) acc[e] += a[e];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < V; ++e) red[w][lane * V + e] = acc[e];
+  __syncthreads();
+  const int n0 = blockIdx.y * 64 * V;
+  for (int i = threadIdx.x; i < 64 * V; i += 256) {
+    const int n = n0 + i;
+    if (n < N) part[(long)blockIdx.x * N + n] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
+  }
+}
+
 // Adjoint of SB Conv1d's reflect "same" padding for the data gradient (K16):
 //   dX[b,s] = Xp[b,s+P] + [1<=s<=P] Xp[b,P-s] + [T-1-P<=s<=T-2] Xp[b,2(T-1)-s+P]
 // where Xp (fp32, T+2P rows per utterance) is the zero-padded shift-conv GEMM output
@@ -1058,7 +1104,16 @@ extern "C" int fs2_colsum(const void* X, int64_t ldx, int M, int N, int dtype, f
   const int rpb = (M + nb - 1) / nb;
   const int V = dtype == FS2_BF16 ? 8 : 4;
   const bool vec = (N % V) == 0 && N / V <= 256 && a16(X) && (ldx % V) == 0;
-  if (dtype == FS2_BF16) {
+  static const int slab = fs2_exp_int("FS2_COLSUM_SLAB", 1);
+  if (vec && slab && N / V >= 32) {
+    const dim3 g(nb, (N / V + 63) / 64);
+    if (dtype == FS2_BF16)
+      hipLaunchKernelGGL((colsum_slab_kernel<bf16, 8>), g, dim3(256), 0, st, (const bf16*)X, (long)ldx, M, N, rpb, workspace);
+    else if (dtype == FS2_F32)
+      hipLaunchKernelGGL((colsum_slab_kernel<float, 8>), g, dim3(256), 0, st, (const float*)X, (long)ldx, M, N, rpb, workspace);
+    else
+      return FS2_EINVAL;
+  } else if (dtype == FS2_BF16) {
     if (vec)
       hipLaunchKernelGGL(colsum_vec_kernel<bf16>, dim3(nb), dim3(256), 0, st, (const bf16*)X, (long)ldx, M, N, rpb, workspace);
     else

@@ -984,9 +984,13 @@ def test_gemm_short_k_two_streams(cuda):
 
 
 @pytest.mark.parametrize("dt,code,tol", DT)
-@pytest.mark.parametrize("M,N,ldx", [(31264, 1536, 1536), (6400, 1152, 1152 * 3), (777, 90, 96)])
+@pytest.mark.parametrize("M,N,ldx", [(31264, 1536, 1536), (6400, 1152, 1152 * 3), (777, 90, 96),
+                                      (31264, 1152, 1152), (5000, 264, 264), (1000, 520, 528),
+                                      (33, 384, 384)])
 def test_colsum_bias_gradient(cuda, dt, code, tol, M, N, ldx):
-    """fs2_colsum (bias gradients): out (+)= column sums over rows of a row-pitched matrix."""
+    """fs2_colsum (bias gradients): out (+)= column sums over rows of a row-pitched matrix
+    (N / VEC >= 32: the column-slab kernel, partial last slab at N = 264 / 520; else the
+    sub-row kernel)."""
     from fastspeech2 import ops
     torch.manual_seed(M)
     X = torch.randn(M, ldx, device=cuda).to(dt)
