@@ -1085,7 +1085,10 @@ extern "C" int fs2_ln_bwd(const void* dy, int64_t lddy, const void* s, int64_t l
     return FS2_EINVAL;
   }
   FS2_CHECK_LAUNCH();
-  if (npart) {
+  // FS2_LN_NORED=1 (experiments build, timing probe only -- the parameter gradients are then
+  // left unreduced): what the reduce_parts launches cost the step
+  static const int nored = fs2_exp_int("FS2_LN_NORED", 0);
+  if (npart && !nored) {
     float* o0 = dgamma ? dgamma : dcol;
     float* o1 = dgamma ? dbeta : nullptr;
     float* o2 = dgamma ? dcol : nullptr;
