@@ -27,6 +27,15 @@ sys.path.insert(0, ROOT)
 import torch
 import torch.distributed as dist
 
+
+def _build_record():
+    """which sources the loaded library was built from (fs2_source_hash) against this tree's
+    (fastspeech2/_native.py refuses a mismatch at load, so these two are equal in any line)"""
+    from fastspeech2 import _native
+    return {"library": _native.LIB_PATH, "library_source_hash": _native.lib().fs2_source_hash().decode(),
+            "tree_source_hash": _native.source_hash()}
+
+
 MFMA_BF16_PEAK_TFLOPS = 2500.0   # MI355X dense bf16 (MI355X_MICROARCH.md)
 
 
@@ -484,6 +493,7 @@ def main():
                           "persistent kernel holding one block per CU), so the duration includes "
                           "its wait for CUs (DESIGN.md 6.4 has the standalone time)"},
             "hip_graph": graphed,
+            "build": _build_record(),
             # the step-level roofline on VALID frames -- frames/s x the train FLOPs
             # of one mel frame at T_phon=200, T_mel=1000 (338.8 MFLOP at default dims) / peak
             "roofline_step": {"bound": "mfma",

@@ -160,9 +160,30 @@ SIGNATURES = {
     "fs2_cast": (I, [P, I, P, I, I64, P]),
     "fs2_set_dropout_seed": (I, [U32, P]),
     "fs2_version": (ctypes.c_char_p, []),
+    "fs2_source_hash": (ctypes.c_char_p, []),
 }
 
 _lib = None
+
+
+_CSRC = os.path.join(os.path.dirname(_HERE), "csrc")
+_HEADER = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "fs2_hip.h")
+
+
+def source_hash():
+    """SHA-256 (first 16 hex digits) of the library's sources in this tree, in the Makefile's
+    HASH_SRCS order (csrc/*.hip by name, csrc/fs2_common.h, include/fs2_hip.h); None when the
+    sources are not present."""
+    import hashlib
+    names = sorted(f for f in os.listdir(_CSRC) if f.endswith(".hip")) if os.path.isdir(_CSRC) else []
+    files = [os.path.join(_CSRC, f) for f in names] + [os.path.join(_CSRC, "fs2_common.h"), _HEADER]
+    if not names or not all(os.path.exists(f) for f in files):
+        return None
+    h = hashlib.sha256()
+    for f in files:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
 
 
 def load(path=None):
@@ -187,6 +208,11 @@ def load(path=None):
         fn.argtypes = args
     if missing:
         raise NativeLibraryError(f"libfs2_hip.so is missing symbols: {missing}")
+    built, tree = lib.fs2_source_hash().decode(), source_hash()
+    if tree is not None and built != tree:
+        raise NativeLibraryError(
+            f"{p} was built from other sources (hash {built}, this tree's csrc {tree}): rebuild "
+            f"it with `python -c 'import __graft_entry__ as g; g.build()'`")
     if path is None:
         _lib = lib
     return lib

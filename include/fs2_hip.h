@@ -413,6 +413,10 @@ int fs2_cast(const void* src, int src_dtype, void* dst, int dst_dtype, int64_t n
  * it 0.  Stream-ordered. */
 int fs2_set_dropout_seed(uint32_t seed_base, void* stream);
 const char* fs2_version(void);
+/* first 16 hex digits of the SHA-256 of the sources the library was built from (csrc/*.hip
+ * in name order, csrc/fs2_common.h, this header): fastspeech2/_native.py refuses a library
+ * whose hash differs from the tree's sources (a stale build)                                */
+const char* fs2_source_hash(void);
 
 #ifdef __cplusplus
 }

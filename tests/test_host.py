@@ -35,6 +35,19 @@ def test_library_exports_every_declared_symbol():
     assert lib.fs2_version().startswith(b"fs2_hip")
 
 
+def test_library_built_from_this_tree_and_stale_build_refused(monkeypatch):
+    """fs2_source_hash (Makefile buildinfo) equals the hash of the tree's csrc + header, and
+    a library whose hash differs from the tree's is refused at load (no stale build runs)."""
+    from fastspeech2 import _native
+    lib = _native.load()
+    tree = _native.source_hash()
+    assert tree is not None and len(tree) == 16
+    assert lib.fs2_source_hash().decode() == tree
+    monkeypatch.setattr(_native, "source_hash", lambda: "0" * 16)
+    with pytest.raises(_native.NativeLibraryError, match="other sources"):
+        _native.load(_native.LIB_PATH)
+
+
 def test_gemm_host_validation_rejects_bad_args():
     from fastspeech2 import _native as N
     lib = N.load()
