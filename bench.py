@@ -344,12 +344,18 @@ def main():
     if args.plumbing_check:
         plumbing_check(world, rank, local)
         return
-    if local >= torch.cuda.device_count():
+    # FS2_BENCH_REHEARSE=1 under torch.distributed.run: every rank on GPU 0 over gloo -- a
+    # rehearsal of the N > 1 code path (launcher, bucketed gradient all-reduce, barriers,
+    # max-over-ranks timing, rank-0 line) on a one-GPU box; never a measurement
+    rehearse = world > 1 and os.environ.get("FS2_BENCH_REHEARSE") == "1"
+    if local >= torch.cuda.device_count() and not rehearse:
         print(f"bench.py: LOCAL_RANK {local} but only {torch.cuda.device_count()} GPU(s) "
               f"visible", file=sys.stderr)
         sys.exit(2)
-    torch.cuda.set_device(local)
-    if world > 1:
+    torch.cuda.set_device(0 if rehearse else local)
+    if rehearse:
+        dist.init_process_group("gloo")
+    elif world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     from fastspeech2 import load_config
     from fastspeech2.model import FastSpeech2
@@ -493,6 +499,8 @@ def main():
                           "persistent kernel holding one block per CU), so the duration includes "
                           "its wait for CUs (DESIGN.md 6.4 has the standalone time)"},
             "hip_graph": graphed,
+            **({"rehearsal": f"gloo, {world} ranks on one GPU: the N > 1 code path, NOT a "
+                             "measurement"} if rehearse else {}),
             "build": _build_record(),
             # the step-level roofline on VALID frames -- frames/s x the train FLOPs
             # of one mel frame at T_phon=200, T_mel=1000 (338.8 MFLOP at default dims) / peak

@@ -82,3 +82,25 @@ def test_bench_refuses_more_gpus_than_visible():
                        cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=240)
     assert r.returncode == 2
     assert "GPU(s) visible" in r.stderr
+
+
+@pytest.mark.gpu
+def test_bench_two_rank_path_rehearsed_on_one_gpu():
+    """GPU: the N > 1 bench path end to end -- torch.distributed.run, two ranks, the bucketed
+    gradient all-reduce, barriers, max-over-ranks timing and the rank-0 line -- with both ranks
+    on GPU 0 over gloo (FS2_BENCH_REHEARSE=1; RCCL needs one GPU per rank).  Not a
+    measurement: the line says so."""
+    e = _env()
+    e["FS2_BENCH_REHEARSE"] = "1"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={bench._free_port()}",
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--no-cpu-baseline", "--no-extractor", "--no-fp32-leg", "--no-config2-leg"]
+    r = subprocess.run(cmd, cwd=ROOT, env=e, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(line) == 1, r.stdout          # rank 0 only
+    d = json.loads(line[0])
+    assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 64
+    assert d["config"]["parallelism"] == "dp2" and "rehearsal" in d
+    assert d["value"] > 0 and d["build"]["library_source_hash"] == d["build"]["tree_source_hash"]
