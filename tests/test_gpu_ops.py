@@ -104,9 +104,10 @@ def test_gemm_batched_attention_shapes(cuda, dt, code, tol):
 
 
 @pytest.mark.parametrize("dt,code,tol", DT)
-@pytest.mark.parametrize("D", [384, 90, 80, 512])
+@pytest.mark.parametrize("D", [384, 90, 80, 512, 8, 64])
 def test_layernorm_fwd_bwd(cuda, dt, code, tol, D):
-    """D=384: 16-byte vector kernels; D=90: scalar kernels.  dcol = fused column sum of the
+    """D=384: 16-byte vector kernels; D=90: scalar kernels; bf16 D = 8 / 80 / 512: the rows
+    kernels' DPP row sums with 1 / 10 / 64 lanes holding data.  dcol = fused column sum of the
     emitted gradient (the bias gradient of the layer that produced s)."""
     from fastspeech2 import ops
     torch.manual_seed(2)
