@@ -518,7 +518,7 @@ template <int R, bool TANH, bool DPP>
 __global__ void __launch_bounds__(256) ln_bwd_rows_kernel(LnBwdP p, float* part, int npart,
                                                           int kind0) {
   constexpr int V = 8;
-  __shared__ float red[4][512];
+  __shared__ float red[3][4][512];   // [kind][wave][column]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int d0 = lane * V;
   const bool act = d0 < p.D;
@@ -613,17 +613,24 @@ __global__ void __launch_bounds__(256) ln_bwd_rows_kernel(LnBwdP p, float* part,
     }
   }
   if (!part) return;
-  for (int k = 0; k < npart; ++k) {
-    const int kind = kind0 + k;  // 0 gamma, 1 beta, 2 column sum
-    if (act) {
+  // every kind's wave partials into LDS, ONE barrier, then the block's npart partial rows in
+  // one contiguous pass (the same fixed-order sums as one barrier pair per kind)
+  if (act) {
 #pragma unroll
-      for (int e = 0; e < V; ++e) red[wave][d0 + e] = kind == 0 ? pg[e] : (kind == 1 ? pb[e] : pc[e]);
+    for (int k = 0; k < 3; ++k) {
+      if (k < npart) {
+        const int kind = kind0 + k;  // 0 gamma, 1 beta, 2 column sum
+#pragma unroll
+        for (int e = 0; e < V; ++e)
+          red[k][wave][d0 + e] = kind == 0 ? pg[e] : (kind == 1 ? pb[e] : pc[e]);
+      }
     }
-    __syncthreads();
-    for (int d = threadIdx.x; d < p.D; d += 256)
-      part[((long)blockIdx.x * npart + k) * p.D + d] =
-          (red[0][d] + red[1][d]) + (red[2][d] + red[3][d]);
-    __syncthreads();
+  }
+  __syncthreads();
+  float* prow = part + (long)blockIdx.x * npart * p.D;
+  for (int i = threadIdx.x; i < npart * p.D; i += 256) {
+    const int k = i / p.D, d = i - k * p.D;
+    prow[i] = (red[k][0][d] + red[k][1][d]) + (red[k][2][d] + red[k][3][d]);
   }
 }
 

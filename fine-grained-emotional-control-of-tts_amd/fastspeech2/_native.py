@@ -209,7 +209,8 @@ def load(path=None):
     if missing:
         raise NativeLibraryError(f"libfs2_hip.so is missing symbols: {missing}")
     built, tree = lib.fs2_source_hash().decode(), source_hash()
-    if tree is not None and built != tree:
+    # FS2_LIB_OTHER_SOURCES=1: a deliberately older build (tools/ab_lib.sh's A arm)
+    if tree is not None and built != tree and os.environ.get("FS2_LIB_OTHER_SOURCES") != "1":
         raise NativeLibraryError(
             f"{p} was built from other sources (hash {built}, this tree's csrc {tree}): rebuild "
             f"it with `python -c 'import __graft_entry__ as g; g.build()'`")

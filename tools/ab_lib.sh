@@ -6,7 +6,7 @@ cd ${GRAFT_REPO_ROOT:-$(pwd)}
 L=$(pwd)/fine-grained-emotional-control-of-tts_amd/fastspeech2
 BA="--no-cpu-baseline --no-extractor --no-fp32-leg --no-config2-leg"
 for i in $(seq ${1:-3}); do
-  FS2_HIP_LIB=$L/libfs2_hip_base.so timeout -k 10 200 python -u bench.py $BA 2>/dev/null > /tmp/abl_A.json || exit 1
+  FS2_LIB_OTHER_SOURCES=1 FS2_HIP_LIB=$L/libfs2_hip_base.so timeout -k 10 200 python -u bench.py $BA 2>/dev/null > /tmp/abl_A.json || exit 1
   timeout -k 10 200 python -u bench.py $BA 2>/dev/null > /tmp/abl_B.json || exit 1
   python -c "import json; a=json.load(open('/tmp/abl_A.json')); b=json.load(open('/tmp/abl_B.json')); k=lambda d: ' '.join('%s=%.1f' % (n.split('.')[0][9:] + n.split('.')[1][:3], v * 1e3) for n, v in d.get('kernel_ms', {}).items()); print('A', round(a['ms_per_step'], 3), k(a), '| B', round(b['ms_per_step'], 3), k(b))"
 done
